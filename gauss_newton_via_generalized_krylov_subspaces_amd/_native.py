@@ -1,0 +1,198 @@
+"""ctypes binding of libgnk.so (include/gnk.h) and the HIP kernel backend.
+
+The solver talks to a *backend* object whose methods mirror the C-ABI one to one
+and take torch tensors.  ``HipBackend`` is the only backend the product uses; if
+the library is missing or no GPU is visible it raises -- there is no CPU
+fallback anywhere in the package.  (The test suite injects its own NumPy
+backend to exercise the multi-rank host logic on CPU with gloo; that backend
+lives in tests/ and is never importable from here.)
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("GNK_LIB", os.path.join(_HERE, "libgnk.so"))
+GHOST = 2  # GNK_GHOST_ROWS
+
+_c_int, _c_i64, _c_dbl, _c_vp = ctypes.c_int, ctypes.c_int64, ctypes.c_double, ctypes.c_void_p
+
+# name -> (restype, argtypes); exactly the declarations of include/gnk.h
+SIGNATURES = {
+    "gnk_abi_version": (_c_int, []),
+    "gnk_ctx_create": (_c_int, [_c_int, ctypes.POINTER(_c_vp)]),
+    "gnk_ctx_destroy": (None, [_c_vp]),
+    "gnk_last_error": (ctypes.c_char_p, [_c_vp]),
+    "gnk_set_stream": (_c_int, [_c_vp, _c_vp]),
+    "gnk_set_bratu": (_c_int, [_c_vp, _c_i64, _c_i64, _c_i64, _c_dbl, _c_dbl, _c_dbl]),
+    "gnk_slab_len": (_c_i64, [_c_vp]),
+    "gnk_bratu_jvp": (_c_int, [_c_vp, _c_vp, _c_vp, _c_vp]),
+    "gnk_bratu_vjp": (_c_int, [_c_vp, _c_vp, _c_vp, _c_vp]),
+    "gnk_bratu_forward": (_c_int, [_c_vp, _c_vp, _c_vp]),
+    "gnk_bratu_residual": (_c_int, [_c_vp, _c_vp, _c_vp, _c_vp, _c_vp]),
+    "gnk_bratu_diag_jtj": (_c_int, [_c_vp, _c_vp, _c_vp, _c_int]),
+    "gnk_bratu_jdiag": (_c_int, [_c_vp, _c_vp, _c_vp]),
+    "gnk_basis_gemv": (_c_int, [_c_vp, _c_vp, _c_i64, _c_int, _c_vp, _c_vp]),
+    "gnk_vjp_gemv_t": (_c_int, [_c_vp, _c_vp, _c_vp, _c_vp, _c_i64, _c_int, _c_vp, _c_vp]),
+    "gnk_cgs_update": (_c_int, [_c_vp, _c_vp, _c_i64, _c_int, _c_vp, _c_vp, _c_vp]),
+    "gnk_vec_stats": (_c_int, [_c_vp, _c_vp, _c_vp]),
+    "gnk_vec_div": (_c_int, [_c_vp, _c_vp, _c_dbl, _c_vp, _c_int]),
+    "gnk_vec_axpy": (_c_int, [_c_vp, _c_vp, _c_dbl, _c_vp, _c_vp, _c_int]),
+    "gnk_gram_padded_dim": (_c_int, [_c_int, _c_int]),
+    "gnk_gram": (_c_int, [_c_vp, _c_vp, _c_vp, _c_i64, _c_int, _c_vp, _c_i64, _c_vp, _c_vp]),
+    "gnk_cg_normal_matvec": (_c_int, [_c_vp, _c_vp, _c_vp, _c_vp, _c_vp]),
+    "gnk_cg_update_xr": (_c_int, [_c_vp, _c_dbl, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp]),
+    "gnk_cg_update_p": (_c_int, [_c_vp, _c_dbl, _c_int, _c_vp, _c_vp]),
+    "gnk_probe_mfma_f64": (_c_int, [_c_vp, _c_vp, _c_int, _c_int]),
+}
+
+_LIB = None
+
+
+class NativeLibraryError(RuntimeError):
+    pass
+
+
+def load_library(path: str = LIB_PATH):
+    """Load libgnk.so and bind every symbol of include/gnk.h (raises if any is missing)."""
+    global _LIB
+    if _LIB is not None and path == LIB_PATH:
+        return _LIB
+    if not os.path.exists(path):
+        raise NativeLibraryError(
+            f"libgnk.so not found at {path}: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
+            "or `make -C gauss_newton_via_generalized_krylov_subspaces_amd/csrc`")
+    lib = ctypes.CDLL(path)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)  # AttributeError = missing export
+        fn.restype = res
+        fn.argtypes = args
+    if lib.gnk_abi_version() != 1:
+        raise NativeLibraryError("libgnk.so ABI version mismatch")
+    if path == LIB_PATH:
+        _LIB = lib
+    return lib
+
+
+def _p(t):
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+class HipBackend:
+    """One gnk_ctx on one GPU; every method enqueues on torch's current stream."""
+
+    def __init__(self, device: torch.device):
+        if not torch.cuda.is_available():
+            raise NativeLibraryError("no ROCm GPU visible: the GNK hot path runs only on MI355X (gfx950)")
+        self.lib = load_library()
+        self.device = torch.device(device)
+        idx = self.device.index if self.device.index is not None else torch.cuda.current_device()
+        self.device = torch.device("cuda", idx)
+        ctx = ctypes.c_void_p()
+        with torch.cuda.device(idx):
+            rc = self.lib.gnk_ctx_create(idx, ctypes.byref(ctx))
+        if rc != 0:
+            raise NativeLibraryError(f"gnk_ctx_create failed ({rc})")
+        self.ctx = ctx
+        self._stream = None
+
+    def __del__(self):
+        try:
+            if getattr(self, "ctx", None) and self.lib is not None:
+                self.lib.gnk_ctx_destroy(self.ctx)
+                self.ctx = None
+        except Exception:
+            pass
+
+    def _sync_stream(self):
+        s = torch.cuda.current_stream(self.device).cuda_stream
+        if s != self._stream:
+            self._chk(self.lib.gnk_set_stream(self.ctx, ctypes.c_void_p(s)), "set_stream")
+            self._stream = s
+
+    def _chk(self, rc, what):
+        if rc != 0:
+            msg = self.lib.gnk_last_error(self.ctx)
+            raise RuntimeError(f"libgnk {what} failed ({rc}): {msg.decode() if msg else ''}")
+
+    def _call(self, name, *args):
+        self._sync_stream()
+        self._chk(getattr(self.lib, name)(self.ctx, *args), name)
+
+    # --- problem ---------------------------------------------------------------
+    def set_bratu(self, N, row0, nrows, h, alpha, lam):
+        self._chk(self.lib.gnk_set_bratu(self.ctx, N, row0, nrows, float(h), float(alpha), float(lam)), "set_bratu")
+
+    def slab_len(self):
+        return int(self.lib.gnk_slab_len(self.ctx))
+
+    def empty(self, *shape):
+        return torch.empty(*shape, dtype=torch.float64, device=self.device)
+
+    def zeros(self, *shape):
+        return torch.zeros(*shape, dtype=torch.float64, device=self.device)
+
+    def to_device(self, a):
+        return torch.as_tensor(a, dtype=torch.float64).to(self.device)
+
+    # --- operator ----------------------------------------------------------------
+    def jvp(self, u, v, out):
+        self._call("gnk_bratu_jvp", _p(u), _p(v), _p(out))
+
+    def vjp(self, u, w, out):
+        self._call("gnk_bratu_vjp", _p(u), _p(w), _p(out))
+
+    def forward(self, x, F):
+        self._call("gnk_bratu_forward", _p(x), _p(F))
+
+    def residual(self, x, y, r, norm2):
+        self._call("gnk_bratu_residual", _p(x), _p(y), _p(r), _p(norm2))
+
+    def diag_jtj(self, u, out, reciprocal=False):
+        self._call("gnk_bratu_diag_jtj", _p(u), _p(out), int(bool(reciprocal)))
+
+    def jdiag(self, u, d):
+        self._call("gnk_bratu_jdiag", _p(u), _p(d))
+
+    # --- basis -------------------------------------------------------------------
+    def gemv(self, V, k, c, x):
+        self._call("gnk_basis_gemv", _p(V), V.stride(0), int(k), _p(c), _p(x))
+
+    def vjp_gemv_t(self, u, r, V, k, g, h):
+        ldv = V.stride(0) if V is not None else 0
+        self._call("gnk_vjp_gemv_t", _p(u), _p(r), _p(V), ldv, int(k), _p(g), _p(h))
+
+    def cgs_update(self, V, k, h, g, stats):
+        self._call("gnk_cgs_update", _p(V), V.stride(0), int(k), _p(h), _p(g), _p(stats))
+
+    def vec_stats(self, x, stats):
+        self._call("gnk_vec_stats", _p(x), _p(stats))
+
+    def vec_div(self, src, denom, dst, full_slab):
+        self._call("gnk_vec_div", _p(src), float(denom), _p(dst), int(bool(full_slab)))
+
+    def vec_axpy(self, x, alpha, d, out, full_slab):
+        self._call("gnk_vec_axpy", _p(x), float(alpha), _p(d), _p(out), int(bool(full_slab)))
+
+    def gram_dim(self, k, with_r):
+        return int(self.lib.gnk_gram_padded_dim(int(k), int(bool(with_r))))
+
+    def gram(self, u, V, k, rinv, r, G):
+        kp = self.gram_dim(k, r is not None)
+        self._call("gnk_gram", _p(u), _p(V), V.stride(0), int(k), _p(rinv), kp, _p(r), _p(G))
+
+    # --- CG ------------------------------------------------------------------------
+    def cg_matvec(self, d, p, q, pq):
+        self._call("gnk_cg_normal_matvec", _p(d), _p(p), _p(q), _p(pq))
+
+    def cg_update_xr(self, alpha, p, q, x, r, dinv, z, out):
+        self._call("gnk_cg_update_xr", float(alpha), _p(p), _p(q), _p(x), _p(r), _p(dinv), _p(z), _p(out))
+
+    def cg_update_p(self, beta, first, z, p):
+        self._call("gnk_cg_update_p", float(beta), int(bool(first)), _p(z), _p(p))
+
+    def probe_mfma(self, out, blocks, iters):
+        self._call("gnk_probe_mfma_f64", _p(out), int(blocks), int(iters))

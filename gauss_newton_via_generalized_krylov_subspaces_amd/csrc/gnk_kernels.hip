@@ -1,0 +1,1015 @@
+// gnk_kernels.hip -- gfx950 (MI355X / CDNA4) kernels + C-ABI for the
+// generalized-Krylov Gauss-Newton hot path on the Bratu problem.
+//
+// Reference algorithm: mariusbaehr/gauss_newton_via_generalized_krylov_subspaces
+//   krylow.py:30-73            basis start / x / update (CGS1)         -> gemv, vjp_gemv_t, cgs_update, vec_div
+//   gauss_newton_krylow.py:16-36  LAPACK QR of -J@V + q.T@y           -> gram (CholeskyQR2 on fp64 MFMA)
+//   armijo_goldstein.py:49-58  sum(res**2) per trial                  -> residual (fused norm)
+//   bratu_pde_problem.py:76-96 F(u), CSR Jacobian                     -> matrix-free stencils
+//   gauss_newton.py:11-60      scipy cg on A.T A                       -> cg_* kernels
+//
+// Layout: "slab vectors" of (nrows + 2*GHOST) * N doubles, row-major over the
+// grid's x index (flat = jx*N + iy), owned rows at offset GHOST*N (gnk.h).
+// Every stencil sum accumulates from 0 in scipy's CSR column order
+// (i-N, i-1, i, i+1, i+N); the file is compiled with -ffp-contract=off so
+// products and sums round like the reference's sparsetools loops.
+//
+// Reductions are two-stage and deterministic: per-block partials in the
+// context's scratch arena, then one block sums them in block order.
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+#include <string>
+
+#include "../../include/gnk.h"
+
+#define G GNK_GHOST_ROWS
+
+namespace {
+
+constexpr int BLOCK = 256;
+constexpr int MAX_RED_BLOCKS = 4096;     // cap on per-block partials of a reduction
+constexpr int KC = 32;                   // columns per chunk in V^T g
+constexpr int PPW = 10;                  // Gram accumulator tiles per wave
+constexpr size_t SCRATCH_DOUBLES = size_t(16) << 20;   // 128 MiB arena
+
+typedef double d2 __attribute__((ext_vector_type(2)));
+typedef double d4 __attribute__((ext_vector_type(4)));
+
+struct Geo {
+  int64_t N;      // row length == number of global rows (square grid)
+  int64_t row0;   // global row of the first owned row
+  int64_t nrows;  // owned rows
+};
+
+// Coefficients of the CSR entries (ref:bratu_pde_problem.py:43-67, 92-96)
+struct Coef {
+  double hm2;         // h^-2            (= -L off-diagonal)
+  double l_off;       // -1 * h^-2
+  double l_diag;      // 4 * h^-2
+  double dx_diag;     // ALPHA * (-h^-1)
+  double dx_up;       // ALPHA * (+h^-1)
+  double j_lin_diag;  // l_diag + dx_diag      (L + ALPHA D_x) diagonal
+  double j_lin_up;    // l_off + dx_up         (L + ALPHA D_x) at column i+N
+  double lam;
+  int lam_zero;
+};
+
+__device__ __forceinline__ double jdiag(const Coef& c, double u) {
+  // diagonal of L + ALPHA D_x + LAMBDA diag(exp u) (ref:bratu_pde_problem.py:92-96)
+  return c.lam_zero ? c.j_lin_diag : c.j_lin_diag + c.lam * exp(u);
+}
+
+// J v at one point: J = -(...), CSR row order i-N, i-1, i, i+1, i+N
+__device__ __forceinline__ double jvp_pt(const Coef& c, double d, double vn, double vw, bool hw,
+                                         double vc, double ve, bool he, double vs) {
+  double s = 0.0 + c.hm2 * vn;
+  if (hw) s = s + c.hm2 * vw;
+  s = s + (-d) * vc;
+  if (he) s = s + c.hm2 * ve;
+  s = s + (-c.j_lin_up) * vs;
+  return s;
+}
+
+// J^T w at one point: csc_matvec order (source rows ascending)
+__device__ __forceinline__ double vjp_pt(const Coef& c, double d, double wn, double ww, bool hw,
+                                         double wc, double we, bool he, double ws) {
+  double s = 0.0 + (-c.j_lin_up) * wn;
+  if (hw) s = s + c.hm2 * ww;
+  s = s + (-d) * wc;
+  if (he) s = s + c.hm2 * we;
+  s = s + c.hm2 * ws;
+  return s;
+}
+
+// pde_operator(x) at one point: (L x + (ALPHA D_x) x) + LAMBDA exp(x)
+__device__ __forceinline__ double fwd_pt(const Coef& c, double xn, double xw, bool hw, double xc,
+                                         double xe, bool he, double xs) {
+  double l = 0.0 + c.l_off * xn;
+  if (hw) l = l + c.l_off * xw;
+  l = l + c.l_diag * xc;
+  if (he) l = l + c.l_off * xe;
+  l = l + c.l_off * xs;
+  double dx = 0.0 + c.dx_diag * xc;
+  dx = dx + c.dx_up * xs;
+  double f = l + dx;
+  if (!c.lam_zero) f = f + c.lam * exp(xc);
+  return f;
+}
+
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+
+__device__ __forceinline__ double nan_max(double a, double b) {
+  // max that propagates NaN (np.allclose never calls a NaN close)
+  return (b > a || b != b) ? b : a;
+}
+
+__device__ __forceinline__ double wave_max(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = nan_max(v, __shfl_xor(v, o));
+  return v;
+}
+
+// block-wide sum of `n` per-thread values, result written by thread 0..n-1 into out[0..n)
+template <int NV>
+__device__ __forceinline__ void block_sum_store(double (&v)[NV], int n, double* out, double* sh) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+  for (int j = 0; j < NV; ++j) {
+    if (j < n) {
+      double s = wave_sum(v[j]);
+      if (lane == 0) sh[wave * NV + j] = s;
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x < n) {
+    double s = sh[threadIdx.x];
+    for (int w = 1; w < BLOCK / 64; ++w) s += sh[w * NV + threadIdx.x];
+    out[threadIdx.x] = s;
+  }
+}
+
+// ---------------------------------------------------------------- row-tiled launch geometry
+// grid.x covers one row (VEC elements per thread), grid.y strides over rows.
+struct RowLaunch {
+  dim3 grid;
+  int64_t lr0, nlr;  // local row range [lr0, lr0 + nlr)
+};
+
+// Element loop helper: for local row lr and element iy of a row.
+#define ROW_LOOP_BEGIN(VEC)                                                          \
+  const int64_t N = geo.N;                                                           \
+  const int64_t iy = (int64_t(blockIdx.x) * BLOCK + threadIdx.x) * (VEC);           \
+  for (int64_t lr = lr0 + blockIdx.y; lr < lr0 + nlr; lr += gridDim.y) {             \
+    if (iy >= N) continue;                                                           \
+    const int64_t li = lr * N + iy;
+
+#define ROW_LOOP_END }
+
+// ---------------------------------------------------------------- operator kernels
+template <int VEC>
+__global__ __launch_bounds__(BLOCK) void k_jvp(const double* __restrict__ u, const double* __restrict__ v,
+                                               double* __restrict__ out, Geo geo, Coef c, int64_t lr0,
+                                               int64_t nlr, int transpose) {
+  ROW_LOOP_BEGIN(VEC)
+#pragma unroll
+  for (int q = 0; q < VEC; ++q) {
+    const int64_t i = li + q;
+    const int64_t y = iy + q;
+    if (y >= N) break;
+    const bool hw = y > 0, he = y < N - 1;
+    const double d = jdiag(c, u[i]);
+    const double vn = v[i - N], vs = v[i + N], vc = v[i];
+    const double vw = hw ? v[i - 1] : 0.0, ve = he ? v[i + 1] : 0.0;
+    out[i] = transpose ? vjp_pt(c, d, vn, vw, hw, vc, ve, he, vs) : jvp_pt(c, d, vn, vw, hw, vc, ve, he, vs);
+  }
+  ROW_LOOP_END
+}
+
+template <int VEC>
+__global__ __launch_bounds__(BLOCK) void k_forward(const double* __restrict__ x, const double* __restrict__ y,
+                                                   double* __restrict__ out, Geo geo, Coef c, int64_t lr0,
+                                                   int64_t nlr, double* __restrict__ partial) {
+  // out = pde_operator(x) (y == nullptr) or y - pde_operator(x); partial: sum out^2 over owned rows
+  __shared__ double sh[BLOCK / 64];
+  double acc[1] = {0.0};
+  ROW_LOOP_BEGIN(VEC)
+  const bool owned = lr >= G && lr < G + geo.nrows;
+#pragma unroll
+  for (int q = 0; q < VEC; ++q) {
+    const int64_t i = li + q;
+    const int64_t yy = iy + q;
+    if (yy >= N) break;
+    const bool hw = yy > 0, he = yy < N - 1;
+    const double xw = hw ? x[i - 1] : 0.0, xe = he ? x[i + 1] : 0.0;
+    const double f = fwd_pt(c, x[i - N], xw, hw, x[i], xe, he, x[i + N]);
+    const double r = y ? y[i] - f : f;
+    out[i] = r;
+    if (owned) acc[0] += r * r;
+  }
+  ROW_LOOP_END
+  if (partial) block_sum_store<1>(acc, 1, partial + (blockIdx.y * gridDim.x + blockIdx.x), sh);
+}
+
+template <int VEC>
+__global__ __launch_bounds__(BLOCK) void k_diag_jtj(const double* __restrict__ u, double* __restrict__ out,
+                                                    Geo geo, Coef c, int64_t lr0, int64_t nlr, int recip) {
+  ROW_LOOP_BEGIN(VEC)
+  const int64_t grow = geo.row0 + (lr - G);
+#pragma unroll
+  for (int q = 0; q < VEC; ++q) {
+    const int64_t i = li + q;
+    const int64_t yy = iy + q;
+    if (yy >= N) break;
+    const double d = jdiag(c, u[i]);
+    const double o2 = c.l_off * c.l_off;
+    const double up = grow > 0 ? c.j_lin_up * c.j_lin_up : 0.0;
+    const double west = yy > 0 ? o2 : 0.0;
+    const double east = yy < N - 1 ? o2 : 0.0;
+    const double south = grow < N - 1 ? o2 : 0.0;
+    const double v = (((up + west) + d * d) + east) + south;
+    out[i] = recip ? 1.0 / v : v;
+  }
+  ROW_LOOP_END
+}
+
+// ---------------------------------------------------------------- basis kernels
+// x = V[:, :k] @ c
+template <int VEC>
+__global__ __launch_bounds__(BLOCK) void k_gemv(const double* __restrict__ V, int64_t ldv, int k,
+                                                const double* __restrict__ cvec, double* __restrict__ x,
+                                                Geo geo, int64_t lr0, int64_t nlr) {
+  ROW_LOOP_BEGIN(VEC)
+  if (VEC == 2 && iy + 1 < N) {
+    d2 acc = {0.0, 0.0};
+    for (int j = 0; j < k; ++j) {
+      const d2 vv = *reinterpret_cast<const d2*>(V + j * ldv + li);
+      const double cj = cvec[j];
+      acc.x = acc.x + vv.x * cj;
+      acc.y = acc.y + vv.y * cj;
+    }
+    *reinterpret_cast<d2*>(x + li) = acc;
+  } else {
+    for (int q = 0; q < VEC && iy + q < N; ++q) {
+      double acc = 0.0;
+      for (int j = 0; j < k; ++j) acc = acc + V[j * ldv + li + q] * cvec[j];
+      x[li + q] = acc;
+    }
+  }
+  ROW_LOOP_END
+}
+
+// g = -(J^T r) on owned rows (chunk 0 stores it), h[j0 + j] partial = V_j . g
+template <int VEC>
+__global__ __launch_bounds__(BLOCK) void k_vjp_gemv_t(const double* __restrict__ u, const double* __restrict__ r,
+                                                      const double* __restrict__ V, int64_t ldv, int k,
+                                                      double* __restrict__ g, Geo geo, Coef c, int64_t lr0,
+                                                      int64_t nlr, double* __restrict__ partial) {
+  __shared__ double sh[(BLOCK / 64) * KC];
+  const int j0 = blockIdx.z * KC;
+  const int kc = min(KC, k - j0);
+  double acc[KC];
+#pragma unroll
+  for (int j = 0; j < KC; ++j) acc[j] = 0.0;
+  ROW_LOOP_BEGIN(VEC)
+#pragma unroll
+  for (int q = 0; q < VEC; ++q) {
+    const int64_t i = li + q;
+    const int64_t yy = iy + q;
+    if (yy >= N) break;
+    const bool hw = yy > 0, he = yy < N - 1;
+    const double d = jdiag(c, u[i]);
+    const double rw = hw ? r[i - 1] : 0.0, re = he ? r[i + 1] : 0.0;
+    const double gi = -vjp_pt(c, d, r[i - N], rw, hw, r[i], re, he, r[i + N]);
+    if (blockIdx.z == 0) g[i] = gi;
+#pragma unroll
+    for (int j = 0; j < KC; ++j)
+      if (j < kc) acc[j] = acc[j] + V[(j0 + j) * ldv + i] * gi;
+  }
+  ROW_LOOP_END
+  const int nblk = gridDim.x * gridDim.y;
+  block_sum_store<KC>(acc, kc, partial + (size_t(blockIdx.z) * nblk + blockIdx.y * gridDim.x + blockIdx.x) * KC, sh);
+}
+
+// g -= V[:, :k] @ h ; partial {sum g^2, max|g|}
+template <int VEC>
+__global__ __launch_bounds__(BLOCK) void k_cgs(const double* __restrict__ V, int64_t ldv, int k,
+                                               const double* __restrict__ h, double* __restrict__ g, Geo geo,
+                                               int64_t lr0, int64_t nlr, double* __restrict__ partial) {
+  __shared__ double sh[BLOCK / 64][2];
+  double ss = 0.0, mx = 0.0;
+  ROW_LOOP_BEGIN(VEC)
+  if (VEC == 2 && iy + 1 < N) {
+    d2 s = {0.0, 0.0};
+    for (int j = 0; j < k; ++j) {
+      const d2 vv = *reinterpret_cast<const d2*>(V + j * ldv + li);
+      const double hj = h[j];
+      s.x = s.x + vv.x * hj;
+      s.y = s.y + vv.y * hj;
+    }
+    d2 gg = *reinterpret_cast<const d2*>(g + li);
+    gg.x = gg.x - s.x;
+    gg.y = gg.y - s.y;
+    *reinterpret_cast<d2*>(g + li) = gg;
+    ss += gg.x * gg.x;
+    ss += gg.y * gg.y;
+    mx = nan_max(mx, fabs(gg.x));
+    mx = nan_max(mx, fabs(gg.y));
+  } else {
+    for (int q = 0; q < VEC && iy + q < N; ++q) {
+      double s = 0.0;
+      for (int j = 0; j < k; ++j) s = s + V[j * ldv + li + q] * h[j];
+      const double gi = g[li + q] - s;
+      g[li + q] = gi;
+      ss += gi * gi;
+      mx = nan_max(mx, fabs(gi));
+    }
+  }
+  ROW_LOOP_END
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  ss = wave_sum(ss);
+  mx = wave_max(mx);
+  if (lane == 0) { sh[wave][0] = ss; sh[wave][1] = mx; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double a = sh[0][0], b = sh[0][1];
+    for (int w = 1; w < BLOCK / 64; ++w) { a += sh[w][0]; b = nan_max(b, sh[w][1]); }
+    const size_t blk = blockIdx.y * gridDim.x + blockIdx.x;
+    partial[2 * blk] = a;
+    partial[2 * blk + 1] = b;
+  }
+}
+
+// {sum x^2, max |x|}
+template <int VEC>
+__global__ __launch_bounds__(BLOCK) void k_stats(const double* __restrict__ x, Geo geo, int64_t lr0, int64_t nlr,
+                                                 double* __restrict__ partial) {
+  __shared__ double sh[BLOCK / 64][2];
+  double ss = 0.0, mx = 0.0;
+  ROW_LOOP_BEGIN(VEC)
+  for (int q = 0; q < VEC && iy + q < N; ++q) {
+    const double xi = x[li + q];
+    ss += xi * xi;
+    mx = nan_max(mx, fabs(xi));
+  }
+  ROW_LOOP_END
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  ss = wave_sum(ss);
+  mx = wave_max(mx);
+  if (lane == 0) { sh[wave][0] = ss; sh[wave][1] = mx; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double a = sh[0][0], b = sh[0][1];
+    for (int w = 1; w < BLOCK / 64; ++w) { a += sh[w][0]; b = nan_max(b, sh[w][1]); }
+    const size_t blk = blockIdx.y * gridDim.x + blockIdx.x;
+    partial[2 * blk] = a;
+    partial[2 * blk + 1] = b;
+  }
+}
+
+template <int VEC>
+__global__ __launch_bounds__(BLOCK) void k_div(const double* __restrict__ src, double denom, double* __restrict__ dst,
+                                               Geo geo, int64_t lr0, int64_t nlr) {
+  ROW_LOOP_BEGIN(VEC)
+  for (int q = 0; q < VEC && iy + q < N; ++q) dst[li + q] = src[li + q] / denom;
+  ROW_LOOP_END
+}
+
+// out = x + (alpha * d): the two roundings of NumPy's `x + step_length * descent_direction`
+template <int VEC>
+__global__ __launch_bounds__(BLOCK) void k_axpy(const double* __restrict__ x, double alpha, const double* __restrict__ d,
+                                                double* __restrict__ out, Geo geo, int64_t lr0, int64_t nlr) {
+  ROW_LOOP_BEGIN(VEC)
+  for (int q = 0; q < VEC && iy + q < N; ++q) {
+    const double td = alpha * d[li + q];
+    out[li + q] = x[li + q] + td;
+  }
+  ROW_LOOP_END
+}
+
+// ---------------------------------------------------------------- CG kernels
+// d = diag of (L + ALPHA D_x + LAMBDA diag e^u), constant during a CG solve
+template <int VEC>
+__global__ __launch_bounds__(BLOCK) void k_jdiag(const double* __restrict__ u, double* __restrict__ d, Geo geo,
+                                                 Coef c, int64_t lr0, int64_t nlr) {
+  ROW_LOOP_BEGIN(VEC)
+  for (int q = 0; q < VEC && iy + q < N; ++q) d[li + q] = jdiag(c, u[li + q]);
+  ROW_LOOP_END
+}
+
+// (J p)_j for a point j of row gj (outside the domain -> 0)
+__device__ __forceinline__ double tj(const Coef& c, const double* __restrict__ d, const double* __restrict__ p,
+                                     int64_t j, int64_t gj, int64_t jy, int64_t N) {
+  if (gj < 0 || gj >= N) return 0.0;
+  const bool hw = jy > 0, he = jy < N - 1;
+  const double pw = hw ? p[j - 1] : 0.0, pe = he ? p[j + 1] : 0.0;
+  return jvp_pt(c, d[j], p[j - N], pw, hw, p[j], pe, he, p[j + N]);
+}
+
+// q = J^T (J p), 13-point fused; identical arithmetic to t = J p followed by q = J^T t
+template <int VEC>
+__global__ __launch_bounds__(BLOCK) void k_cg_matvec(const double* __restrict__ d, const double* __restrict__ p,
+                                                     double* __restrict__ q, Geo geo, Coef c, int64_t lr0,
+                                                     int64_t nlr, double* __restrict__ partial) {
+  __shared__ double sh[BLOCK / 64];
+  double acc[1] = {0.0};
+  ROW_LOOP_BEGIN(VEC)
+  const int64_t gr = geo.row0 + (lr - G);
+#pragma unroll
+  for (int qq = 0; qq < VEC; ++qq) {
+    const int64_t i = li + qq;
+    const int64_t yy = iy + qq;
+    if (yy >= N) break;
+    const bool hw = yy > 0, he = yy < N - 1;
+    const double tn = tj(c, d, p, i - N, gr - 1, yy, N);
+    const double tw = hw ? tj(c, d, p, i - 1, gr, yy - 1, N) : 0.0;
+    const double tc = tj(c, d, p, i, gr, yy, N);
+    const double te = he ? tj(c, d, p, i + 1, gr, yy + 1, N) : 0.0;
+    const double ts = tj(c, d, p, i + N, gr + 1, yy, N);
+    const double qi = vjp_pt(c, d[i], tn, tw, hw, tc, te, he, ts);
+    q[i] = qi;
+    acc[0] += p[i] * qi;
+  }
+  ROW_LOOP_END
+  block_sum_store<1>(acc, 1, partial + (blockIdx.y * gridDim.x + blockIdx.x), sh);
+}
+
+template <int VEC>
+__global__ __launch_bounds__(BLOCK) void k_cg_xr(double alpha, const double* __restrict__ p,
+                                                 const double* __restrict__ q, double* __restrict__ x,
+                                                 double* __restrict__ r, const double* __restrict__ dinv,
+                                                 double* __restrict__ z, Geo geo, int64_t lr0, int64_t nlr,
+                                                 double* __restrict__ partial) {
+  __shared__ double sh[(BLOCK / 64) * 2];
+  double acc[2] = {0.0, 0.0};
+  ROW_LOOP_BEGIN(VEC)
+  for (int qq = 0; qq < VEC && iy + qq < N; ++qq) {
+    const int64_t i = li + qq;
+    x[i] = x[i] + alpha * p[i];
+    const double ri = r[i] - alpha * q[i];
+    r[i] = ri;
+    const double zi = dinv ? 0.0 + dinv[i] * ri : ri;
+    if (dinv) z[i] = zi;
+    acc[0] += ri * ri;
+    acc[1] += ri * zi;
+  }
+  ROW_LOOP_END
+  block_sum_store<2>(acc, 2, partial + 2 * (blockIdx.y * gridDim.x + blockIdx.x), sh);
+}
+
+template <int VEC>
+__global__ __launch_bounds__(BLOCK) void k_cg_p(double beta, int first, const double* __restrict__ z,
+                                                double* __restrict__ p, Geo geo, int64_t lr0, int64_t nlr) {
+  ROW_LOOP_BEGIN(VEC)
+  for (int qq = 0; qq < VEC && iy + qq < N; ++qq) {
+    const int64_t i = li + qq;
+    p[i] = first ? z[i] : p[i] * beta + z[i];
+  }
+  ROW_LOOP_END
+}
+
+// ---------------------------------------------------------------- deterministic partial reduction
+// out[j] = sum_b partial[b * stride + j], b ascending; mode 1 = max (NaN-propagating)
+__global__ __launch_bounds__(BLOCK) void k_reduce(const double* __restrict__ partial, int nblk, int len,
+                                                  int stride, const int* __restrict__ is_max, double* out) {
+  for (int j = blockIdx.x * BLOCK + threadIdx.x; j < len; j += gridDim.x * BLOCK) {
+    const bool mx = is_max ? is_max[j] != 0 : false;
+    double s = partial[j];
+    for (int b = 1; b < nblk; ++b) {
+      const double v = partial[size_t(b) * stride + j];
+      s = mx ? nan_max(s, v) : s + v;
+    }
+    out[j] = s;
+  }
+}
+
+// sum-over-chunks layout used by k_vjp_gemv_t: partial[(z * nblk + b) * KC + j]
+__global__ __launch_bounds__(BLOCK) void k_reduce_chunks(const double* __restrict__ partial, int nblk, int k,
+                                                         double* out) {
+  for (int jj = blockIdx.x * BLOCK + threadIdx.x; jj < k; jj += gridDim.x * BLOCK) {
+    const int z = jj / KC, j = jj % KC;
+    const double* p = partial + size_t(z) * nblk * KC + j;
+    double s = p[0];
+    for (int b = 1; b < nblk; ++b) s += p[size_t(b) * KC];
+    out[jj] = s;
+  }
+}
+
+// ---------------------------------------------------------------- Gram on fp64 MFMA
+// v_mfma_f64_16x16x4_f64:  C[16x16] += A[16x4] B[4x16];  lane l holds A[l&15][l>>4],
+// B[l>>4][l&15]; C/D reg i of lane l is C[(l>>4) + 4i][l&15] (cdna_hip_programming.md §3).
+// For a Gram tile (a, b) over 4 rows: A[i][kk] = W[row kk][16a + i], B[kk][j] = W[row kk][16b + j]
+// so lane l supplies W[row l>>4][16a + (l&15)] and W[row l>>4][16b + (l&15)].
+__device__ __forceinline__ d4 mfma64(double a, double b, d4 c) {
+  return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ void pair_ab(int p, int nb, int& a, int& b) {
+  a = 0;
+  int rem = p;
+  while (rem >= nb - a) { rem -= nb - a; ++a; }
+  b = a + rem;
+}
+
+// W tile rows [e0, e0 + T) in LDS as Wt[t * S + col] (S = KP + 1).
+// Pass 1 (rinv == nullptr): W = J V.  Pass 2: W = [J V | r] @ RinvAug (RinvAug kp x kp).
+// rowsplit = 1: each wave accumulates all P pair tiles over its quarter of the rows.
+// rowsplit = 0: blockIdx.y = pair group; wave w owns pairs grp*4*PPW + w*PPW + q over all rows.
+__global__ __launch_bounds__(BLOCK) void k_gram(const double* __restrict__ u, const double* __restrict__ V,
+                                                int64_t ldv, int k, const double* __restrict__ rinv,
+                                                const double* __restrict__ r, Geo geo, Coef c, int T, int logT,
+                                                int KP, int P, int rowsplit, int64_t ntiles,
+                                                double* __restrict__ partial) {
+  extern __shared__ __attribute__((aligned(16))) double lds[];
+  const int S = KP + 1;
+  double* Wt = lds;
+  double* dg = lds + T * S;
+  int* fl = reinterpret_cast<int*>(dg + T);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int nb = KP / 16;
+  const int64_t N = geo.N;
+  const int64_t nown = geo.nrows * N;
+  const int64_t base = int64_t(G) * N;
+
+  int pa[PPW], pb[PPW];
+  bool pv[PPW];
+#pragma unroll
+  for (int q = 0; q < PPW; ++q) {
+    const int p = rowsplit ? q : (blockIdx.y * 4 * PPW + wave * PPW + q);
+    pv[q] = rowsplit ? (q < P) : (p < P);
+    pair_ab(pv[q] ? p : 0, nb, pa[q], pb[q]);
+  }
+  d4 acc[PPW];
+#pragma unroll
+  for (int q = 0; q < PPW; ++q) acc[q] = d4{0.0, 0.0, 0.0, 0.0};
+
+  const int rq = rowsplit ? T / 4 : T;
+  const int rbeg = rowsplit ? wave * rq : 0;
+
+  for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const int64_t e0 = tile << logT;
+    for (int t = tid; t < T; t += BLOCK) {
+      const int64_t e = e0 + t;
+      int f = 0;
+      double dd = 0.0;
+      if (e < nown) {
+        const int64_t iy = e % N;
+        f = 4 | (iy > 0 ? 1 : 0) | (iy < N - 1 ? 2 : 0);
+        dd = jdiag(c, u[base + e]);
+      }
+      fl[t] = f;
+      dg[t] = dd;
+    }
+    __syncthreads();
+    const int ncol = KP;
+    for (int idx = tid; idx < T * ncol; idx += BLOCK) {
+      const int t = idx & (T - 1);
+      const int j = idx >> logT;
+      const int f = fl[t];
+      double w = 0.0;
+      if (f & 4) {
+        const int64_t i = base + e0 + t;
+        if (j < k) {
+          const double* v = V + j * ldv;
+          const bool hw = f & 1, he = f & 2;
+          const double vw = hw ? v[i - 1] : 0.0, ve = he ? v[i + 1] : 0.0;
+          w = jvp_pt(c, dg[t], v[i - N], vw, hw, v[i], ve, he, v[i + N]);
+        } else if (j == k && r) {
+          w = r[i];
+        }
+      }
+      Wt[t * S + j] = w;
+    }
+    __syncthreads();
+    if (rinv) {
+      // in-place W <- W @ RinvAug; column blocks descending so each block reads only
+      // not-yet-overwritten blocks a <= cb. Rows split over the 4 waves.
+      const int rq4 = T / 4;
+      for (int c16 = wave * rq4; c16 < (wave + 1) * rq4; c16 += 16) {
+        for (int cb = nb - 1; cb >= 0; --cb) {
+          d4 qv = d4{0.0, 0.0, 0.0, 0.0};
+          for (int ab = 0; ab <= cb; ++ab) {
+#pragma unroll
+            for (int ks = 0; ks < 4; ++ks) {
+              const int kk = ab * 16 + ks * 4 + (lane >> 4);
+              const double a = Wt[(c16 + (lane & 15)) * S + kk];
+              const double b = rinv[kk * KP + cb * 16 + (lane & 15)];
+              qv = mfma64(a, b, qv);
+            }
+          }
+#pragma unroll
+          for (int i = 0; i < 4; ++i) Wt[(c16 + (lane >> 4) + 4 * i) * S + cb * 16 + (lane & 15)] = qv[i];
+        }
+      }
+      __syncthreads();
+    }
+    for (int rr = rbeg; rr < rbeg + rq; rr += 4) {
+      const double* row = Wt + (rr + (lane >> 4)) * S + (lane & 15);
+#pragma unroll
+      for (int q = 0; q < PPW; ++q) {
+        if (pv[q]) acc[q] = mfma64(row[pa[q] * 16], row[pb[q] * 16], acc[q]);
+      }
+    }
+    __syncthreads();
+  }
+
+  // block partial: partial[((grp * gridDim.x + blockIdx.x) * PG + pair_local) * 256 + lane * 4 + i],
+  // PG = pairs per group (P when rowsplit, 4 * PPW otherwise)
+  const int PG = rowsplit ? P : 4 * PPW;
+  double* out = partial + (size_t(blockIdx.y) * gridDim.x + blockIdx.x) * size_t(PG) * 256;
+  if (rowsplit) {
+    // ((w0 + w1) + w2) + w3 through LDS (reuses the tile; P * 256 <= T * S checked on the host)
+    double* red = lds;
+    for (int w = 0; w < 4; ++w) {
+      if (wave == w) {
+#pragma unroll
+        for (int q = 0; q < PPW; ++q)
+          if (pv[q])
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+              double* dst = red + q * 256 + lane * 4 + i;
+              *dst = (w == 0) ? acc[q][i] : *dst + acc[q][i];
+            }
+      }
+      __syncthreads();
+    }
+    for (int idx = tid; idx < P * 256; idx += BLOCK) out[idx] = red[idx];
+  } else {
+#pragma unroll
+    for (int q = 0; q < PPW; ++q) {
+      if (pv[q]) {
+        const int pl = wave * PPW + q;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) out[size_t(pl) * 256 + lane * 4 + i] = acc[q][i];
+      }
+    }
+  }
+}
+
+// Sum Gram partials over blocks (block order) and scatter into G[KP][KP] (symmetric).
+__global__ __launch_bounds__(BLOCK) void k_gram_reduce(const double* __restrict__ partial, int nblk, int P,
+                                                       int rowsplit, int KP, double* __restrict__ Gout) {
+  const int nb = KP / 16;
+  const int PG = rowsplit ? P : 4 * PPW;
+  for (int idx = blockIdx.x * BLOCK + threadIdx.x; idx < P * 256; idx += gridDim.x * BLOCK) {
+    const int p = idx >> 8, li = idx & 255, lane = li >> 2, i = li & 3;
+    const int grp = p / PG, pl = p % PG;
+    const double* src = partial + (size_t(grp) * nblk * PG + pl) * 256 + li;
+    double s = src[0];
+    for (int b = 1; b < nblk; ++b) s += src[size_t(b) * PG * 256];
+    int a, bb;
+    pair_ab(p, nb, a, bb);
+    const int row = a * 16 + (lane >> 4) + 4 * i;
+    const int col = bb * 16 + (lane & 15);
+    if (a != bb || row <= col) {
+      Gout[row * KP + col] = s;
+      Gout[col * KP + row] = s;
+    }
+  }
+}
+
+// ---------------------------------------------------------------- probes (tooling)
+__global__ void k_probe_mfma(double* out, int iters) {
+  d4 c0 = {0, 0, 0, 0}, c1 = c0, c2 = c0, c3 = c0;
+  double a = 1.0 + threadIdx.x * 1e-9, b = 1.0 - threadIdx.x * 1e-9;
+  for (int i = 0; i < iters; ++i) {
+    c0 = mfma64(a, b, c0);
+    c1 = mfma64(b, a, c1);
+    c2 = mfma64(a, a, c2);
+    c3 = mfma64(b, b, c3);
+  }
+  const d4 s = c0 + c1 + c2 + c3;
+  if (s[0] == 12345.0) out[threadIdx.x] = s[1] + s[2] + s[3];
+}
+
+}  // namespace
+
+// ======================================================================== C-ABI
+struct gnk_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  Geo geo{0, 0, 0};
+  Coef coef{};
+  double* scratch = nullptr;
+  int num_cus = 256;
+  std::string err;
+};
+
+namespace {
+
+int fail(gnk_ctx* ctx, const std::string& msg, int code = -1) {
+  if (ctx) ctx->err = msg;
+  return code;
+}
+
+int check_launch(gnk_ctx* ctx, const char* what) {
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return fail(ctx, std::string(what) + ": " + hipGetErrorString(e), -2);
+  return 0;
+}
+
+bool ready(gnk_ctx* ctx) {
+  if (!ctx) return false;
+  if (ctx->geo.N <= 0) {
+    ctx->err = "gnk_set_bratu has not been called";
+    return false;
+  }
+  return true;
+}
+
+// launch geometry for local rows [lr0, lr0 + nlr), VEC elements per thread
+RowLaunch rows(const gnk_ctx* ctx, int64_t lr0, int64_t nlr, int vec, int cap_blocks = MAX_RED_BLOCKS) {
+  RowLaunch L;
+  const int64_t per_block = int64_t(BLOCK) * vec;
+  const int64_t bx = (ctx->geo.N + per_block - 1) / per_block;
+  int64_t by = std::max<int64_t>(1, cap_blocks / bx);
+  by = std::min<int64_t>(by, std::max<int64_t>(nlr, 1));
+  by = std::min<int64_t>(by, 65535);
+  L.grid = dim3(unsigned(bx), unsigned(by), 1);
+  L.lr0 = lr0;
+  L.nlr = nlr;
+  return L;
+}
+
+int vec_of(const gnk_ctx* ctx) { return (ctx->geo.N % 2 == 0) ? 2 : 1; }
+
+int64_t owned_lr0() { return G; }
+
+// local rows of the residual: owned +- 1 clipped to the domain
+void residual_rows(const gnk_ctx* ctx, int64_t& lr0, int64_t& nlr) {
+  const Geo& g = ctx->geo;
+  int64_t lo = G - 1, hi = G + g.nrows + 1;       // [lo, hi)
+  if (g.row0 == 0) lo = G;                        // global row -1 is outside
+  if (g.row0 + g.nrows >= g.N) hi = G + g.nrows;  // global row N is outside
+  lr0 = lo;
+  nlr = hi - lo;
+}
+
+int reduce(gnk_ctx* ctx, const double* partial, int nblk, int len, int stride, const int* is_max, double* out) {
+  hipLaunchKernelGGL(k_reduce, dim3((len + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, ctx->stream, partial, nblk, len,
+                     stride, is_max, out);
+  return check_launch(ctx, "reduce");
+}
+
+// device constant {0, 1} flags for {sum, max} reductions
+__device__ int d_sum_max_flags[2] = {0, 1};
+
+const int* sum_max_flags() {
+  void* p = nullptr;
+  (void)hipGetSymbolAddress(&p, HIP_SYMBOL(d_sum_max_flags));
+  return static_cast<const int*>(p);
+}
+
+}  // namespace
+
+extern "C" {
+
+int gnk_abi_version(void) { return GNK_ABI_VERSION; }
+
+int gnk_ctx_create(int device, gnk_ctx** out) {
+  if (!out) return -1;
+  *out = nullptr;
+  hipError_t e = hipSetDevice(device);
+  if (e != hipSuccess) return -2;
+  auto* ctx = new gnk_ctx();
+  ctx->device = device;
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, device) == hipSuccess) ctx->num_cus = prop.multiProcessorCount;
+  e = hipMalloc(&ctx->scratch, SCRATCH_DOUBLES * sizeof(double));
+  if (e != hipSuccess) {
+    delete ctx;
+    return -3;
+  }
+  *out = ctx;
+  return 0;
+}
+
+void gnk_ctx_destroy(gnk_ctx* ctx) {
+  if (!ctx) return;
+  if (ctx->scratch) (void)hipFree(ctx->scratch);
+  delete ctx;
+}
+
+const char* gnk_last_error(const gnk_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+
+int gnk_set_stream(gnk_ctx* ctx, void* stream) {
+  if (!ctx) return -1;
+  ctx->stream = static_cast<hipStream_t>(stream);
+  return 0;
+}
+
+int gnk_set_bratu(gnk_ctx* ctx, int64_t N, int64_t row0, int64_t nrows, double h, double alpha, double lambda) {
+  if (!ctx) return -1;
+  if (N < 2 || nrows < 1 || row0 < 0 || row0 + nrows > N) return fail(ctx, "gnk_set_bratu: bad slab geometry");
+  if (nrows < G && nrows != N) return fail(ctx, "gnk_set_bratu: slab must own >= GNK_GHOST_ROWS rows");
+  ctx->geo = Geo{N, row0, nrows};
+  Coef c;
+  // identical float expressions to ref:bratu_pde_problem.py:58,67 (h ** -2, h ** -1)
+  const double hm2 = std::pow(h, -2.0);
+  const double hm1 = std::pow(h, -1.0);
+  c.hm2 = -(-1.0 * hm2);
+  c.l_off = -1.0 * hm2;
+  c.l_diag = 4.0 * hm2;
+  c.dx_diag = alpha * (-1.0 * hm1);
+  c.dx_up = alpha * (1.0 * hm1);
+  c.j_lin_diag = c.l_diag + c.dx_diag;
+  c.j_lin_up = c.l_off + c.dx_up;
+  c.lam = lambda;
+  c.lam_zero = (lambda == 0.0) ? 1 : 0;
+  ctx->coef = c;
+  return 0;
+}
+
+int64_t gnk_slab_len(const gnk_ctx* ctx) {
+  if (!ctx) return -1;
+  return (ctx->geo.nrows + 2 * G) * ctx->geo.N;
+}
+
+#define DISPATCH_VEC(ctx, KERNEL, L, SHMEM, ...)                                                     \
+  do {                                                                                              \
+    if (vec_of(ctx) == 2)                                                                           \
+      hipLaunchKernelGGL(KERNEL<2>, L.grid, dim3(BLOCK), SHMEM, ctx->stream, __VA_ARGS__);          \
+    else                                                                                            \
+      hipLaunchKernelGGL(KERNEL<1>, L.grid, dim3(BLOCK), SHMEM, ctx->stream, __VA_ARGS__);          \
+  } while (0)
+
+int gnk_bratu_jvp(gnk_ctx* ctx, const double* u, const double* v, double* out) {
+  if (!ready(ctx)) return -1;
+  RowLaunch L = rows(ctx, G, ctx->geo.nrows, vec_of(ctx), 1 << 30);
+  DISPATCH_VEC(ctx, k_jvp, L, 0, u, v, out, ctx->geo, ctx->coef, L.lr0, L.nlr, 0);
+  return check_launch(ctx, "bratu_jvp");
+}
+
+int gnk_bratu_vjp(gnk_ctx* ctx, const double* u, const double* w, double* out) {
+  if (!ready(ctx)) return -1;
+  RowLaunch L = rows(ctx, G, ctx->geo.nrows, vec_of(ctx), 1 << 30);
+  DISPATCH_VEC(ctx, k_jvp, L, 0, u, w, out, ctx->geo, ctx->coef, L.lr0, L.nlr, 1);
+  return check_launch(ctx, "bratu_vjp");
+}
+
+int gnk_bratu_forward(gnk_ctx* ctx, const double* x, double* F) {
+  if (!ready(ctx)) return -1;
+  RowLaunch L = rows(ctx, G, ctx->geo.nrows, vec_of(ctx), 1 << 30);
+  DISPATCH_VEC(ctx, k_forward, L, 0, x, (const double*)nullptr, F, ctx->geo, ctx->coef, L.lr0, L.nlr,
+               (double*)nullptr);
+  return check_launch(ctx, "bratu_forward");
+}
+
+int gnk_bratu_residual(gnk_ctx* ctx, const double* x, const double* y, double* r, double* norm2_out) {
+  if (!ready(ctx)) return -1;
+  if (!y) return fail(ctx, "bratu_residual: y is NULL");
+  int64_t lr0, nlr;
+  residual_rows(ctx, lr0, nlr);
+  RowLaunch L = rows(ctx, lr0, nlr, vec_of(ctx));
+  const int nblk = L.grid.x * L.grid.y;
+  DISPATCH_VEC(ctx, k_forward, L, 0, x, y, r, ctx->geo, ctx->coef, L.lr0, L.nlr, ctx->scratch);
+  int rc = check_launch(ctx, "bratu_residual");
+  if (rc) return rc;
+  if (norm2_out) return reduce(ctx, ctx->scratch, nblk, 1, 1, nullptr, norm2_out);
+  return 0;
+}
+
+int gnk_bratu_diag_jtj(gnk_ctx* ctx, const double* u, double* out, int reciprocal) {
+  if (!ready(ctx)) return -1;
+  RowLaunch L = rows(ctx, G, ctx->geo.nrows, vec_of(ctx), 1 << 30);
+  DISPATCH_VEC(ctx, k_diag_jtj, L, 0, u, out, ctx->geo, ctx->coef, L.lr0, L.nlr, reciprocal);
+  return check_launch(ctx, "bratu_diag_jtj");
+}
+
+int gnk_bratu_jdiag(gnk_ctx* ctx, const double* u, double* d) {
+  if (!ready(ctx)) return -1;
+  int64_t lr0, nlr;
+  residual_rows(ctx, lr0, nlr);
+  RowLaunch L = rows(ctx, lr0, nlr, vec_of(ctx), 1 << 30);
+  DISPATCH_VEC(ctx, k_jdiag, L, 0, u, d, ctx->geo, ctx->coef, L.lr0, L.nlr);
+  return check_launch(ctx, "bratu_jdiag");
+}
+
+int gnk_basis_gemv(gnk_ctx* ctx, const double* V, int64_t ldv, int k, const double* c, double* x) {
+  if (!ready(ctx)) return -1;
+  if (k < 1) return fail(ctx, "basis_gemv: k < 1");
+  if (vec_of(ctx) == 2 && (ldv % 2 != 0)) return fail(ctx, "basis_gemv: ldv must be even");
+  RowLaunch L = rows(ctx, 0, ctx->geo.nrows + 2 * G, vec_of(ctx), 1 << 30);
+  DISPATCH_VEC(ctx, k_gemv, L, 0, V, ldv, k, c, x, ctx->geo, L.lr0, L.nlr);
+  return check_launch(ctx, "basis_gemv");
+}
+
+int gnk_vjp_gemv_t(gnk_ctx* ctx, const double* u, const double* r, const double* V, int64_t ldv, int k,
+                   double* g, double* h_out) {
+  if (!ready(ctx)) return -1;
+  if (k < 0) return fail(ctx, "vjp_gemv_t: k < 0");
+  const int nchunk = std::max(1, (k + KC - 1) / KC);
+  RowLaunch L = rows(ctx, G, ctx->geo.nrows, vec_of(ctx), std::max(64, MAX_RED_BLOCKS / nchunk));
+  L.grid.z = nchunk;
+  const int nblk = L.grid.x * L.grid.y;
+  if (size_t(nblk) * nchunk * KC > SCRATCH_DOUBLES) return fail(ctx, "vjp_gemv_t: scratch too small");
+  DISPATCH_VEC(ctx, k_vjp_gemv_t, L, 0, u, r, V, ldv, k, g, ctx->geo, ctx->coef, L.lr0, L.nlr, ctx->scratch);
+  int rc = check_launch(ctx, "vjp_gemv_t");
+  if (rc || k == 0 || !h_out) return rc;
+  hipLaunchKernelGGL(k_reduce_chunks, dim3((k + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, ctx->stream, ctx->scratch, nblk,
+                     k, h_out);
+  return check_launch(ctx, "vjp_gemv_t reduce");
+}
+
+int gnk_cgs_update(gnk_ctx* ctx, const double* V, int64_t ldv, int k, const double* h, double* g,
+                   double* stats_out) {
+  if (!ready(ctx)) return -1;
+  if (k < 1) return fail(ctx, "cgs_update: k < 1");
+  if (vec_of(ctx) == 2 && (ldv % 2 != 0)) return fail(ctx, "cgs_update: ldv must be even");
+  RowLaunch L = rows(ctx, G, ctx->geo.nrows, vec_of(ctx));
+  const int nblk = L.grid.x * L.grid.y;
+  DISPATCH_VEC(ctx, k_cgs, L, 0, V, ldv, k, h, g, ctx->geo, L.lr0, L.nlr, ctx->scratch);
+  int rc = check_launch(ctx, "cgs_update");
+  if (rc) return rc;
+  return reduce(ctx, ctx->scratch, nblk, 2, 2, sum_max_flags(), stats_out);
+}
+
+int gnk_vec_stats(gnk_ctx* ctx, const double* x, double* stats_out) {
+  if (!ready(ctx)) return -1;
+  RowLaunch L = rows(ctx, G, ctx->geo.nrows, vec_of(ctx));
+  const int nblk = L.grid.x * L.grid.y;
+  DISPATCH_VEC(ctx, k_stats, L, 0, x, ctx->geo, L.lr0, L.nlr, ctx->scratch);
+  int rc = check_launch(ctx, "vec_stats");
+  if (rc) return rc;
+  return reduce(ctx, ctx->scratch, nblk, 2, 2, sum_max_flags(), stats_out);
+}
+
+int gnk_vec_div(gnk_ctx* ctx, const double* src, double denom, double* dst, int full_slab) {
+  if (!ready(ctx)) return -1;
+  RowLaunch L = full_slab ? rows(ctx, 0, ctx->geo.nrows + 2 * G, vec_of(ctx), 1 << 30)
+                          : rows(ctx, G, ctx->geo.nrows, vec_of(ctx), 1 << 30);
+  DISPATCH_VEC(ctx, k_div, L, 0, src, denom, dst, ctx->geo, L.lr0, L.nlr);
+  return check_launch(ctx, "vec_div");
+}
+
+int gnk_vec_axpy(gnk_ctx* ctx, const double* x, double alpha, const double* d, double* out, int full_slab) {
+  if (!ready(ctx)) return -1;
+  RowLaunch L = full_slab ? rows(ctx, 0, ctx->geo.nrows + 2 * G, vec_of(ctx), 1 << 30)
+                          : rows(ctx, G, ctx->geo.nrows, vec_of(ctx), 1 << 30);
+  DISPATCH_VEC(ctx, k_axpy, L, 0, x, alpha, d, out, ctx->geo, L.lr0, L.nlr);
+  return check_launch(ctx, "vec_axpy");
+}
+
+int gnk_gram_padded_dim(int k, int with_r) { return ((k + (with_r ? 1 : 0) + 15) / 16) * 16; }
+
+int gnk_gram(gnk_ctx* ctx, const double* u, const double* V, int64_t ldv, int k, const double* rinv, int64_t ldr,
+             const double* r, double* G_out) {
+  if (!ready(ctx)) return -1;
+  if (k < 1) return fail(ctx, "gram: k < 1");
+  const int KP = gnk_gram_padded_dim(k, r != nullptr);
+  if (rinv && ldr != KP) return fail(ctx, "gram: rinv must be the kp x kp augmented inverse (ldr == kp)");
+  const int nb = KP / 16;
+  const int P = nb * (nb + 1) / 2;
+  const int rowsplit = P <= PPW ? 1 : 0;
+  const int groups = rowsplit ? 1 : (P + 4 * PPW - 1) / (4 * PPW);
+  // tile rows: LDS tile <= ~40 KB for small KP (several WGs per CU), 64 rows otherwise
+  int T = 256;
+  while (T > 64 && size_t(T) * (KP + 1) * 8 > 40 * 1024) T >>= 1;
+  int logT = 0;
+  while ((1 << logT) < T) ++logT;
+  size_t lds = size_t(T) * (KP + 1) * 8 + size_t(T) * 8 + size_t(T) * 4;
+  lds = (lds + 15) & ~size_t(15);
+  if (rowsplit && size_t(P) * 256 > size_t(T) * (KP + 1)) return fail(ctx, "gram: reduction staging does not fit");
+  if (lds > 160 * 1024) return fail(ctx, "gram: k too large for the LDS tile");
+  const int64_t nown = ctx->geo.nrows * ctx->geo.N;
+  const int64_t ntiles = (nown + T - 1) / T;
+  const int wg_per_cu = std::max<int>(1, std::min<int>(4, int((160 * 1024) / lds)));
+  int64_t nblk = std::min<int64_t>(ntiles, int64_t(ctx->num_cus) * wg_per_cu);
+  nblk = std::max<int64_t>(nblk, 1);
+  const size_t per_group_pairs = rowsplit ? P : 4 * PPW;
+  if (size_t(nblk) * groups * per_group_pairs * 256 > SCRATCH_DOUBLES) return fail(ctx, "gram: scratch too small");
+  hipLaunchKernelGGL(k_gram, dim3(unsigned(nblk), unsigned(groups)), dim3(BLOCK), lds, ctx->stream, u, V, ldv, k, rinv,
+                     r, ctx->geo, ctx->coef, T, logT, KP, P, rowsplit, ntiles, ctx->scratch);
+  int rc = check_launch(ctx, "gram");
+  if (rc) return rc;
+  (void)hipMemsetAsync(G_out, 0, size_t(KP) * KP * sizeof(double), ctx->stream);
+  hipLaunchKernelGGL(k_gram_reduce, dim3((P * 256 + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, ctx->stream, ctx->scratch,
+                     int(nblk), P, rowsplit, KP, G_out);
+  return check_launch(ctx, "gram reduce");
+}
+
+int gnk_cg_normal_matvec(gnk_ctx* ctx, const double* d, const double* p, double* q, double* pq_out) {
+  if (!ready(ctx)) return -1;
+  RowLaunch L = rows(ctx, G, ctx->geo.nrows, vec_of(ctx));
+  const int nblk = L.grid.x * L.grid.y;
+  DISPATCH_VEC(ctx, k_cg_matvec, L, 0, d, p, q, ctx->geo, ctx->coef, L.lr0, L.nlr, ctx->scratch);
+  int rc = check_launch(ctx, "cg_normal_matvec");
+  if (rc) return rc;
+  return reduce(ctx, ctx->scratch, nblk, 1, 1, nullptr, pq_out);
+}
+
+int gnk_cg_update_xr(gnk_ctx* ctx, double alpha, const double* p, const double* q, double* x, double* r,
+                     const double* dinv, double* z, double* out) {
+  if (!ready(ctx)) return -1;
+  RowLaunch L = rows(ctx, G, ctx->geo.nrows, vec_of(ctx));
+  const int nblk = L.grid.x * L.grid.y;
+  DISPATCH_VEC(ctx, k_cg_xr, L, 0, alpha, p, q, x, r, dinv, z, ctx->geo, L.lr0, L.nlr, ctx->scratch);
+  int rc = check_launch(ctx, "cg_update_xr");
+  if (rc) return rc;
+  return reduce(ctx, ctx->scratch, nblk, 2, 2, nullptr, out);
+}
+
+int gnk_cg_update_p(gnk_ctx* ctx, double beta, int first, const double* z, double* p) {
+  if (!ready(ctx)) return -1;
+  RowLaunch L = rows(ctx, G, ctx->geo.nrows, vec_of(ctx), 1 << 30);
+  DISPATCH_VEC(ctx, k_cg_p, L, 0, beta, first, z, p, ctx->geo, L.lr0, L.nlr);
+  return check_launch(ctx, "cg_update_p");
+}
+
+// tooling: fp64 MFMA issue-rate probe (not part of the solver)
+int gnk_probe_mfma_f64(gnk_ctx* ctx, double* out, int blocks, int iters) {
+  if (!ctx) return -1;
+  hipLaunchKernelGGL(k_probe_mfma, dim3(blocks), dim3(BLOCK), 0, ctx->stream, out, iters);
+  return check_launch(ctx, "probe_mfma");
+}
+
+}  // extern "C"

@@ -1,0 +1,241 @@
+"""Classical Gauss-Newton with the CGLS inner solve on MI355X (ref:gauss_newton.py:11-138).
+
+``cg_least_squares`` restates scipy 1.15.3 ``scipy.sparse.linalg.cg``
+(iterative.py:305-422: x0 = 0, atol = rtol * ||b||, strict ``<`` test before
+each iteration, ``maxiter = 10 n``) on the normal equations A^T A x = A^T y with
+A = -J(u), including the reference's quirk of running an unpreconditioned CG
+first when ``preconditioner=False`` (ref:gauss_newton.py:45-48) whose
+iterations are counted but whose result is discarded.
+
+Per CG iteration on the GPU: one fused 13-point J^T J p stencil with p . q in
+the epilogue (gnk_cg_normal_matvec), one fused x/r/z update with r.r and r.z,
+one p update -- 112 n bytes of algorithmic traffic -- and two scalar syncs.
+``cg_rtol`` is exposed (the reference hard-codes 1e-4, which stays the default).
+"""
+from __future__ import annotations
+
+import math
+from collections.abc import Callable
+from typing import Optional
+
+import numpy as np
+import torch
+
+from ._device import BratuDevice
+from .armijo_goldstein import armijo_device
+from .gauss_newton_krylow import _noop, resolve_bratu
+from .regression_result import RegressionResult
+from .slab import Comm
+
+
+class DeviceCG:
+    """Device state of the CGLS solve for one rank."""
+
+    def __init__(self, dev: BratuDevice):
+        self.dev = dev
+        self.be = dev.backend
+        v = dev.vec
+        self.b, self.x, self.r, self.z, self.p, self.q = v(), v(), v(), v(), v(), v()
+        self.dvec, self.dinv = v(), v()
+        self._s2 = dev.scalar(2)
+        self._s1 = dev.scalar(1)
+        self.total_iters = 0
+
+    def _sum2(self):
+        return self.dev.comm.sum(self._s2)
+
+    def solve(self, u, y, cg_rtol=1e-4, preconditioner=True, callback=None):
+        """x = argmin ||y - A x||, A = -J(u); returns (x slab, cg_iter) like ref:gauss_newton.py:11-60.
+        ``u`` and ``y`` are slab vectors (u valid on owned +-2 rows, y on owned +-1 rows)."""
+        be, dev = self.be, self.dev
+        sl = dev.slab
+        be.vjp_gemv_t(u, y, None, 0, self.b, None)                 # b = A.T @ y = -(J.T y)
+        be.jdiag(u, self.dvec)                                     # J's diagonal, fixed during CG
+        count = [0]
+
+        def cb():
+            count[0] += 1
+            if callback is not None:
+                callback(self.x)
+
+        if not preconditioner:
+            self._cg(cg_rtol, None, cb)                            # ref:gauss_newton.py:45-48
+        be.diag_jtj(u, self.dinv, reciprocal=True)                 # ref:gauss_newton.py:50-54
+        self._cg(cg_rtol, self.dinv, cb)                           # :56-58
+        self.total_iters += count[0]
+        dev.comm.halo(self.x, sl.N, sl.nrows)
+        return self.x, count[0]
+
+    def _cg(self, rtol, dinv, cb):
+        """scipy iterative.py:305-422 with x0 = 0, atol = 0."""
+        be, dev, sl = self.be, self.dev, self.dev.slab
+        be.vec_stats(self.b, self._s2)
+        bb, _ = dev.comm.sum_max(self._s2)
+        bnrm2 = math.sqrt(bb)
+        atol = max(0.0, float(rtol) * float(bnrm2))
+        self.x.zero_()
+        if bnrm2 == 0:
+            self.x.copy_(self.b)
+            return 0
+        n = sl.n_global
+        maxiter = n * 10
+        self.r.copy_(self.b)
+        self.p.zero_()
+        self.q.zero_()
+        # z = M r and (r.r, r.z) via the update kernel with alpha = 0 (x, r unchanged)
+        be.cg_update_xr(0.0, self.p, self.q, self.x, self.r, dinv, self.z, self._s2)
+        rr, rz = self._sum2()
+        z = self.z if dinv is not None else self.r
+        rho_prev = None
+        for iteration in range(maxiter):
+            if math.sqrt(rr) < atol:
+                return iteration
+            rho = rz
+            if iteration > 0:
+                be.cg_update_p(rho / rho_prev, False, z, self.p)
+            else:
+                be.cg_update_p(0.0, True, z, self.p)
+            dev.comm.halo(self.p, sl.N, sl.nrows)
+            be.cg_matvec(self.dvec, self.p, self.q, self._s1)
+            pq = float(dev.comm.sum(self._s1)[0])
+            alpha = rho / pq
+            be.cg_update_xr(alpha, self.p, self.q, self.x, self.r, dinv, self.z, self._s2)
+            rr, rz = self._sum2()
+            rho_prev = rho
+            cb()
+        return maxiter
+
+
+def cg_least_squares(A, y, x0=None, cg_rtol=1e-4, preconditioner=True):
+    """Drop-in for ref:gauss_newton.py:11-60 with A = -jac(u) (a matrix-free BratuJacobian
+    scaled by -1) and y a host vector.  Returns (x as numpy, cg_iter)."""
+    from .bratu_pde_problem import BratuJacobian
+    if x0 is not None:
+        raise NotImplementedError("x0 != None is not used by the reference (ref:gauss_newton.py:112-114)")
+    if not isinstance(A, BratuJacobian) or A.sign != -1.0:
+        raise TypeError("cg_least_squares on MI355X expects A = -1 * jac(u) from BratuPdeProblem.make_jac()")
+    dev = BratuDevice(A.problem, Comm(single=True))
+    cg = DeviceCG(dev)
+    u = dev.load(A.u if not torch.is_tensor(A.u) else A.u.cpu().numpy())
+    ys = dev.load(y)
+    x, it = cg.solve(u, ys, cg_rtol=cg_rtol, preconditioner=preconditioner)
+    return dev.slab.to_host(x), it
+
+
+class GNSolver:
+    """Device Gauss-Newton loop (ref:gauss_newton.py:63-138), one outer iteration per ``step()``."""
+
+    def __init__(self, problem, y, tol=1e-8, max_iter=100, cg_preconditioner=False, cg_rtol=1e-4,
+                 comm: Optional[Comm] = None, device=None, backend=None, callback: Callable = None,
+                 callback_format="numpy"):
+        self.dev = BratuDevice(problem, comm, device, backend)
+        self.be = self.dev.backend
+        self.comm = self.dev.comm
+        self.tol, self.max_iter = tol, int(max_iter)
+        self.cg_pre, self.cg_rtol = cg_preconditioner, cg_rtol
+        self.callback, self.callback_format = callback, callback_format
+        self.y = self.dev.load(y)
+        self.cg = DeviceCG(self.dev)
+        self.xb = [self.dev.vec(), self.dev.vec()]
+        self.rb = [self.dev.vec(), self.dev.vec()]
+        self.jd = self.dev.vec()
+        self._s1 = self.dev.scalar(1)
+        self._s2 = self.dev.scalar(2)
+        self.trace = []
+
+    def _residual(self, x, r):
+        self.be.residual(x, self.y, r, self._s1)
+        return float(self.comm.sum(self._s1)[0])
+
+    def setup(self, x0):
+        self.xi, self.ri = 0, 0
+        self.xb[0].copy_(self.dev.load(x0))                          # x = x0.copy() (:95)
+        self.rr = self._residual(self.xb[0], self.rb[0])             # :100
+        self.nfev, self.njev = 1, 0
+        self.cg_iter = None
+        self.success = False
+        self.iter = 0
+        self.done = False
+        if self.max_iter < 2:
+            raise UnboundLocalError("local variable 'iter' referenced before assignment")
+
+    def step(self):
+        it = self.iter + 1
+        sl = self.dev.slab
+        x, r = self.xb[self.xi], self.rb[self.ri]
+        self.njev += 1                                               # :107-108
+        d, self.cg_iter = self.cg.solve(x, r, cg_rtol=self.cg_rtol, preconditioner=self.cg_pre)   # :111-114
+        self.be.jvp(x, d, self.jd)                                   # jac_ev @ d (ref:armijo_goldstein.py:50)
+        self.be.vec_stats(self.jd, self._s2)
+        jdd, _ = self.comm.sum_max(self._s2)
+        xt, rt = self.xb[1 - self.xi], self.rb[1 - self.ri]
+        last = {}
+
+        def trial(t):
+            self.be.vec_axpy(x, t, d, xt, True)                      # x + t d (whole slab)
+            last["rr"] = self._residual(xt, rt)
+            return last["rr"]
+
+        t, ntrial = armijo_device(trial, self.rr, jdd, d_norm_host(self, d))
+        self.nfev += ntrial
+        self.be.vec_stats(x, self._s2)
+        s, _ = self.comm.sum_max(self._s2)                          # np.sum(x**2) (:123)
+        self.be.vec_stats(d, self._s2)
+        dd, _ = self.comm.sum_max(self._s2)
+        self.xi, self.ri = 1 - self.xi, 1 - self.ri                  # x += t d (:125) == trial point
+        self.rr = last["rr"]
+        self.iter = it
+        self.trace.append({"t": t, "trials": ntrial, "cg_iter": self.cg_iter})
+        if self.callback is not None:
+            xs = self.xb[self.xi]
+            xo = xs[sl.own] if self.callback_format == "torch" else sl.to_host(xs)
+            self.callback(x=xo, nfev=self.nfev, cg_iter=self.cg_iter)
+        if t ** 2 * dd <= self.tol ** 2 * s:                         # :129-131
+            self.success = True
+            self.done = True
+        elif it >= self.max_iter - 1:
+            self.done = True
+        return self.done
+
+    def finish(self, result_format="numpy"):
+        if not self.success:
+            print("Warning: The gauss_newton algorithm reached maximal iteration bound before terminating!")
+        xs = self.xb[self.xi]
+        x = xs[self.dev.slab.own].clone() if result_format == "torch" else self.dev.slab.to_host(xs)
+        return RegressionResult("gauss newton", x, self.success, self.nfev, self.njev, self.iter)
+
+
+class _DNorm:
+    """Lazy ||d|| for the StepLengthConvergenceError message only."""
+
+    def __init__(self, solver, d):
+        self.solver, self.d = solver, d
+
+    def __array__(self, dtype=None, copy=None):
+        be = self.solver.be
+        be.vec_stats(self.d, self.solver._s2)
+        s, _ = self.solver.comm.sum_max(self.solver._s2)
+        return np.array([math.sqrt(s)])
+
+
+def d_norm_host(solver, d):
+    return _DNorm(solver, d)
+
+
+def gauss_newton(res, x0, jac, args: tuple = (), tol: float = 1e-8, max_iter=100, step_length_control=None,
+                 callback: Callable = _noop, cg_preconditioner: bool = False, *, cg_rtol: float = 1e-4,
+                 comm: Optional[Comm] = None, device=None, callback_format: str = "numpy",
+                 result_format: str = "numpy", _backend=None) -> RegressionResult:
+    """Drop-in for ref:gauss_newton.py:63-138 (sparse-Jacobian / CGLS branch); ``cg_rtol`` added."""
+    problem, y = resolve_bratu(res, jac)
+    if args:
+        raise TypeError("<lambda>() takes 1 positional argument but {} were given".format(1 + len(args)))
+    if step_length_control is not None:
+        raise NotImplementedError("the device solver uses the reference's armijo_goldstein rule")
+    cb = None if (callback is None or callback is _noop) else callback
+    solver = GNSolver(problem, y, tol=tol, max_iter=max_iter, cg_preconditioner=cg_preconditioner, cg_rtol=cg_rtol,
+                      comm=comm, device=device, backend=_backend, callback=cb, callback_format=callback_format)
+    solver.setup(x0 if not torch.is_tensor(x0) else x0.detach().cpu().numpy())
+    while not solver.step():
+        pass
+    return solver.finish(result_format)

@@ -1,0 +1,206 @@
+"""Gauss-Newton in generalized Krylov subspaces on MI355X (ref:gauss_newton_krylow.py:39-145).
+
+``gauss_newton_krylow`` keeps the reference's call surface and semantics --
+counters (nfev / njev / nit), the ``range(1, max_iter)`` loop bound, the first
+Jacobian at x0 but first residual at V @ c, the coordinate-norm convergence
+test, the four ``version`` update rules, restart, every printed message and
+every exception -- and runs each n-sized operation on the GPU:
+
+  per outer iteration (k basis columns, a Armijo trials)
+    2 Gram passes (fp64 MFMA, J V on the fly)   -> CholQR2 LS solve   (lls.py)
+    a x [basis GEMV + fused residual/||r||^2]   -> Armijo trials
+    fused -J^T r + V^T g, CGS update + stats, normalise, halo  -> basis update
+
+Host <-> device traffic per iteration is O(k^2) doubles (Gram matrices, k
+coefficients, a few scalars).  ``GNKSolver`` exposes the same loop one outer
+iteration at a time (used by bench.py to time exact steps).
+
+Problems: the device path needs the residual/Jacobian to come from this
+package's ``BratuPdeProblem.make_res`` / ``make_jac`` (matrix-free Bratu).
+"""
+from __future__ import annotations
+
+from collections.abc import Callable
+from typing import Optional
+
+import numpy as np
+import torch
+
+from ._device import BratuDevice
+from .armijo_goldstein import armijo_device
+from .bratu_pde_problem import BratuJacobianFunction, BratuResidual
+from .krylow import (DeviceKrylovBasis, GeneralizedKrylowSubspaceBreakdown,
+                     GeneralizedKrylowSubspaceSpansEntireSpace)
+from .lls import CholQR2Solver
+from .regression_result import RegressionResult
+from .slab import Comm
+
+VERSIONS = ("res_old", "res_new", "jac_old_res_old", "jac_old_res_new")
+
+
+def _noop(**kwargs):
+    return None
+
+
+def resolve_bratu(res, jac):
+    if not isinstance(res, BratuResidual) or not isinstance(jac, BratuJacobianFunction):
+        raise TypeError(
+            "the MI355X solver runs matrix-free problems: pass res = BratuPdeProblem.make_res(y) and "
+            "jac = BratuPdeProblem.make_jac() from gauss_newton_via_generalized_krylov_subspaces_amd")
+    if res.problem is not jac.problem:
+        raise ValueError("res and jac must come from the same BratuPdeProblem")
+    return res.problem, res.y
+
+
+class GNKSolver:
+    """One rank of the device GNK loop; ``step()`` runs exactly one outer iteration."""
+
+    def __init__(self, problem, y, krylow_restart=None, tol=1e-8, max_iter=100, version="res_old",
+                 comm: Optional[Comm] = None, device=None, backend=None, callback: Callable = None,
+                 callback_format: str = "numpy"):
+        self.dev = BratuDevice(problem, comm, device, backend)
+        self.be = self.dev.backend
+        self.comm = self.dev.comm
+        self.tol = tol
+        self.max_iter = int(max_iter)
+        self.version = version
+        self.restart = self.max_iter if krylow_restart is None else int(krylow_restart)
+        kmax = min(self.restart, max(self.max_iter - 1, 1)) + 1
+        kmax = min(kmax, self.dev.slab.n_global)
+        self.callback = callback
+        self.callback_format = callback_format
+        self.y = self.dev.load(y)
+        self.basis = DeviceKrylovBasis(self.dev, kmax)
+        self.lls = CholQR2Solver(self.dev, kmax)
+        self.xb = [self.dev.vec() for _ in range(3)]
+        self.rb = [self.dev.vec() for _ in range(2)]
+        self._n2 = self.dev.scalar(1)
+        self.trace = []          # per-iteration (t, k, trials) for tests / diagnostics
+
+    # -- pieces -------------------------------------------------------------------------
+    def _residual(self, x, r) -> float:
+        self.be.residual(x, self.y, r, self._n2)
+        return float(self.comm.sum(self._n2)[0])
+
+    def _free_x(self, *busy):
+        for i in range(3):
+            if i not in busy:
+                return i
+        raise RuntimeError("no free iterate buffer")
+
+    def _emit(self, xslab):
+        if self.callback is None:
+            return
+        if self.callback_format == "torch":
+            x = xslab[self.dev.slab.own]
+        else:
+            x = self.dev.slab.to_host(xslab)
+        self.callback(x=x, nfev=self.nfev, cg_iter=None)
+
+    # -- loop ---------------------------------------------------------------------------
+    def setup(self, x0):
+        """ref:gauss_newton_krylow.py:68-82"""
+        self.success = False
+        self.iter = 0
+        self.done = False
+        self.uJ = 0                                        # J is evaluated at x0 (:78)
+        self.xb[0].copy_(self.dev.load(x0))
+        self.c = self.basis.start(self.xb[0])              # :71
+        xi = self._free_x(self.uJ)
+        self.basis.x(self.c, self.xb[xi])
+        self.ri = 0
+        self.rr = self._residual(self.xb[xi], self.rb[0])  # :76 (at V @ c)
+        self.nfev = 1
+        self.njev = 1
+        if self.max_iter < 2:
+            raise UnboundLocalError("local variable 'iter' referenced before assignment")
+
+    def step(self) -> bool:
+        """One pass of ref:gauss_newton_krylow.py:84-136; returns True when the loop has ended."""
+        it = self.iter + 1
+        basis = self.basis
+        r_old = self.rb[self.ri]
+        d, jdd, _ = self.lls.solve(self.xb[self.uJ], basis, r_old)       # :86-89
+        xi = self._free_x(self.uJ)
+        rti = 1 - self.ri
+        x_t, r_t = self.xb[xi], self.rb[rti]
+        last = {}
+
+        def trial(t):
+            basis.x(self.c + t * d, x_t)                                  # res_krylow(x + t d)
+            last["rr"] = self._residual(x_t, r_t)
+            return last["rr"]
+
+        t, ntrial = armijo_device(trial, self.rr, jdd, d)                 # :91-93
+        self.nfev += ntrial                                               # :94
+        s = np.sum(self.c ** 2)                                           # :96
+        self.c += t * d                                                   # :98
+        self.trace.append({"t": t, "k": basis.k, "trials": ntrial})
+        self._emit(x_t)                                                   # :100
+        self.iter = it
+        self.x_last = xi
+        if t ** 2 * np.sum(d ** 2) <= self.tol ** 2 * s:                  # :102-104
+            self.success = True
+            self.done = True
+            return True
+        uJ_old, self.uJ = self.uJ, xi                                     # :106-108
+        self.njev += 1
+        try:
+            if self.version == "res_old":
+                basis.update(self.xb[self.uJ], r_old)
+            elif self.version == "res_new":
+                basis.update(self.xb[self.uJ], r_t)
+            elif self.version == "jac_old_res_old":
+                basis.update(self.xb[uJ_old], r_old)
+            elif self.version == "jac_old_res_new":
+                basis.update(self.xb[uJ_old], r_t)
+            else:
+                raise ValueError(
+                    "Variable version must be in ['res_old','res_new','jac_old_res_old','jac_old_res_new']")
+            self.c = np.append(self.c, 0)                                 # :124
+        except GeneralizedKrylowSubspaceBreakdown:
+            print(f"Generalized krylow subspace breakdown at iteration = {it}, basis.shape = {basis.shape}")
+        except GeneralizedKrylowSubspaceSpansEntireSpace:
+            print("Warning: The genearlized krylow subspace is now identical to the whole parameter space "
+                  f"at iteration = {it}")
+        self.ri = rti
+        self.rr = last["rr"]
+        if it % self.restart == 0:                                        # :135-136
+            xr = self._free_x(self.uJ)
+            basis.x(self.c, self.xb[xr])
+            self.c = basis.start(self.xb[xr])
+        if it >= self.max_iter - 1:
+            self.done = True
+        return self.done
+
+    def finish(self, result_format="numpy"):
+        """ref:gauss_newton_krylow.py:138-145"""
+        if not self.success:
+            print("Warning: The gauss_newton_krylow algorithm reached maximal iteration bound before terminating!")
+        xi = self._free_x(self.uJ)
+        xs = self.basis.x(self.c, self.xb[xi])
+        x = xs[self.dev.slab.own].clone() if result_format == "torch" else self.dev.slab.to_host(xs)
+        return RegressionResult("gauss newton krylow", x, self.success, self.nfev, self.njev, self.iter)
+
+
+def gauss_newton_krylow(res, x0, jac, krylow_restart: Optional[int] = None, args: tuple = (), tol: float = 1e-8,
+                        max_iter=100, callback: Callable = _noop, version: str = "res_old", *,
+                        comm: Optional[Comm] = None, device=None, callback_format: str = "numpy",
+                        result_format: str = "numpy", _backend=None) -> RegressionResult:
+    """Drop-in for ref:gauss_newton_krylow.py:39-145 (same positional/keyword arguments).
+
+    Extra keyword-only arguments: ``comm`` (a ``slab.Comm``; default: the initialised
+    torch.distributed group, else single rank), ``device``, ``callback_format``
+    ("numpy": full host vector like the reference; "torch": this rank's device rows),
+    ``result_format`` (same choice for ``RegressionResult.x``).
+    """
+    problem, y = resolve_bratu(res, jac)
+    if args:
+        raise TypeError("<lambda>() takes 1 positional argument but {} were given".format(1 + len(args)))
+    cb = None if (callback is None or callback is _noop) else callback
+    solver = GNKSolver(problem, y, krylow_restart=krylow_restart, tol=tol, max_iter=max_iter, version=version,
+                       comm=comm, device=device, backend=_backend, callback=cb, callback_format=callback_format)
+    solver.setup(x0 if not torch.is_tensor(x0) else x0.detach().cpu().numpy())
+    while not solver.step():
+        pass
+    return solver.finish(result_format)

@@ -1,0 +1,82 @@
+"""Generalized Krylov subspace on the GPU (ref:krylow.py:1-73).
+
+The basis is a device matrix ``V`` of shape (kmax, slab_len): row j is basis
+column j as a slab vector (column-major basis, contiguous columns), so one
+kernel pass streams k contiguous columns.  Columns are appended in place --
+the reference's ``np.hstack`` copy of the whole basis (ref:krylow.py:73, 6 % of
+its run time) does not exist here.
+
+Numerics follow the reference step by step: single classical Gram-Schmidt
+pass (CGS1, :64), breakdown when every |g_i| <= 1e-8 (:66, np.allclose with
+rtol=0), normalisation by division (:71).
+"""
+from __future__ import annotations
+
+import math
+
+import numpy as np
+
+
+class GeneralizedKrylowSubspaceBreakdown(Exception):
+    """ref:krylow.py:8-9"""
+
+
+class GeneralizedKrylowSubspaceSpansEntireSpace(Exception):
+    """ref:krylow.py:12-13"""
+
+
+class DeviceKrylovBasis:
+    def __init__(self, dev, kmax: int):
+        self.dev = dev
+        self.be = dev.backend
+        self.kmax = int(kmax)
+        self.V = self.be.zeros(self.kmax, dev.slab.length)
+        self.k = 0
+        self._c = self.be.zeros(self.kmax)
+        self._h = self.be.zeros(self.kmax)
+        self._stats = self.be.zeros(2)
+
+    @property
+    def shape(self):
+        """(n, k) like ``basis.shape`` in the reference (n = global unknowns)."""
+        return (self.dev.slab.n_global, self.k)
+
+    def start(self, x) -> np.ndarray:
+        """ref:krylow.py:30-39.  ``x`` is a slab vector valid on owned +-GHOST rows."""
+        self.be.vec_stats(x, self._stats)
+        sumsq, maxabs = self.dev.comm.sum_max(self._stats)
+        if maxabs <= 1e-8:                                    # np.allclose(x0, 0) (:31)
+            raise ValueError("x0 is not allowed to be 0 in the gauss_newton_krylow algorithm")
+        nrm = math.sqrt(sumsq)                                # np.linalg.norm (:36)
+        self.be.vec_div(x, nrm, self.V[0], True)              # whole slab incl. ghosts (:37)
+        self.k = 1
+        return np.array([nrm])
+
+    def x(self, c: np.ndarray, out):
+        """out = V @ c over the whole slab (ref:krylow.py:41-42)."""
+        k = len(c)
+        self._c[:k].copy_(self.be.to_device(c))
+        self.be.gemv(self.V, k, self._c, out)
+        return out
+
+    def update(self, u_jac, r):
+        """ref:krylow.py:55-73 with jac_ev = J(u_jac), res_ev = r (slab vectors)."""
+        k = self.k
+        if k == self.dev.slab.n_global:                       # :59-60
+            raise GeneralizedKrylowSubspaceSpansEntireSpace
+        if k >= self.kmax:
+            raise RuntimeError("Krylov basis storage exhausted")
+        g = self.V[k]                                         # new column built in place
+        self.be.vjp_gemv_t(u_jac, r, self.V, k, g, self._h)   # g = -J^T r ; h = V^T g (:62, :64)
+        h = self.dev.comm.sum(self._h[:k])
+        self._h[:k].copy_(self.be.to_device(h))
+        self.be.cgs_update(self.V, k, self._h, g, self._stats)   # g -= V h (:64)
+        sumsq, maxabs = self.dev.comm.sum_max(self._stats)
+        if maxabs <= 1e-8 and not math.isnan(sumsq):          # :66
+            raise GeneralizedKrylowSubspaceBreakdown(
+                "Normal residual is allready inside generalized Krylow Subspcae, there for gauss newton "
+                "krylow algorithm has to proceed without enlarging the subspace.")
+        nrm = math.sqrt(sumsq)                                # :71
+        self.be.vec_div(g, nrm, g, False)
+        self.dev.comm.halo(g, self.dev.slab.N, self.dev.slab.nrows)
+        self.k = k + 1

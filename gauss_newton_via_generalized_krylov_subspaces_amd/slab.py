@@ -1,0 +1,137 @@
+"""Row-slab decomposition of the Bratu grid over ranks (one process per GPU).
+
+The reference is single-process; this module is the build's
+multi-GPU layer.  Rank p owns global grid rows (the slow x index)
+[row0, row0 + nrows); every n-length object -- basis columns, iterates,
+residuals, CG vectors -- is split identically and stored as a slab vector with
+GHOST rows on each side (include/gnk.h).
+
+Determinism: every cross-rank reduction all-gathers the per-rank partials and
+sums them in rank order on every rank, so the control decisions (Armijo,
+breakdown, convergence, restart) are bit-identical on all ranks.
+
+Collectives: only two kinds exist on the data path --
+  * halo: P2P send/recv of GHOST boundary rows to the two neighbours, once per
+    appended basis column (and per CG iteration for the search direction);
+  * small all-gathers (Gram matrices, V^T g, norms), <= (k+1)^2 doubles.
+With world_size == 1 both are no-ops.
+"""
+from __future__ import annotations
+
+import math
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+from ._native import GHOST
+
+
+def row_partition(N: int, world: int, rank: int):
+    """Contiguous, balanced split of N rows over `world` ranks -> (row0, nrows)."""
+    base, rem = divmod(N, world)
+    nrows = base + (1 if rank < rem else 0)
+    row0 = rank * base + min(rank, rem)
+    return row0, nrows
+
+
+class Comm:
+    """Rank-ordered reductions and halo exchange over torch.distributed (RCCL on
+    GPUs, gloo on CPU).  ``group=None`` with no initialised process group means a
+    single rank."""
+
+    def __init__(self, group=None, single: bool = False):
+        if not single and dist.is_available() and dist.is_initialized():
+            self.group = group
+            self.rank = dist.get_rank(group)
+            self.world = dist.get_world_size(group)
+        else:
+            self.group = None
+            self.rank, self.world = 0, 1
+
+    # -- reductions -------------------------------------------------------------
+    def _gather(self, t: torch.Tensor) -> np.ndarray:
+        if self.world == 1:
+            return t.detach().to("cpu", torch.float64).numpy()[None]
+        t = t.contiguous().reshape(-1)
+        buf = torch.empty(self.world * t.numel(), dtype=t.dtype, device=t.device)
+        dist.all_gather_into_tensor(buf, t, group=self.group)
+        return buf.to("cpu").numpy().reshape(self.world, -1)
+
+    def sum(self, t: torch.Tensor) -> np.ndarray:
+        """Sum of a small per-rank tensor over ranks, in rank order (host result)."""
+        parts = self._gather(t)
+        s = parts[0].copy()
+        for p in range(1, parts.shape[0]):
+            s = s + parts[p]
+        return s
+
+    def sum_max(self, t: torch.Tensor) -> tuple[float, float]:
+        """t = [sum, max] per rank -> (sum over ranks, NaN-propagating max over ranks)."""
+        parts = self._gather(t)
+        s, m = float(parts[0][0]), float(parts[0][1])
+        for p in range(1, parts.shape[0]):
+            s = s + float(parts[p][0])
+            v = float(parts[p][1])
+            if v > m or math.isnan(v):
+                m = v
+        return s, m
+
+    def barrier(self):
+        if self.world > 1:
+            dist.barrier(group=self.group)
+
+    # -- halo -------------------------------------------------------------------
+    def halo(self, vec: torch.Tensor, N: int, nrows: int):
+        """Fill the GHOST ghost rows of a slab vector from the neighbouring ranks."""
+        if self.world == 1:
+            return
+        g = GHOST * N
+        own_end = (GHOST + nrows) * N
+        ops = []
+        if self.rank > 0:
+            ops.append(dist.P2POp(dist.isend, vec[g:2 * g], self.rank - 1, self.group))
+            ops.append(dist.P2POp(dist.irecv, vec[0:g], self.rank - 1, self.group))
+        if self.rank < self.world - 1:
+            ops.append(dist.P2POp(dist.isend, vec[own_end - g:own_end], self.rank + 1, self.group))
+            ops.append(dist.P2POp(dist.irecv, vec[own_end:own_end + g], self.rank + 1, self.group))
+        for req in dist.batch_isend_irecv(ops):
+            req.wait()
+
+    def gather_rows(self, owned: torch.Tensor, N: int) -> np.ndarray:
+        """All ranks' owned rows -> the full host vector (variable slab sizes)."""
+        host = owned.detach().to("cpu").numpy()
+        if self.world == 1:
+            return host.copy()
+        parts = [None] * self.world
+        dist.all_gather_object(parts, host, group=self.group)
+        return np.concatenate(parts)
+
+
+class Slab:
+    """Geometry of this rank's slab + helpers to move whole-grid host arrays in and out."""
+
+    def __init__(self, N: int, comm: Comm):
+        self.N = int(N)
+        self.comm = comm
+        if comm.world > N // GHOST:
+            raise ValueError(f"grid of {N} rows cannot be split over {comm.world} ranks "
+                             f"(each rank needs >= {GHOST} rows)")
+        self.row0, self.nrows = row_partition(self.N, comm.world, comm.rank)
+        self.length = (self.nrows + 2 * GHOST) * self.N
+        self.own = slice(GHOST * self.N, (GHOST + self.nrows) * self.N)
+        self.n_global = self.N * self.N
+
+    def from_host(self, full, backend) -> torch.Tensor:
+        """Slab vector (owned + up to GHOST rows each side) from a full-grid vector."""
+        full = torch.as_tensor(np.asarray(full, dtype=np.float64) if not torch.is_tensor(full) else full)
+        out = backend.zeros(self.length)
+        lo = max(self.row0 - GHOST, 0)
+        hi = min(self.row0 + self.nrows + GHOST, self.N)
+        dst0 = (lo - (self.row0 - GHOST)) * self.N
+        out[dst0:dst0 + (hi - lo) * self.N] = full.reshape(-1)[lo * self.N:hi * self.N].to(out.device, torch.float64)
+        return out
+
+    def to_host(self, slab_vec: torch.Tensor) -> np.ndarray:
+        """Full-grid host vector gathered from every rank's owned rows."""
+        return self.comm.gather_rows(slab_vec[self.own], self.N)

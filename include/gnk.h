@@ -1,0 +1,132 @@
+/*
+ * gnk.h -- C-ABI of libgnk.so, the MI355X (gfx950) hot path of the
+ * generalized-Krylov Gauss-Newton solver on the Bratu problem.
+ *
+ * Reference (mariusbaehr/gauss_newton_via_generalized_krylov_subspaces, read-only
+ * at /root/reference in the build container) is pure Python/NumPy/SciPy; there
+ * is no native interface to replace.  Each entry point below names the Python
+ * expression of the reference it executes on the GPU, so a maintainer can bind
+ * it with ctypes (INTEGRATION.md shows the binding).
+ *
+ * Conventions
+ *  - Every pointer argument is a DEVICE pointer (hipMalloc / torch CUDA tensor)
+ *    unless its name ends in _host.  Sizes are element counts.
+ *  - All work is enqueued on the stream given to gnk_set_stream (default: the
+ *    null stream).  Functions do not synchronise and never allocate (the
+ *    context owns a fixed scratch arena made at gnk_ctx_create).
+ *  - Return value: 0 = OK, < 0 = error; gnk_last_error(ctx) has the text.
+ *  - Grid vectors are "slab vectors": the rank owns global rows
+ *    [row0, row0 + nrows) of the N x N interior grid (flat index jx*N + iy, jx
+ *    slow, ref:bratu_pde_problem.py:69-74) and stores them with GNK_GHOST_ROWS
+ *    ghost rows on each side: length (nrows + 2*GNK_GHOST_ROWS) * N, owned data
+ *    at offset GNK_GHOST_ROWS * N.  Ghost rows outside the domain are zero.
+ *  - Reductions write their result into a small device array (the caller
+ *    combines ranks in rank order); they are deterministic run to run.
+ */
+#ifndef GNK_H
+#define GNK_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GNK_GHOST_ROWS 2
+#define GNK_ABI_VERSION 1
+
+typedef struct gnk_ctx gnk_ctx;
+
+/* ---- context ---------------------------------------------------------- */
+int gnk_abi_version(void);
+int gnk_ctx_create(int device, gnk_ctx** out);
+void gnk_ctx_destroy(gnk_ctx* ctx);
+const char* gnk_last_error(const gnk_ctx* ctx);
+int gnk_set_stream(gnk_ctx* ctx, void* hip_stream);
+
+/* Bratu slab geometry + coefficients.  h = grid_resolution, alpha = ALPHA,
+ * lambda = LAMBDA of BratuPdeProblem (ref:bratu_pde_problem.py:20-67). */
+int gnk_set_bratu(gnk_ctx* ctx, int64_t N, int64_t row0, int64_t nrows,
+                  double h, double alpha, double lambda);
+int64_t gnk_slab_len(const gnk_ctx* ctx);
+
+/* ---- Bratu operator (matrix-free; replaces the per-call CSR assembly) --- */
+/* out = J(u) @ v on owned rows; v's ghost rows must be valid.
+ * J(u) = -(L + ALPHA*D_x + LAMBDA*diag(exp u))      ref:bratu_pde_problem.py:88-96 */
+int gnk_bratu_jvp(gnk_ctx* ctx, const double* u, const double* v, double* out);
+/* out = J(u).T @ w on owned rows               ref:krylow.py:62 (jac_ev.T @ res_ev) */
+int gnk_bratu_vjp(gnk_ctx* ctx, const double* u, const double* w, double* out);
+/* F = pde_operator(x) on owned rows             ref:bratu_pde_problem.py:76-83 */
+int gnk_bratu_forward(gnk_ctx* ctx, const double* x, double* F);
+/* r = y - pde_operator(x) on owned rows and the one ghost row each side that
+ * lies inside the domain (x must be valid on owned +-2 rows);
+ * norm2_out[0] = sum(r**2) over owned rows      ref:bratu_pde_problem.py:85-86,
+ *                                               ref:armijo_goldstein.py:49,57 */
+int gnk_bratu_residual(gnk_ctx* ctx, const double* x, const double* y, double* r,
+                       double* norm2_out);
+/* out = diag(J(u).T @ J(u)) (closed form), or 1 / that when reciprocal != 0
+ * (the Jacobi preconditioner)                   ref:gauss_newton.py:50-54 */
+int gnk_bratu_diag_jtj(gnk_ctx* ctx, const double* u, double* out, int reciprocal);
+/* d = diagonal of L + ALPHA*D_x + LAMBDA*diag(exp u) on owned +-1 rows (inside
+ * the domain); u must be valid there        ref:bratu_pde_problem.py:92-96 */
+int gnk_bratu_jdiag(gnk_ctx* ctx, const double* u, double* d);
+
+/* ---- generalized Krylov basis (column-major V, column stride ldv) -------- */
+/* x = V[:, :k] @ c over the whole slab (ghost rows included)
+ *                                               ref:krylow.py:41-42 */
+int gnk_basis_gemv(gnk_ctx* ctx, const double* V, int64_t ldv, int k,
+                   const double* c, double* x);
+/* g = -(J(u).T @ r) on owned rows, h = V[:, :k].T @ g (local partial; k may
+ * be 0, then only g is written and h_out may be NULL)
+ *                                               ref:krylow.py:62,64 */
+int gnk_vjp_gemv_t(gnk_ctx* ctx, const double* u, const double* r,
+                   const double* V, int64_t ldv, int k, double* g, double* h_out);
+/* g -= V[:, :k] @ h on owned rows; stats_out = {sum g**2, max|g|}
+ *                                               ref:krylow.py:64,66,71 */
+int gnk_cgs_update(gnk_ctx* ctx, const double* V, int64_t ldv, int k,
+                   const double* h, double* g, double* stats_out);
+/* stats_out = {sum x**2, max|x|} over owned rows  ref:krylow.py:31,36 */
+int gnk_vec_stats(gnk_ctx* ctx, const double* x, double* stats_out);
+/* dst = src / denom on owned rows (full_slab = 0) or the whole slab (1)
+ *                                               ref:krylow.py:37,71 */
+int gnk_vec_div(gnk_ctx* ctx, const double* src, double denom, double* dst, int full_slab);
+
+/* out = x + (alpha * d) (two roundings, as NumPy's x + t * d) on owned rows or
+ * the whole slab                                ref:gauss_newton.py:125,
+ *                                               ref:armijo_goldstein.py:56 */
+int gnk_vec_axpy(gnk_ctx* ctx, const double* x, double alpha, const double* d, double* out,
+                 int full_slab);
+
+/* ---- Gram passes of the CholeskyQR2 least-squares solve (fp64 MFMA) ----
+ * W = [J(u) @ V[:, :k] | r] @ RinvAug  (RinvAug: kp x kp row-major, ld = kp: the
+ * inverse of the pass-1 R factor, 1 at [k][k] when r is given, zeros elsewhere;
+ * NULL = identity; r: NULL = no extra column).
+ * G_out (kp x kp, kp = k (+1 if r) rounded up to 16, row-major) = W.T @ W
+ * over owned rows.  This replaces scipy.linalg.qr(-J@V) + q.T @ y of
+ *                                               ref:gauss_newton_krylow.py:30,35 */
+int gnk_gram_padded_dim(int k, int with_r);
+int gnk_gram(gnk_ctx* ctx, const double* u, const double* V, int64_t ldv, int k,
+             const double* rinv, int64_t ldr, const double* r, double* G_out);
+
+/* ---- CGLS (scipy cg on A.T A, A = -J)     ref:gauss_newton.py:11-60 ----- */
+/* q = A.T @ (A @ p) = J.T (J p), A = -J, as one fused 13-point stencil over the
+ * precomputed diagonal d (gnk_bratu_jdiag); p valid on owned +-2 rows.
+ * pq_out[0] = p . q over owned rows        ref:gauss_newton.py:36, scipy iterative.py:411-412 */
+int gnk_cg_normal_matvec(gnk_ctx* ctx, const double* d, const double* p, double* q,
+                         double* pq_out);
+/* x += alpha p ; r -= alpha q ; z = dinv * r (or r if dinv NULL);
+ * out = {r . r, r . z} (owned)              scipy iterative.py:401-415 */
+int gnk_cg_update_xr(gnk_ctx* ctx, double alpha, const double* p, const double* q,
+                     double* x, double* r, const double* dinv, double* z, double* out);
+/* p = z (first) or p = beta * p + z (owned rows) */
+int gnk_cg_update_p(gnk_ctx* ctx, double beta, int first, const double* z, double* p);
+
+/* ---- tooling (not on the solver path) ----------------------------------- */
+/* back-to-back v_mfma_f64_16x16x4_f64 issue-rate probe: blocks x 256 threads,
+ * 4 independent accumulators per wave, iters x 4 MFMAs per wave */
+int gnk_probe_mfma_f64(gnk_ctx* ctx, double* out, int blocks, int iters);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GNK_H */

@@ -1,0 +1,233 @@
+"""CPU test double of the libgnk C-ABI (include/gnk.h), for host-logic tests only.
+
+Implements every backend method of ``_native.HipBackend`` with NumPy on CPU
+torch tensors, slab by slab (ghost rows included), so the solver drivers and
+the multi-rank slab logic (halo exchange, rank-ordered reductions over gloo) can
+be exercised without a GPU.  It is NOT a fallback: the product package never
+imports it; tests inject it through the private ``_backend`` argument.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+GHOST = 2
+
+
+class NumpyBackend:
+    def __init__(self):
+        self.device = torch.device("cpu")
+        self.geo = None
+
+    # -- setup -------------------------------------------------------------------------
+    def set_bratu(self, N, row0, nrows, h, alpha, lam):
+        self.N, self.row0, self.nrows = int(N), int(row0), int(nrows)
+        hm2, hm1 = h ** -2, h ** -1
+        self.hm2 = -(-1.0 * hm2)
+        self.l_off = -1.0 * hm2
+        self.l_diag = 4.0 * hm2
+        self.dx_diag = alpha * (-1.0 * hm1)
+        self.dx_up = alpha * (1.0 * hm1)
+        self.j_lin_diag = self.l_diag + self.dx_diag
+        self.j_lin_up = self.l_off + self.dx_up
+        self.lam = lam
+
+    def slab_len(self):
+        return (self.nrows + 2 * GHOST) * self.N
+
+    def empty(self, *shape):
+        return torch.empty(*shape, dtype=torch.float64)
+
+    def zeros(self, *shape):
+        return torch.zeros(*shape, dtype=torch.float64)
+
+    def to_device(self, a):
+        return torch.as_tensor(np.asarray(a, dtype=np.float64)).clone()
+
+    def gram_dim(self, k, with_r):
+        return ((k + (1 if with_r else 0) + 15) // 16) * 16
+
+    # -- helpers -----------------------------------------------------------------------
+    def _m(self, t):
+        return t.numpy().reshape(self.nrows + 2 * GHOST, self.N)
+
+    def _rows(self, lo, hi):
+        return slice(lo, hi)
+
+    def _res_rows(self):
+        lo, hi = GHOST - 1, GHOST + self.nrows + 1
+        if self.row0 == 0:
+            lo = GHOST
+        if self.row0 + self.nrows >= self.N:
+            hi = GHOST + self.nrows
+        return lo, hi
+
+    def _diag(self, U):
+        if self.lam == 0:
+            return np.full_like(U, self.j_lin_diag)
+        return self.j_lin_diag + self.lam * np.exp(U)
+
+    def _nb(self, X, lo, hi):
+        C = X[lo:hi]
+        n_ = X[lo - 1:hi - 1]
+        s_ = X[lo + 1:hi + 1]
+        w_ = np.zeros_like(C); w_[:, 1:] = C[:, :-1]
+        e_ = np.zeros_like(C); e_[:, :-1] = C[:, 1:]
+        return n_, w_, C, e_, s_
+
+    def _jvp_block(self, D, vn, vw, vc, ve, vs):
+        s = 0.0 + self.hm2 * vn
+        s = s + self.hm2 * vw
+        s = s + (-D) * vc
+        s = s + self.hm2 * ve
+        s = s + (-self.j_lin_up) * vs
+        return s
+
+    def _vjp_block(self, D, wn, ww, wc, we, ws):
+        s = 0.0 + (-self.j_lin_up) * wn
+        s = s + self.hm2 * ww
+        s = s + (-D) * wc
+        s = s + self.hm2 * we
+        s = s + self.hm2 * ws
+        return s
+
+    # -- operator ----------------------------------------------------------------------
+    def jvp(self, u, v, out):
+        lo, hi = GHOST, GHOST + self.nrows
+        O = self._m(out)
+        O[lo:hi] = self._jvp_block(self._diag(self._m(u)[lo:hi]), *self._nb(self._m(v), lo, hi))
+
+    def vjp(self, u, w, out):
+        lo, hi = GHOST, GHOST + self.nrows
+        O = self._m(out)
+        O[lo:hi] = self._vjp_block(self._diag(self._m(u)[lo:hi]), *self._nb(self._m(w), lo, hi))
+
+    def _fwd(self, X, lo, hi):
+        xn, xw, xc, xe, xs = self._nb(X, lo, hi)
+        l = 0.0 + self.l_off * xn
+        l = l + self.l_off * xw
+        l = l + self.l_diag * xc
+        l = l + self.l_off * xe
+        l = l + self.l_off * xs
+        dx = 0.0 + self.dx_diag * xc
+        dx = dx + self.dx_up * xs
+        f = l + dx
+        if self.lam != 0:
+            f = f + self.lam * np.exp(xc)
+        return f
+
+    def forward(self, x, F):
+        lo, hi = GHOST, GHOST + self.nrows
+        self._m(F)[lo:hi] = self._fwd(self._m(x), lo, hi)
+
+    def residual(self, x, y, r, norm2):
+        lo, hi = self._res_rows()
+        R = self._m(r)
+        R[lo:hi] = self._m(y)[lo:hi] - self._fwd(self._m(x), lo, hi)
+        own = R[GHOST:GHOST + self.nrows]
+        norm2[0] = float(np.sum(own * own))
+
+    def diag_jtj(self, u, out, reciprocal=False):
+        lo, hi = GHOST, GHOST + self.nrows
+        D = self._diag(self._m(u)[lo:hi])
+        N = self.N
+        grow = (self.row0 + np.arange(self.nrows))[:, None]
+        iy = np.arange(N)[None, :]
+        o2 = self.l_off * self.l_off
+        up = np.where(grow > 0, self.j_lin_up * self.j_lin_up, 0.0)
+        west = np.where(iy > 0, o2, 0.0)
+        east = np.where(iy < N - 1, o2, 0.0)
+        south = np.where(grow < N - 1, o2, 0.0)
+        v = (((up + west) + D * D) + east) + south
+        self._m(out)[lo:hi] = 1.0 / v if reciprocal else v
+
+    def jdiag(self, u, d):
+        lo, hi = self._res_rows()
+        self._m(d)[lo:hi] = self._diag(self._m(u)[lo:hi])
+
+    # -- basis -------------------------------------------------------------------------
+    def gemv(self, V, k, c, x):
+        Vn = V.numpy()[:k]
+        x.numpy()[:] = np.asarray(c.numpy()[:k]) @ Vn
+
+    def vjp_gemv_t(self, u, r, V, k, g, h):
+        lo, hi = GHOST, GHOST + self.nrows
+        G = self._m(g)
+        G[lo:hi] = -self._vjp_block(self._diag(self._m(u)[lo:hi]), *self._nb(self._m(r), lo, hi))
+        if k > 0:
+            own = slice(GHOST * self.N, (GHOST + self.nrows) * self.N)
+            h.numpy()[:k] = V.numpy()[:k, own] @ g.numpy()[own]
+
+    def cgs_update(self, V, k, h, g, stats):
+        own = slice(GHOST * self.N, (GHOST + self.nrows) * self.N)
+        gv = g.numpy()
+        gv[own] = gv[own] - h.numpy()[:k] @ V.numpy()[:k, own]
+        o = gv[own]
+        stats[0] = float(np.sum(o * o))
+        stats[1] = float(np.max(np.abs(o))) if not np.isnan(o).any() else float("nan")
+
+    def vec_stats(self, x, stats):
+        own = slice(GHOST * self.N, (GHOST + self.nrows) * self.N)
+        o = x.numpy()[own]
+        stats[0] = float(np.sum(o * o))
+        stats[1] = float(np.max(np.abs(o)))
+
+    def vec_div(self, src, denom, dst, full_slab):
+        sl = slice(None) if full_slab else slice(GHOST * self.N, (GHOST + self.nrows) * self.N)
+        dst.numpy()[sl] = src.numpy()[sl] / denom
+
+    def vec_axpy(self, x, alpha, d, out, full_slab):
+        sl = slice(None) if full_slab else slice(GHOST * self.N, (GHOST + self.nrows) * self.N)
+        out.numpy()[sl] = x.numpy()[sl] + alpha * d.numpy()[sl]
+
+    def gram(self, u, V, k, rinv, r, G):
+        lo, hi = GHOST, GHOST + self.nrows
+        D = self._diag(self._m(u)[lo:hi])
+        cols = []
+        for j in range(k):
+            Vj = V[j].numpy().reshape(self.nrows + 2 * GHOST, self.N)
+            cols.append(self._jvp_block(D, *self._nb(Vj, lo, hi)).reshape(-1))
+        if r is not None:
+            cols.append(self._m(r)[lo:hi].reshape(-1).copy())
+        kp = self.gram_dim(k, r is not None)
+        W = np.zeros((len(cols[0]), kp))
+        W[:, :len(cols)] = np.stack(cols, axis=1)
+        if rinv is not None:
+            W = W @ rinv.numpy().reshape(kp, kp)
+        G.numpy()[:kp * kp] = (W.T @ W).reshape(-1)
+
+    # -- CG ------------------------------------------------------------------------------
+    def cg_matvec(self, d, p, q, pq):
+        # t = J p on owned +-1 rows (inside the domain), then q = J^T t
+        lo, hi = GHOST, GHOST + self.nrows
+        P = self._m(p)
+        Dm = self._m(d)
+        T = np.zeros_like(P)
+        tlo = max(lo - 1, GHOST - (self.row0 - 0) if self.row0 == 0 else lo - 1)
+        tlo = GHOST if self.row0 == 0 else lo - 1
+        thi = GHOST + self.nrows if self.row0 + self.nrows >= self.N else hi + 1
+        T[tlo:thi] = self._jvp_block(Dm[tlo:thi], *self._nb(P, tlo, thi))
+        Q = self._m(q)
+        Q[lo:hi] = self._vjp_block(Dm[lo:hi], *self._nb(T, lo, hi))
+        own = slice(GHOST * self.N, (GHOST + self.nrows) * self.N)
+        pq[0] = float(np.dot(p.numpy()[own], q.numpy()[own]))
+
+    def cg_update_xr(self, alpha, p, q, x, r, dinv, z, out):
+        own = slice(GHOST * self.N, (GHOST + self.nrows) * self.N)
+        xv, rv = x.numpy(), r.numpy()
+        xv[own] = xv[own] + alpha * p.numpy()[own]
+        rv[own] = rv[own] - alpha * q.numpy()[own]
+        if dinv is not None:
+            z.numpy()[own] = 0.0 + dinv.numpy()[own] * rv[own]
+            zz = z.numpy()[own]
+        else:
+            zz = rv[own]
+        out[0] = float(np.dot(rv[own], rv[own]))
+        out[1] = float(np.dot(rv[own], zz))
+
+    def cg_update_p(self, beta, first, z, p):
+        own = slice(GHOST * self.N, (GHOST + self.nrows) * self.N)
+        if first:
+            p.numpy()[own] = z.numpy()[own]
+        else:
+            p.numpy()[own] = p.numpy()[own] * beta + z.numpy()[own]
