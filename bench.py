@@ -1,0 +1,238 @@
+#!/usr/bin/env python3
+"""Benchmark: GN-Krylov outer iterations/s on the Bratu grid (BASELINE.json metric).
+
+Workload (BASELINE.json configs[1]/metric): Bratu 2-D, ALPHA = 5, LAMBDA = 10,
+u0 = u_true + 0.1 N(0, 1) (np.random.seed(42), ref:bratu_pde_test.py:22-36),
+fp64, gauss_newton_krylow with krylow_restart = 20 ("Krylov dim 20") on an
+N x N interior grid (default N = 8192, the metric's grid).  One *step* = one GNK
+outer iteration (LS solve + Armijo trials + basis update); the timed steps cover
+a full restart cycle so every basis size 1..21 is represented.
+
+Multi-GPU (torchrun, one process per GPU): the same grid is row-partitioned
+over the ranks (strong scaling); halos + rank-ordered all-gathers over RCCL.
+value = outer iterations of the whole job per second (max elapsed over ranks).
+
+Also reported: the dominant kernel's roofline (fp64-MFMA Gram pass, HBM-bound,
+timed per launch with HIP events over the timed region), the single-vector
+JVP microbenchmark (the north star's "8192^2 JVP HBM GB/s"), the whole-step
+algorithmic GB/s, and the CPU oracle timed on a bounded sample on this host.
+"""
+from __future__ import annotations
+
+import argparse
+import contextlib
+import glob
+import io
+import json
+import math
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0     # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--grid", type=int, default=8192, help="interior points per side N")
+    ap.add_argument("--restart", type=int, default=20)
+    ap.add_argument("--version", default="res_old")
+    ap.add_argument("--cpu-seconds", type=float, default=20.0, help="CPU oracle sample budget (0 = skip)")
+    ap.add_argument("--jvp-reps", type=int, default=20)
+    return ap.parse_args()
+
+
+def bratu_inputs(N, seed=42):
+    """u_true (Fortran-order flatten == jx*N + iy) and u0 of ref:bratu_pde_test.py:34-36."""
+    from gauss_newton_via_generalized_krylov_subspaces_amd import BratuPdeProblem
+    prob = BratuPdeProblem(N + 1, 5, 10)
+    u_true = prob.u_true
+    np.random.seed(seed)
+    u0 = u_true + 0.1 * np.random.normal(loc=0, scale=1, size=len(u_true))
+    return prob, u_true, u0
+
+
+def step_bytes(n, k, a):
+    """Algorithmic HBM bytes of one outer iteration as implemented:
+    2 Gram passes (k+1, k+2 vectors), a trials x (GEMV k+1 + residual 3),
+    fused VJP + V^T g (k+3), CGS update (k+2), normalise (2)."""
+    return 8.0 * n * (4 * k + 10 + a * (k + 4))
+
+
+def cpu_baseline(N, seconds, version, restart):
+    """The CPU oracle (NumPy restatement of the reference, oracle/) on this host:
+    setup excluded, GNK outer iterations until `seconds` of work (>= 1)."""
+    from oracle import gnk_oracle as O
+    threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+    prob, y, u0 = O.bratu_workload(N)
+    res, jac = prob.make_res(y), prob.make_jac()
+    times = []
+
+    class Stop(Exception):
+        pass
+
+    t_last = [None]
+
+    def cb(x, nfev, cg_iter):
+        now = time.perf_counter()
+        times.append(now - t_last[0])
+        t_last[0] = now
+        if sum(times) >= seconds:
+            raise Stop
+
+    t_last[0] = time.perf_counter()
+    with contextlib.redirect_stdout(io.StringIO()):
+        try:
+            O.gauss_newton_krylow(res, u0, jac, krylow_restart=restart, max_iter=10 ** 6, callback=cb, version=version)
+        except Stop:
+            pass
+    it = len(times)
+    total = sum(times)
+    return {"value": it / total, "unit": "outer_iters/s", "cores": threads, "kind": "port",
+            "sample": f"oracle/gnk_oracle.py GNK on the same {N}^2 workload, first {it} outer iterations "
+                      f"(basis k=1..{it}; {total:.1f} s, setup excluded), OPENBLAS threads={threads}"}
+
+
+def pmc_traffic(config_key):
+    """HBM bytes per Gram launch from the committed rocprofv3 PMC summary, if one matches."""
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "pmc_summary.json")), reverse=True):
+        try:
+            with open(path) as f:
+                d = json.load(f)
+            if d.get("config") == config_key and d.get("traffic_bytes_per_launch"):
+                return d["traffic_bytes_per_launch"], os.path.relpath(path, ROOT)
+        except (OSError, ValueError):
+            continue
+    return None, None
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(0)
+    device = torch.device("cuda", torch.cuda.current_device())
+
+    import gauss_newton_via_generalized_krylov_subspaces_amd as gnk
+    from gauss_newton_via_generalized_krylov_subspaces_amd import _native
+    from gauss_newton_via_generalized_krylov_subspaces_amd._device import SingleRankOperator
+    from gauss_newton_via_generalized_krylov_subspaces_amd.slab import Comm
+
+    N = args.grid
+    n = N * N
+    prob, u_true, u0 = bratu_inputs(N)
+    y = SingleRankOperator(prob, device).forward(u_true)            # y = F(u_true) (ref:bratu_pde_test.py:29)
+    comm = Comm()
+    solver = gnk.GNKSolver(prob, y, krylow_restart=args.restart, tol=1e-8, max_iter=10 ** 9,
+                           version=args.version, comm=comm, device=device)
+    del y
+    solver.setup(u0)
+    be = solver.be
+    with contextlib.redirect_stdout(io.StringIO()):
+        for _ in range(args.warmup):
+            solver.step()
+    cap = 4 * (args.steps + 1)
+    be.timer_start(_native.TIMER_GRAM, cap)
+    k_trace0 = len(solver.trace)
+    comm.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    with contextlib.redirect_stdout(io.StringIO()):
+        for _ in range(args.steps):
+            if solver.step():
+                break
+    torch.cuda.synchronize()
+    comm.barrier()
+    elapsed = time.perf_counter() - t0
+    steps_done = len(solver.trace) - k_trace0
+    launches = be.timer_collect(cap)
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = t.item()
+
+    # whole-step algorithmic bytes (global grid) over the timed steps
+    tr = solver.trace[k_trace0:]
+    total_bytes = sum(step_bytes(n, s["k"], s["trials"]) for s in tr)
+    # dominant kernel: Gram pass (per-launch events; bytes are this rank's slab)
+    g_ms = [m for m, _ in launches]
+    g_by = [b for _, b in launches]
+    g_avg_ms = float(np.mean(g_ms)) if g_ms else float("nan")
+    g_avg_bytes = float(np.mean(g_by)) if g_by else float("nan")
+    g_gbs = g_avg_bytes / (g_avg_ms * 1e-3) / 1e9 if g_ms else float("nan")
+    gram_share = sum(g_ms) * 1e-3 / elapsed if g_ms else float("nan")
+
+    # JVP microbenchmark (single vector, 24 n bytes per launch)
+    sl = solver.dev.slab
+    v = solver.dev.vec()
+    out = solver.dev.vec()
+    gen = torch.Generator(device=device).manual_seed(1)
+    v[sl.own] = torch.randn(sl.nrows * N, generator=gen, device=device, dtype=torch.float64)
+    uu = solver.xb[solver.uJ]
+    for _ in range(3):
+        be.jvp(uu, v, out)
+    be.timer_start(_native.TIMER_JVP, args.jvp_reps)
+    for _ in range(args.jvp_reps):
+        be.jvp(uu, v, out)
+    jl = be.timer_collect(args.jvp_reps)
+    j_ms = float(np.median([m for m, _ in jl]))
+    j_gbs = jl[0][1] / (j_ms * 1e-3) / 1e9
+
+    config_key = f"bratu{N}_gnk_restart{args.restart}_{args.version}_ranks{world}"
+    traffic, traffic_src = pmc_traffic(config_key)
+    result = {
+        "metric": "GN-Krylov outer iters/sec + JVP HBM GB/s, Bratu 8192² fp64, 1/2/4/8 GPUs",
+        "value": steps_done / elapsed,
+        "unit": "outer_iters/s",
+        "n_gpus": world,
+        "steps": steps_done,
+        "warmup": args.warmup,
+        "ms_per_step": 1e3 * elapsed / max(steps_done, 1),
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic (Bratu u_true + 0.1 N(0,1), seed 42; ref:bratu_pde_test.py:22-36)",
+        "config": {"workload": f"bratu_{N}x{N}_gnk_krylov_dim{args.restart}", "grid": N, "unknowns": n,
+                   "krylow_restart": args.restart, "version": args.version, "ALPHA": 5, "LAMBDA": 10,
+                   "basis_k_range": [min(s["k"] for s in tr), max(s["k"] for s in tr)] if tr else None,
+                   "armijo_trials": int(sum(s["trials"] for s in tr)),
+                   "parallelism": f"slab{world}"},
+        "roofline": {"kernel": "k_gram (fp64 MFMA Gram pass of CholQR2, J V on the fly)", "bound": "hbm",
+                     "achieved": g_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": g_gbs / HBM_PEAK_GBS,
+                     "traffic": traffic, "traffic_source": traffic_src,
+                     "avg_launch_ms": g_avg_ms, "algorithmic_bytes_per_launch": g_avg_bytes,
+                     "launches": len(g_ms), "share_of_step_time": gram_share},
+        "jvp": {"kernel": "k_jvp (J(u) v, 5-point stencil)", "grid": N, "median_ms": j_ms, "GBs": j_gbs,
+                "frac_of_peak": j_gbs / HBM_PEAK_GBS, "algorithmic_bytes": jl[0][1]},
+        "step_algorithmic_GBs": total_bytes / elapsed / 1e9,
+    }
+    if rank == 0 and world == 1 and args.cpu_seconds > 0:
+        try:
+            result["cpu_baseline"] = cpu_baseline(N, args.cpu_seconds, args.version, args.restart)
+        except Exception as e:  # report, never hide
+            result["cpu_baseline"] = {"value": None, "error": repr(e)}
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

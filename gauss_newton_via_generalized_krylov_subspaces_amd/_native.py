@@ -17,6 +17,7 @@ import torch
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("GNK_LIB", os.path.join(_HERE, "libgnk.so"))
 GHOST = 2  # GNK_GHOST_ROWS
+TIMER_GRAM, TIMER_JVP = 1, 2  # GNK_TIMER_*
 
 _c_int, _c_i64, _c_dbl, _c_vp = ctypes.c_int, ctypes.c_int64, ctypes.c_double, ctypes.c_void_p
 
@@ -47,6 +48,8 @@ SIGNATURES = {
     "gnk_cg_update_xr": (_c_int, [_c_vp, _c_dbl, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp]),
     "gnk_cg_update_p": (_c_int, [_c_vp, _c_dbl, _c_int, _c_vp, _c_vp]),
     "gnk_probe_mfma_f64": (_c_int, [_c_vp, _c_vp, _c_int, _c_int]),
+    "gnk_timer_start": (_c_int, [_c_vp, _c_int, _c_int]),
+    "gnk_timer_collect": (_c_int, [_c_vp, ctypes.POINTER(_c_dbl), ctypes.POINTER(_c_dbl), _c_int]),
 }
 
 _LIB = None
@@ -193,6 +196,18 @@ class HipBackend:
 
     def cg_update_p(self, beta, first, z, p):
         self._call("gnk_cg_update_p", float(beta), int(bool(first)), _p(z), _p(p))
+
+    def timer_start(self, kernel_id, capacity):
+        self._chk(self.lib.gnk_timer_start(self.ctx, int(kernel_id), int(capacity)), "timer_start")
+
+    def timer_collect(self, capacity):
+        """-> list of (ms, algorithmic bytes) for each timed launch."""
+        ms = (_c_dbl * capacity)()
+        by = (_c_dbl * capacity)()
+        n = self.lib.gnk_timer_collect(self.ctx, ms, by, int(capacity))
+        if n < 0:
+            self._chk(n, "timer_collect")
+        return [(ms[i], by[i]) for i in range(n)]
 
     def probe_mfma(self, out, blocks, iters):
         self._call("gnk_probe_mfma_f64", _p(out), int(blocks), int(iters))

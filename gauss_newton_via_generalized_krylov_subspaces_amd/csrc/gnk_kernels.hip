@@ -25,6 +25,7 @@
 #include <cstdio>
 #include <cstring>
 #include <string>
+#include <vector>
 
 #include "../../include/gnk.h"
 
@@ -682,6 +683,11 @@ struct gnk_ctx {
   double* scratch = nullptr;
   int num_cus = 256;
   std::string err;
+  // per-launch timer (tooling, see gnk_timer_start)
+  int timer_kernel = 0;
+  int timer_count = 0;
+  std::vector<hipEvent_t> timer_ev;
+  std::vector<double> timer_bytes;
 };
 
 namespace {
@@ -734,6 +740,23 @@ void residual_rows(const gnk_ctx* ctx, int64_t& lr0, int64_t& nlr) {
   nlr = hi - lo;
 }
 
+// records an event pair around one launch of the timed kernel
+struct TimedLaunch {
+  gnk_ctx* ctx;
+  int slot = -1;
+  TimedLaunch(gnk_ctx* c, int kernel_id, double bytes) : ctx(c) {
+    if (c->timer_kernel == kernel_id && c->timer_count < int(c->timer_bytes.size())) {
+      slot = c->timer_count++;
+      c->timer_bytes[slot] = bytes;
+      (void)hipEventRecord(c->timer_ev[2 * slot], c->stream);
+    }
+  }
+  void done() {
+    if (slot >= 0) (void)hipEventRecord(ctx->timer_ev[2 * slot + 1], ctx->stream);
+    slot = -1;
+  }
+};
+
 int reduce(gnk_ctx* ctx, const double* partial, int nblk, int len, int stride, const int* is_max, double* out) {
   hipLaunchKernelGGL(k_reduce, dim3((len + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, ctx->stream, partial, nblk, len,
                      stride, is_max, out);
@@ -775,6 +798,7 @@ int gnk_ctx_create(int device, gnk_ctx** out) {
 
 void gnk_ctx_destroy(gnk_ctx* ctx) {
   if (!ctx) return;
+  for (hipEvent_t e : ctx->timer_ev) (void)hipEventDestroy(e);
   if (ctx->scratch) (void)hipFree(ctx->scratch);
   delete ctx;
 }
@@ -825,7 +849,9 @@ int64_t gnk_slab_len(const gnk_ctx* ctx) {
 int gnk_bratu_jvp(gnk_ctx* ctx, const double* u, const double* v, double* out) {
   if (!ready(ctx)) return -1;
   RowLaunch L = rows(ctx, G, ctx->geo.nrows, vec_of(ctx), 1 << 30);
+  TimedLaunch tl(ctx, GNK_TIMER_JVP, 24.0 * double(ctx->geo.nrows) * double(ctx->geo.N));
   DISPATCH_VEC(ctx, k_jvp, L, 0, u, v, out, ctx->geo, ctx->coef, L.lr0, L.nlr, 0);
+  tl.done();
   return check_launch(ctx, "bratu_jvp");
 }
 
@@ -967,8 +993,11 @@ int gnk_gram(gnk_ctx* ctx, const double* u, const double* V, int64_t ldv, int k,
   nblk = std::max<int64_t>(nblk, 1);
   const size_t per_group_pairs = rowsplit ? P : 4 * PPW;
   if (size_t(nblk) * groups * per_group_pairs * 256 > SCRATCH_DOUBLES) return fail(ctx, "gram: scratch too small");
+  // algorithmic bytes: k basis columns + u (+ r), each 8 bytes per owned point
+  TimedLaunch tl(ctx, GNK_TIMER_GRAM, 8.0 * double(nown) * double(k + 1 + (r ? 1 : 0)));
   hipLaunchKernelGGL(k_gram, dim3(unsigned(nblk), unsigned(groups)), dim3(BLOCK), lds, ctx->stream, u, V, ldv, k, rinv,
                      r, ctx->geo, ctx->coef, T, logT, KP, P, rowsplit, ntiles, ctx->scratch);
+  tl.done();
   int rc = check_launch(ctx, "gram");
   if (rc) return rc;
   (void)hipMemsetAsync(G_out, 0, size_t(KP) * KP * sizeof(double), ctx->stream);
@@ -1003,6 +1032,36 @@ int gnk_cg_update_p(gnk_ctx* ctx, double beta, int first, const double* z, doubl
   RowLaunch L = rows(ctx, G, ctx->geo.nrows, vec_of(ctx), 1 << 30);
   DISPATCH_VEC(ctx, k_cg_p, L, 0, beta, first, z, p, ctx->geo, L.lr0, L.nlr);
   return check_launch(ctx, "cg_update_p");
+}
+
+int gnk_timer_start(gnk_ctx* ctx, int kernel_id, int capacity) {
+  if (!ctx) return -1;
+  if (capacity < 0) return fail(ctx, "timer_start: capacity < 0");
+  while (int(ctx->timer_ev.size()) < 2 * capacity) {
+    hipEvent_t e;
+    if (hipEventCreate(&e) != hipSuccess) return fail(ctx, "timer_start: hipEventCreate failed", -2);
+    ctx->timer_ev.push_back(e);
+  }
+  ctx->timer_bytes.assign(capacity, 0.0);
+  ctx->timer_kernel = kernel_id;
+  ctx->timer_count = 0;
+  return 0;
+}
+
+int gnk_timer_collect(gnk_ctx* ctx, double* ms_out, double* bytes_out, int capacity) {
+  if (!ctx) return -1;
+  const int n = std::min(capacity, ctx->timer_count);
+  for (int i = 0; i < n; ++i) {
+    if (hipEventSynchronize(ctx->timer_ev[2 * i + 1]) != hipSuccess) return fail(ctx, "timer_collect: sync", -2);
+    float ms = 0.f;
+    if (hipEventElapsedTime(&ms, ctx->timer_ev[2 * i], ctx->timer_ev[2 * i + 1]) != hipSuccess)
+      return fail(ctx, "timer_collect: elapsed", -2);
+    ms_out[i] = ms;
+    bytes_out[i] = ctx->timer_bytes[i];
+  }
+  ctx->timer_kernel = 0;
+  ctx->timer_count = 0;
+  return n;
 }
 
 // tooling: fp64 MFMA issue-rate probe (not part of the solver)

@@ -122,6 +122,14 @@ int gnk_cg_update_xr(gnk_ctx* ctx, double alpha, const double* p, const double* 
 int gnk_cg_update_p(gnk_ctx* ctx, double beta, int first, const double* z, double* p);
 
 /* ---- tooling (not on the solver path) ----------------------------------- */
+/* Per-launch HIP-event timer for one kernel class (bench roofline): after
+ * gnk_timer_start, the next `capacity` launches of that kernel are bracketed by
+ * an event pair on the context's stream; gnk_timer_collect synchronises them and
+ * returns the count, the milliseconds and the algorithmic bytes of each launch. */
+#define GNK_TIMER_GRAM 1
+#define GNK_TIMER_JVP 2
+int gnk_timer_start(gnk_ctx* ctx, int kernel_id, int capacity);
+int gnk_timer_collect(gnk_ctx* ctx, double* ms_out, double* bytes_out, int capacity);
 /* back-to-back v_mfma_f64_16x16x4_f64 issue-rate probe: blocks x 256 threads,
  * 4 independent accumulators per wave, iters x 4 MFMAs per wave */
 int gnk_probe_mfma_f64(gnk_ctx* ctx, double* out, int blocks, int iters);

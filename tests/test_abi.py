@@ -1,0 +1,47 @@
+"""The C-ABI library loads and exports every symbol include/gnk.h declares (no GPU needed)."""
+import ctypes
+import os
+import re
+
+import pytest
+
+from gauss_newton_via_generalized_krylov_subspaces_amd import _native
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def header_symbols():
+    with open(os.path.join(ROOT, "include", "gnk.h")) as f:
+        text = f.read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(gnk_[a-z0-9_]+)\s*\(", text)))
+
+
+def test_library_exports_every_header_symbol():
+    if not os.path.exists(_native.LIB_PATH):
+        pytest.fail("libgnk.so is not built (run __graft_entry__.build())")
+    lib = ctypes.CDLL(_native.LIB_PATH)
+    syms = header_symbols()
+    assert len(syms) >= 20
+    missing = [s for s in syms if not hasattr(lib, s)]
+    assert not missing, missing
+
+
+def test_binding_table_matches_header():
+    assert sorted(_native.SIGNATURES) == header_symbols()
+
+
+def test_load_library_binds_and_reports_version():
+    lib = _native.load_library()
+    assert lib.gnk_abi_version() == 1
+    assert lib.gnk_gram_padded_dim(20, 1) == 32
+    assert lib.gnk_gram_padded_dim(16, 0) == 16
+    assert lib.gnk_gram_padded_dim(16, 1) == 32
+
+
+def test_no_cpu_fallback_without_gpu():
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    with pytest.raises(_native.NativeLibraryError):
+        _native.HipBackend(torch.device("cpu"))

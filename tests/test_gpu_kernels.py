@@ -1,0 +1,252 @@
+"""HIP kernels (through the C-ABI) against the CPU oracle / exact NumPy restatements.
+
+Tolerances: stencil kernels follow scipy's CSR summation order with
+-ffp-contract=off, so they agree with the oracle to a few ulps (checked at
+1e-13 relative to the operator scale); reductions differ only in summation order.
+"""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+from gauss_newton_via_generalized_krylov_subspaces_amd import _native  # noqa: E402
+from gauss_newton_via_generalized_krylov_subspaces_amd._device import BratuDevice  # noqa: E402
+from gauss_newton_via_generalized_krylov_subspaces_amd.bratu_pde_problem import BratuPdeProblem  # noqa: E402
+from gauss_newton_via_generalized_krylov_subspaces_amd.slab import Comm  # noqa: E402
+from oracle import gnk_oracle as O  # noqa: E402
+
+G = _native.GHOST
+
+
+def make(N, lam=10.0, alpha=5.0):
+    prob = BratuPdeProblem(N + 1, alpha, lam)
+    dev = BratuDevice(prob, Comm(single=True))
+    ref = O.BratuStencil(N, alpha, lam, prob.grid_resolution)
+    return prob, dev, ref
+
+
+def own(dev, t):
+    return t[dev.slab.own].cpu().numpy()
+
+
+def close(a, b, scale=None, rtol=1e-13):
+    scale = np.abs(b).max() if scale is None else scale
+    np.testing.assert_allclose(a, b, rtol=0, atol=rtol * max(scale, 1e-300))
+
+
+@pytest.mark.parametrize("N", [8, 25, 64, 1024])
+@pytest.mark.parametrize("lam", [10.0, 0.0])
+def test_operators_match_oracle(N, lam):
+    prob, dev, ref = make(N, lam)
+    rng = np.random.default_rng(N)
+    n = N * N
+    u = 0.3 * rng.standard_normal(n)
+    v = rng.standard_normal(n)
+    be = dev.backend
+    us, vs = dev.load(u), dev.load(v)
+    out = dev.vec()
+    be.jvp(us, vs, out)
+    close(own(dev, out), ref.jvp(u, v))
+    be.vjp(us, vs, out)
+    close(own(dev, out), ref.vjp(u, v))
+    be.forward(us, out)
+    close(own(dev, out), ref.pde_operator(u))
+    be.diag_jtj(us, out)
+    close(own(dev, out), ref.diag_jtj(u))
+    be.diag_jtj(us, out, reciprocal=True)
+    np.testing.assert_allclose(own(dev, out), 1.0 / ref.diag_jtj(u), rtol=1e-14)
+    y = ref.pde_operator(0.5 * u)
+    n2 = dev.scalar(1)
+    be.residual(us, dev.load(y), out, n2)
+    r_ref = y - ref.pde_operator(u)
+    close(own(dev, out), r_ref)
+    np.testing.assert_allclose(n2.item(), np.sum(r_ref ** 2), rtol=1e-12)
+
+
+def test_jvp_bitwise_vs_oracle_small():
+    """With the CSR summation order and no FMA contraction the stencil is bit-exact vs the oracle
+    except where exp() differs by an ulp (lambda = 0 removes exp)."""
+    prob, dev, ref = make(64, lam=0.0)
+    rng = np.random.default_rng(7)
+    v = rng.standard_normal(64 * 64)
+    out = dev.vec()
+    dev.backend.jvp(dev.load(np.zeros(64 * 64)), dev.load(v), out)
+    np.testing.assert_array_equal(own(dev, out), ref.jvp(np.zeros(64 * 64), v))
+    dev.backend.vjp(dev.load(np.zeros(64 * 64)), dev.load(v), out)
+    np.testing.assert_array_equal(own(dev, out), ref.vjp(np.zeros(64 * 64), v))
+
+
+@pytest.mark.parametrize("N,k", [(24, 1), (24, 7), (100, 33), (1024, 20), (25, 5)])
+def test_basis_kernels(N, k):
+    prob, dev, ref = make(N)
+    be = dev.backend
+    rng = np.random.default_rng(k)
+    L = dev.slab.length
+    V = be.zeros(k + 1, L)
+    Vh = rng.standard_normal((k + 1, N * N))
+    for j in range(k + 1):
+        V[j].copy_(dev.load(Vh[j]))
+    c = rng.standard_normal(k)
+    x = dev.vec()
+    be.gemv(V, k, be.to_device(c), x)
+    np.testing.assert_allclose(own(dev, x), c @ Vh[:k], rtol=1e-12, atol=1e-12 * np.abs(Vh).max() * k)
+    u = 0.3 * rng.standard_normal(N * N)
+    r = rng.standard_normal(N * N)
+    us, rs = dev.load(u), dev.load(r)
+    h = be.zeros(k)
+    g = V[k]
+    be.vjp_gemv_t(us, rs, V, k, g, h)
+    g_ref = -ref.vjp(u, r)
+    close(own(dev, g), g_ref)
+    np.testing.assert_allclose(h.cpu().numpy(), Vh[:k] @ g_ref, rtol=1e-11, atol=1e-11 * np.abs(g_ref).sum())
+    hh = rng.standard_normal(k)
+    st = be.zeros(2)
+    be.cgs_update(V, k, be.to_device(hh), g, st)
+    g2 = g_ref - hh @ Vh[:k]
+    np.testing.assert_allclose(own(dev, g), g2, rtol=1e-12, atol=1e-12 * np.abs(g2).max() * k)
+    np.testing.assert_allclose(st[0].item(), np.sum(g2 ** 2), rtol=1e-12)
+    assert st[1].item() == np.abs(own(dev, g)).max()
+    be.vec_stats(g, st)
+    np.testing.assert_allclose(st[0].item(), np.sum(own(dev, g) ** 2), rtol=1e-13)
+    be.vec_div(g, 3.0, x, False)
+    np.testing.assert_array_equal(own(dev, x), own(dev, g) / 3.0)
+    be.vec_axpy(us, 0.25, rs, x, True)
+    np.testing.assert_array_equal(own(dev, x), u + 0.25 * r)
+
+
+def test_cgs_max_propagates_nan():
+    prob, dev, ref = make(24)
+    be = dev.backend
+    V = be.zeros(2, dev.slab.length)
+    g = dev.load(np.where(np.arange(576) == 100, np.nan, 1e-12))
+    st = be.zeros(2)
+    be.cgs_update(V, 1, be.zeros(1), g, st)
+    assert np.isnan(st[1].item()) and np.isnan(st[0].item())
+
+
+@pytest.mark.parametrize("N,k,with_r,with_rinv", [(24, 1, False, False), (24, 5, True, True), (100, 20, False, False),
+                                                  (100, 20, True, True), (64, 47, True, True), (64, 70, True, False),
+                                                  (1024, 20, True, True)])
+def test_gram_mfma(N, k, with_r, with_rinv):
+    """W = [J V | r] @ RinvAug on fp64 MFMA vs an fp64 NumPy Gram (host BLAS)."""
+    prob, dev, ref = make(N)
+    be = dev.backend
+    rng = np.random.default_rng(N + k)
+    n = N * N
+    Vh = np.linalg.qr(rng.standard_normal((n, k)))[0].T.copy()
+    V = be.zeros(k, dev.slab.length)
+    for j in range(k):
+        V[j].copy_(dev.load(Vh[j]))
+    u = 0.3 * rng.standard_normal(n)
+    r = rng.standard_normal(n) * 1e3
+    kp = be.gram_dim(k, with_r)
+    W = np.zeros((n, kp))
+    for j in range(k):
+        W[:, j] = ref.jvp(u, Vh[j])
+    if with_r:
+        W[:, k] = r
+    Rinv = None
+    if with_rinv:
+        A = np.triu(rng.standard_normal((kp, kp))) + 3 * np.eye(kp)
+        A[k + (1 if with_r else 0):, :] = 0
+        A[:, k + (1 if with_r else 0):] = 0
+        if with_r:
+            A[k, :] = 0
+            A[:, k] = 0
+            A[k, k] = 1.0
+        Rinv = A
+        W = W @ A
+    Gref = W.T @ W
+    Gd = be.zeros(kp * kp)
+    be.gram(dev.load(u), V, k, None if Rinv is None else be.to_device(Rinv.reshape(-1)),
+            dev.load(r) if with_r else None, Gd)
+    Gdev = Gd.cpu().numpy().reshape(kp, kp)
+    scale = np.sqrt(np.outer(np.diag(Gref), np.diag(Gref))) + 1e-300
+    assert np.max(np.abs(Gdev - Gref) / scale) < 1e-13
+    np.testing.assert_array_equal(Gdev, Gdev.T)
+
+
+def test_gram_deterministic():
+    prob, dev, ref = make(512)
+    be = dev.backend
+    rng = np.random.default_rng(3)
+    k = 12
+    V = be.zeros(k, dev.slab.length)
+    for j in range(k):
+        V[j].copy_(dev.load(rng.standard_normal(512 * 512)))
+    u = dev.load(0.1 * rng.standard_normal(512 * 512))
+    r = dev.load(rng.standard_normal(512 * 512))
+    outs = []
+    for _ in range(3):
+        Gd = be.zeros(be.gram_dim(k, True) ** 2)
+        be.gram(u, V, k, None, r, Gd)
+        outs.append(Gd.cpu().numpy())
+    np.testing.assert_array_equal(outs[0], outs[1])
+    np.testing.assert_array_equal(outs[0], outs[2])
+
+
+@pytest.mark.parametrize("N", [24, 101, 512])
+def test_cg_matvec_matches_two_pass(N):
+    prob, dev, ref = make(N)
+    be = dev.backend
+    rng = np.random.default_rng(N)
+    n = N * N
+    u = 0.3 * rng.standard_normal(n)
+    p = rng.standard_normal(n)
+    us, ps = dev.load(u), dev.load(p)
+    d = dev.vec()
+    be.jdiag(us, d)
+    q = dev.vec()
+    pq = dev.scalar(1)
+    be.cg_matvec(d, ps, q, pq)
+    q_ref = ref.vjp(u, ref.jvp(u, p))
+    close(own(dev, q), q_ref, rtol=1e-12)
+    np.testing.assert_allclose(pq.item(), p @ q_ref, rtol=1e-12)
+
+
+def test_cg_updates():
+    prob, dev, ref = make(64)
+    be = dev.backend
+    rng = np.random.default_rng(5)
+    n = 64 * 64
+    p, q, x, r, dinv = (rng.standard_normal(n) for _ in range(5))
+    ps, qs, xs, rs, ds = (dev.load(a) for a in (p, q, x, r, dinv))
+    z = dev.vec()
+    out = dev.scalar(2)
+    be.cg_update_xr(0.7, ps, qs, xs, rs, ds, z, out)
+    r2 = r - 0.7 * q
+    np.testing.assert_array_equal(own(dev, xs), x + 0.7 * p)
+    np.testing.assert_array_equal(own(dev, rs), r2)
+    np.testing.assert_array_equal(own(dev, z), dinv * r2)
+    np.testing.assert_allclose(out.cpu().numpy(), [r2 @ r2, r2 @ (dinv * r2)], rtol=1e-12)
+    be.cg_update_p(0.3, False, z, ps)
+    np.testing.assert_array_equal(own(dev, ps), p * 0.3 + dinv * r2)
+
+
+def test_jvp_adjoint_and_linearity_8192():
+    """Size-independent properties at the benchmark grid: <J v, w> = <v, J^T w>; J(a v) = a J v."""
+    N = 8192
+    prob, dev, ref = make(N)
+    be = dev.backend
+    g = torch.Generator(device=be.device).manual_seed(0)
+    L = dev.slab.length
+
+    def rnd():
+        t = dev.vec()
+        t[dev.slab.own] = torch.randn(N * N, generator=g, device=be.device, dtype=torch.float64)
+        return t
+
+    u, v, w = rnd(), rnd(), rnd()
+    u.mul_(0.1)
+    jv, jtw = dev.vec(), dev.vec()
+    be.jvp(u, v, jv)
+    be.vjp(u, w, jtw)
+    a = torch.dot(jv[dev.slab.own], w[dev.slab.own]).item()
+    b = torch.dot(v[dev.slab.own], jtw[dev.slab.own]).item()
+    assert abs(a - b) <= 1e-11 * (abs(a) + torch.linalg.norm(jv).item() * torch.linalg.norm(w).item() * 1e-3)
+    v2 = v * 2.0
+    jv2 = dev.vec()
+    be.jvp(u, v2, jv2)
+    assert torch.equal(jv2, jv * 2.0)
+    assert L == (N + 2 * G) * N
