@@ -36,7 +36,7 @@ namespace {
 constexpr int BLOCK = 256;
 constexpr int MAX_RED_BLOCKS = 4096;     // cap on per-block partials of a reduction
 constexpr int KC = 32;                   // columns per chunk in V^T g
-constexpr int PPW = 10;                  // Gram accumulator tiles per wave
+constexpr int PPW_MAX = 10;              // Gram accumulator tiles per wave (pair-split mode)
 constexpr size_t SCRATCH_DOUBLES = size_t(16) << 20;   // 128 MiB arena
 
 typedef double d2 __attribute__((ext_vector_type(2)));
@@ -161,17 +161,41 @@ template <int VEC>
 __global__ __launch_bounds__(BLOCK) void k_jvp(const double* __restrict__ u, const double* __restrict__ v,
                                                double* __restrict__ out, Geo geo, Coef c, int64_t lr0,
                                                int64_t nlr, int transpose) {
+  const int lane = threadIdx.x & 63;
   ROW_LOOP_BEGIN(VEC)
-#pragma unroll
-  for (int q = 0; q < VEC; ++q) {
-    const int64_t i = li + q;
-    const int64_t y = iy + q;
-    if (y >= N) break;
-    const bool hw = y > 0, he = y < N - 1;
-    const double d = jdiag(c, u[i]);
-    const double vn = v[i - N], vs = v[i + N], vc = v[i];
-    const double vw = hw ? v[i - 1] : 0.0, ve = he ? v[i + 1] : 0.0;
-    out[i] = transpose ? vjp_pt(c, d, vn, vw, hw, vc, ve, he, vs) : jvp_pt(c, d, vn, vw, hw, vc, ve, he, vs);
+  if (VEC == 2 && iy + 1 < N) {
+    // two points per lane: 16-B loads of u, v and the rows above/below; the in-row
+    // neighbours come from the adjacent lanes (lane 0 / 63 load their outer one)
+    const d2 uc = *reinterpret_cast<const d2*>(u + li);
+    const d2 vc = *reinterpret_cast<const d2*>(v + li);
+    const d2 vn = *reinterpret_cast<const d2*>(v + li - N);
+    const d2 vs = *reinterpret_cast<const d2*>(v + li + N);
+    const bool hw = iy > 0, he = iy + 2 < N;
+    double vw = __shfl_up(vc.y, 1);
+    double ve = __shfl_down(vc.x, 1);
+    if (lane == 0) vw = hw ? v[li - 1] : 0.0;
+    if (lane == 63 || iy + 2 >= N) ve = he ? v[li + 2] : 0.0;
+    const double d0 = jdiag(c, uc.x), d1 = jdiag(c, uc.y);
+    d2 o;
+    if (transpose) {
+      o.x = vjp_pt(c, d0, vn.x, vw, hw, vc.x, vc.y, true, vs.x);
+      o.y = vjp_pt(c, d1, vn.y, vc.x, true, vc.y, ve, he, vs.y);
+    } else {
+      o.x = jvp_pt(c, d0, vn.x, vw, hw, vc.x, vc.y, true, vs.x);
+      o.y = jvp_pt(c, d1, vn.y, vc.x, true, vc.y, ve, he, vs.y);
+    }
+    *reinterpret_cast<d2*>(out + li) = o;
+  } else {
+    for (int q = 0; q < VEC; ++q) {
+      const int64_t i = li + q;
+      const int64_t y = iy + q;
+      if (y >= N) break;
+      const bool hw = y > 0, he = y < N - 1;
+      const double d = jdiag(c, u[i]);
+      const double vn = v[i - N], vs = v[i + N], vc = v[i];
+      const double vw = hw ? v[i - 1] : 0.0, ve = he ? v[i + 1] : 0.0;
+      out[i] = transpose ? vjp_pt(c, d, vn, vw, hw, vc, ve, he, vs) : jvp_pt(c, d, vn, vw, hw, vc, ve, he, vs);
+    }
   }
   ROW_LOOP_END
 }
@@ -505,6 +529,7 @@ __device__ __forceinline__ void pair_ab(int p, int nb, int& a, int& b) {
 // Pass 1 (rinv == nullptr): W = J V.  Pass 2: W = [J V | r] @ RinvAug (RinvAug kp x kp).
 // rowsplit = 1: each wave accumulates all P pair tiles over its quarter of the rows.
 // rowsplit = 0: blockIdx.y = pair group; wave w owns pairs grp*4*PPW + w*PPW + q over all rows.
+template <int PPW>
 __global__ __launch_bounds__(BLOCK) void k_gram(const double* __restrict__ u, const double* __restrict__ V,
                                                 int64_t ldv, int k, const double* __restrict__ rinv,
                                                 const double* __restrict__ r, Geo geo, Coef c, int T, int logT,
@@ -513,13 +538,12 @@ __global__ __launch_bounds__(BLOCK) void k_gram(const double* __restrict__ u, co
   extern __shared__ __attribute__((aligned(16))) double lds[];
   const int S = KP + 1;
   double* Wt = lds;
-  double* dg = lds + T * S;
-  int* fl = reinterpret_cast<int*>(dg + T);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int nb = KP / 16;
   const int64_t N = geo.N;
   const int64_t nown = geo.nrows * N;
   const int64_t base = int64_t(G) * N;
+  const int K1 = k + (r ? 1 : 0);
 
   int pa[PPW], pb[PPW];
   bool pv[PPW];
@@ -536,39 +560,48 @@ __global__ __launch_bounds__(BLOCK) void k_gram(const double* __restrict__ u, co
   const int rq = rowsplit ? T / 4 : T;
   const int rbeg = rowsplit ? wave * rq : 0;
 
+  // padding columns [K1, KP) stay zero for the whole launch (the pass-2 transform
+  // writes zeros there too: RinvAug is zero outside its k(+1) leading block)
+  for (int idx = tid; idx < T * S; idx += BLOCK) Wt[idx] = 0.0;
+  __syncthreads();
+
+  // fill geometry: thread -> (row t, column phase jh); a wave covers 64 consecutive rows
+  // of one column, so every load below is a coalesced 512-B wave access.
+  const int tpr = BLOCK >> logT;        // threads per row
+  const int t = tid & (T - 1);
+  const int jh = tid >> logT;
+  constexpr int B = 6;                  // columns per batch: 5 B loads in flight per thread
+
   for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-    const int64_t e0 = tile << logT;
-    for (int t = tid; t < T; t += BLOCK) {
-      const int64_t e = e0 + t;
-      int f = 0;
-      double dd = 0.0;
-      if (e < nown) {
-        const int64_t iy = e % N;
-        f = 4 | (iy > 0 ? 1 : 0) | (iy < N - 1 ? 2 : 0);
-        dd = jdiag(c, u[base + e]);
-      }
-      fl[t] = f;
-      dg[t] = dd;
-    }
-    __syncthreads();
-    const int ncol = KP;
-    for (int idx = tid; idx < T * ncol; idx += BLOCK) {
-      const int t = idx & (T - 1);
-      const int j = idx >> logT;
-      const int f = fl[t];
-      double w = 0.0;
-      if (f & 4) {
-        const int64_t i = base + e0 + t;
-        if (j < k) {
+    const int64_t e = (tile << logT) + t;
+    const bool valid = e < nown;
+    const int64_t i = base + (valid ? e : 0);
+    const int64_t iy = valid ? e % N : 0;
+    const bool hw = valid && iy > 0, he = valid && iy < N - 1;
+    const double dd = valid ? jdiag(c, u[i]) : 0.0;
+    for (int j0 = jh; j0 < K1; j0 += B * tpr) {
+      double vn[B], vw[B], vc[B], ve[B], vs[B];
+#pragma unroll
+      for (int q = 0; q < B; ++q) {
+        const int j = j0 + q * tpr;
+        vn[q] = vw[q] = vc[q] = ve[q] = vs[q] = 0.0;
+        if (valid && j < k) {
           const double* v = V + j * ldv;
-          const bool hw = f & 1, he = f & 2;
-          const double vw = hw ? v[i - 1] : 0.0, ve = he ? v[i + 1] : 0.0;
-          w = jvp_pt(c, dg[t], v[i - N], vw, hw, v[i], ve, he, v[i + N]);
-        } else if (j == k && r) {
-          w = r[i];
+          vn[q] = v[i - N];
+          vc[q] = v[i];
+          vs[q] = v[i + N];
+          if (hw) vw[q] = v[i - 1];
+          if (he) ve[q] = v[i + 1];
+        } else if (valid && j == k && r) {
+          vc[q] = r[i];
         }
       }
-      Wt[t * S + j] = w;
+#pragma unroll
+      for (int q = 0; q < B; ++q) {
+        const int j = j0 + q * tpr;
+        if (j < K1) Wt[t * S + j] = (j < k) ? (valid ? jvp_pt(c, dd, vn[q], vw[q], hw, vc[q], ve[q], he, vs[q]) : 0.0)
+                                            : vc[q];
+      }
     }
     __syncthreads();
     if (rinv) {
@@ -640,7 +673,7 @@ __global__ __launch_bounds__(BLOCK) void k_gram(const double* __restrict__ u, co
 __global__ __launch_bounds__(BLOCK) void k_gram_reduce(const double* __restrict__ partial, int nblk, int P,
                                                        int rowsplit, int KP, double* __restrict__ Gout) {
   const int nb = KP / 16;
-  const int PG = rowsplit ? P : 4 * PPW;
+  const int PG = rowsplit ? P : 4 * PPW_MAX;
   for (int idx = blockIdx.x * BLOCK + threadIdx.x; idx < P * 256; idx += gridDim.x * BLOCK) {
     const int p = idx >> 8, li = idx & 255, lane = li >> 2, i = li & 3;
     const int grp = p / PG, pl = p % PG;
@@ -975,14 +1008,14 @@ int gnk_gram(gnk_ctx* ctx, const double* u, const double* V, int64_t ldv, int k,
   if (rinv && ldr != KP) return fail(ctx, "gram: rinv must be the kp x kp augmented inverse (ldr == kp)");
   const int nb = KP / 16;
   const int P = nb * (nb + 1) / 2;
-  const int rowsplit = P <= PPW ? 1 : 0;
-  const int groups = rowsplit ? 1 : (P + 4 * PPW - 1) / (4 * PPW);
+  const int rowsplit = P <= PPW_MAX ? 1 : 0;
+  const int groups = rowsplit ? 1 : (P + 4 * PPW_MAX - 1) / (4 * PPW_MAX);
   // tile rows: LDS tile <= ~40 KB for small KP (several WGs per CU), 64 rows otherwise
   int T = 256;
   while (T > 64 && size_t(T) * (KP + 1) * 8 > 40 * 1024) T >>= 1;
   int logT = 0;
   while ((1 << logT) < T) ++logT;
-  size_t lds = size_t(T) * (KP + 1) * 8 + size_t(T) * 8 + size_t(T) * 4;
+  size_t lds = size_t(T) * (KP + 1) * 8;
   lds = (lds + 15) & ~size_t(15);
   if (rowsplit && size_t(P) * 256 > size_t(T) * (KP + 1)) return fail(ctx, "gram: reduction staging does not fit");
   if (lds > 160 * 1024) return fail(ctx, "gram: k too large for the LDS tile");
@@ -991,12 +1024,19 @@ int gnk_gram(gnk_ctx* ctx, const double* u, const double* V, int64_t ldv, int k,
   const int wg_per_cu = std::max<int>(1, std::min<int>(4, int((160 * 1024) / lds)));
   int64_t nblk = std::min<int64_t>(ntiles, int64_t(ctx->num_cus) * wg_per_cu);
   nblk = std::max<int64_t>(nblk, 1);
-  const size_t per_group_pairs = rowsplit ? P : 4 * PPW;
+  const size_t per_group_pairs = rowsplit ? P : 4 * PPW_MAX;
   if (size_t(nblk) * groups * per_group_pairs * 256 > SCRATCH_DOUBLES) return fail(ctx, "gram: scratch too small");
   // algorithmic bytes: k basis columns + u (+ r), each 8 bytes per owned point
   TimedLaunch tl(ctx, GNK_TIMER_GRAM, 8.0 * double(nown) * double(k + 1 + (r ? 1 : 0)));
-  hipLaunchKernelGGL(k_gram, dim3(unsigned(nblk), unsigned(groups)), dim3(BLOCK), lds, ctx->stream, u, V, ldv, k, rinv,
-                     r, ctx->geo, ctx->coef, T, logT, KP, P, rowsplit, ntiles, ctx->scratch);
+#define GRAM_LAUNCH(PP)                                                                                    \
+  hipLaunchKernelGGL(k_gram<PP>, dim3(unsigned(nblk), unsigned(groups)), dim3(BLOCK), lds, ctx->stream, u, V, ldv, \
+                     k, rinv, r, ctx->geo, ctx->coef, T, logT, KP, P, rowsplit, ntiles, ctx->scratch)
+  if (!rowsplit) GRAM_LAUNCH(PPW_MAX);
+  else if (P == 1) GRAM_LAUNCH(1);
+  else if (P <= 3) GRAM_LAUNCH(3);
+  else if (P <= 6) GRAM_LAUNCH(6);
+  else GRAM_LAUNCH(PPW_MAX);
+#undef GRAM_LAUNCH
   tl.done();
   int rc = check_launch(ctx, "gram");
   if (rc) return rc;
