@@ -23,6 +23,7 @@
 #include <cmath>
 #include <cstdint>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -34,8 +35,7 @@
 namespace {
 
 constexpr int BLOCK = 256;
-constexpr int MAX_RED_BLOCKS = 4096;     // cap on per-block partials of a reduction
-constexpr int KC = 32;                   // columns per chunk in V^T g
+constexpr int MAX_RED_BLOCKS = 1 << 20;  // cap on per-block partials of a reduction
 constexpr int PPW_MAX = 10;              // Gram accumulator tiles per wave (pair-split mode)
 constexpr size_t SCRATCH_DOUBLES = size_t(16) << 20;   // 128 MiB arena
 
@@ -206,20 +206,44 @@ __global__ __launch_bounds__(BLOCK) void k_forward(const double* __restrict__ x,
                                                    int64_t nlr, double* __restrict__ partial) {
   // out = pde_operator(x) (y == nullptr) or y - pde_operator(x); partial: sum out^2 over owned rows
   __shared__ double sh[BLOCK / 64];
+  const int lane = threadIdx.x & 63;
   double acc[1] = {0.0};
   ROW_LOOP_BEGIN(VEC)
   const bool owned = lr >= G && lr < G + geo.nrows;
-#pragma unroll
-  for (int q = 0; q < VEC; ++q) {
-    const int64_t i = li + q;
-    const int64_t yy = iy + q;
-    if (yy >= N) break;
-    const bool hw = yy > 0, he = yy < N - 1;
-    const double xw = hw ? x[i - 1] : 0.0, xe = he ? x[i + 1] : 0.0;
-    const double f = fwd_pt(c, x[i - N], xw, hw, x[i], xe, he, x[i + N]);
-    const double r = y ? y[i] - f : f;
-    out[i] = r;
-    if (owned) acc[0] += r * r;
+  if (VEC == 2 && iy + 1 < N) {
+    const d2 xc = *reinterpret_cast<const d2*>(x + li);
+    const d2 xn = *reinterpret_cast<const d2*>(x + li - N);
+    const d2 xs = *reinterpret_cast<const d2*>(x + li + N);
+    const bool hw = iy > 0, he = iy + 2 < N;
+    double xw = __shfl_up(xc.y, 1);
+    double xe = __shfl_down(xc.x, 1);
+    if (lane == 0) xw = hw ? x[li - 1] : 0.0;
+    if (lane == 63 || iy + 2 >= N) xe = he ? x[li + 2] : 0.0;
+    d2 f;
+    f.x = fwd_pt(c, xn.x, xw, hw, xc.x, xc.y, true, xs.x);
+    f.y = fwd_pt(c, xn.y, xc.x, true, xc.y, xe, he, xs.y);
+    if (y) {
+      const d2 yy = *reinterpret_cast<const d2*>(y + li);
+      f.x = yy.x - f.x;
+      f.y = yy.y - f.y;
+    }
+    *reinterpret_cast<d2*>(out + li) = f;
+    if (owned) {
+      acc[0] += f.x * f.x;
+      acc[0] += f.y * f.y;
+    }
+  } else {
+    for (int q = 0; q < VEC; ++q) {
+      const int64_t i = li + q;
+      const int64_t yy = iy + q;
+      if (yy >= N) break;
+      const bool hw = yy > 0, he = yy < N - 1;
+      const double xw = hw ? x[i - 1] : 0.0, xe = he ? x[i + 1] : 0.0;
+      const double f = fwd_pt(c, x[i - N], xw, hw, x[i], xe, he, x[i + N]);
+      const double rr = y ? y[i] - f : f;
+      out[i] = rr;
+      if (owned) acc[0] += rr * rr;
+    }
   }
   ROW_LOOP_END
   if (partial) block_sum_store<1>(acc, 1, partial + (blockIdx.y * gridDim.x + blockIdx.x), sh);
@@ -273,36 +297,63 @@ __global__ __launch_bounds__(BLOCK) void k_gemv(const double* __restrict__ V, in
   ROW_LOOP_END
 }
 
-// g = -(J^T r) on owned rows (chunk 0 stores it), h[j0 + j] partial = V_j . g
-template <int VEC>
+// g = -(J^T r) on owned rows (chunk 0 stores it), h[j0 + j] partial = V_j . g.
+// KCT columns per chunk (compile time): every V load is unconditional (clamped column),
+// surplus accumulators are discarded by the block reduction (no loads under a branch).
+template <int VEC, int KCT>
 __global__ __launch_bounds__(BLOCK) void k_vjp_gemv_t(const double* __restrict__ u, const double* __restrict__ r,
                                                       const double* __restrict__ V, int64_t ldv, int k,
                                                       double* __restrict__ g, Geo geo, Coef c, int64_t lr0,
                                                       int64_t nlr, double* __restrict__ partial) {
-  __shared__ double sh[(BLOCK / 64) * KC];
-  const int j0 = blockIdx.z * KC;
-  const int kc = min(KC, k - j0);
-  double acc[KC];
+  __shared__ double sh[(BLOCK / 64) * KCT];
+  const int lane = threadIdx.x & 63;
+  const int j0 = blockIdx.z * KCT;
+  const int kc = max(0, min(KCT, k - j0));
+  const int jmax = max(k - 1, 0);
+  double acc[KCT];
 #pragma unroll
-  for (int j = 0; j < KC; ++j) acc[j] = 0.0;
+  for (int j = 0; j < KCT; ++j) acc[j] = 0.0;
   ROW_LOOP_BEGIN(VEC)
+  if (VEC == 2 && iy + 1 < N) {
+    const d2 uc = *reinterpret_cast<const d2*>(u + li);
+    const d2 rc = *reinterpret_cast<const d2*>(r + li);
+    const d2 rn = *reinterpret_cast<const d2*>(r + li - N);
+    const d2 rs = *reinterpret_cast<const d2*>(r + li + N);
+    const bool hw = iy > 0, he = iy + 2 < N;
+    double rw = __shfl_up(rc.y, 1);
+    double re = __shfl_down(rc.x, 1);
+    if (lane == 0) rw = hw ? r[li - 1] : 0.0;
+    if (lane == 63 || iy + 2 >= N) re = he ? r[li + 2] : 0.0;
+    const double g0 = -vjp_pt(c, jdiag(c, uc.x), rn.x, rw, hw, rc.x, rc.y, true, rs.x);
+    const double g1 = -vjp_pt(c, jdiag(c, uc.y), rn.y, rc.x, true, rc.y, re, he, rs.y);
+    if (blockIdx.z == 0) *reinterpret_cast<d2*>(g + li) = d2{g0, g1};
+    if (k > 0) {
 #pragma unroll
-  for (int q = 0; q < VEC; ++q) {
-    const int64_t i = li + q;
-    const int64_t yy = iy + q;
-    if (yy >= N) break;
-    const bool hw = yy > 0, he = yy < N - 1;
-    const double d = jdiag(c, u[i]);
-    const double rw = hw ? r[i - 1] : 0.0, re = he ? r[i + 1] : 0.0;
-    const double gi = -vjp_pt(c, d, r[i - N], rw, hw, r[i], re, he, r[i + N]);
-    if (blockIdx.z == 0) g[i] = gi;
+      for (int j = 0; j < KCT; ++j) {
+        const d2 vv = *reinterpret_cast<const d2*>(V + min(j0 + j, jmax) * ldv + li);
+        acc[j] = acc[j] + vv.x * g0;
+        acc[j] = acc[j] + vv.y * g1;
+      }
+    }
+  } else {
+    for (int q = 0; q < VEC; ++q) {
+      const int64_t i = li + q;
+      const int64_t yy = iy + q;
+      if (yy >= N) break;
+      const bool hw = yy > 0, he = yy < N - 1;
+      const double d = jdiag(c, u[i]);
+      const double rw = hw ? r[i - 1] : 0.0, re = he ? r[i + 1] : 0.0;
+      const double gi = -vjp_pt(c, d, r[i - N], rw, hw, r[i], re, he, r[i + N]);
+      if (blockIdx.z == 0) g[i] = gi;
+      if (k > 0) {
 #pragma unroll
-    for (int j = 0; j < KC; ++j)
-      if (j < kc) acc[j] = acc[j] + V[(j0 + j) * ldv + i] * gi;
+        for (int j = 0; j < KCT; ++j) acc[j] = acc[j] + V[min(j0 + j, jmax) * ldv + i] * gi;
+      }
+    }
   }
   ROW_LOOP_END
   const int nblk = gridDim.x * gridDim.y;
-  block_sum_store<KC>(acc, kc, partial + (size_t(blockIdx.z) * nblk + blockIdx.y * gridDim.x + blockIdx.x) * KC, sh);
+  block_sum_store<KCT>(acc, kc, partial + (size_t(blockIdx.z) * nblk + blockIdx.y * gridDim.x + blockIdx.x) * KCT, sh);
 }
 
 // g -= V[:, :k] @ h ; partial {sum g^2, max|g|}
@@ -483,28 +534,43 @@ __global__ __launch_bounds__(BLOCK) void k_cg_p(double beta, int first, const do
 }
 
 // ---------------------------------------------------------------- deterministic partial reduction
-// out[j] = sum_b partial[b * stride + j], b ascending; mode 1 = max (NaN-propagating)
+// out[j] = sum over b of partial[b * stride + j] (mode is_max[j]: NaN-propagating max).
+// One block per output; thread t folds b = t, t + 256, ... in order, then a fixed tree:
+// the summation order depends only on nblk, so results are bitwise reproducible.
 __global__ __launch_bounds__(BLOCK) void k_reduce(const double* __restrict__ partial, int nblk, int len,
                                                   int stride, const int* __restrict__ is_max, double* out) {
-  for (int j = blockIdx.x * BLOCK + threadIdx.x; j < len; j += gridDim.x * BLOCK) {
-    const bool mx = is_max ? is_max[j] != 0 : false;
-    double s = partial[j];
-    for (int b = 1; b < nblk; ++b) {
-      const double v = partial[size_t(b) * stride + j];
-      s = mx ? nan_max(s, v) : s + v;
-    }
-    out[j] = s;
+  __shared__ double sh[BLOCK];
+  const int j = blockIdx.x;
+  if (j >= len) return;
+  const bool mx = is_max ? is_max[j] != 0 : false;
+  double s = 0.0;
+  bool any = false;
+  for (int b = threadIdx.x; b < nblk; b += BLOCK) {
+    const double v = partial[size_t(b) * stride + j];
+    s = !any ? v : (mx ? nan_max(s, v) : s + v);
+    any = true;
   }
+  if (!any) s = mx ? -1.0 : 0.0;     // empty slot: identity (max over |x| >= 0)
+  sh[threadIdx.x] = s;
+  __syncthreads();
+  for (int w = BLOCK / 2; w > 0; w >>= 1) {
+    if (threadIdx.x < w) {
+      const double a = sh[threadIdx.x], bb = sh[threadIdx.x + w];
+      sh[threadIdx.x] = mx ? nan_max(a, bb) : a + bb;
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) out[j] = mx ? (sh[0] < 0.0 ? 0.0 : sh[0]) : sh[0];
 }
 
 // sum-over-chunks layout used by k_vjp_gemv_t: partial[(z * nblk + b) * KC + j]
 __global__ __launch_bounds__(BLOCK) void k_reduce_chunks(const double* __restrict__ partial, int nblk, int k,
-                                                         double* out) {
+                                                         int kct, double* out) {
   for (int jj = blockIdx.x * BLOCK + threadIdx.x; jj < k; jj += gridDim.x * BLOCK) {
-    const int z = jj / KC, j = jj % KC;
-    const double* p = partial + size_t(z) * nblk * KC + j;
+    const int z = jj / kct, j = jj % kct;
+    const double* p = partial + size_t(z) * nblk * kct + j;
     double s = p[0];
-    for (int b = 1; b < nblk; ++b) s += p[size_t(b) * KC];
+    for (int b = 1; b < nblk; ++b) s += p[size_t(b) * kct];
     out[jj] = s;
   }
 }
@@ -543,7 +609,6 @@ __global__ __launch_bounds__(BLOCK) void k_gram(const double* __restrict__ u, co
   const int64_t N = geo.N;
   const int64_t nown = geo.nrows * N;
   const int64_t base = int64_t(G) * N;
-  const int K1 = k + (r ? 1 : 0);
 
   int pa[PPW], pb[PPW];
   bool pv[PPW];
@@ -563,6 +628,10 @@ __global__ __launch_bounds__(BLOCK) void k_gram(const double* __restrict__ u, co
   // padding columns [K1, KP) stay zero for the whole launch (the pass-2 transform
   // writes zeros there too: RinvAug is zero outside its k(+1) leading block)
   for (int idx = tid; idx < T * S; idx += BLOCK) Wt[idx] = 0.0;
+  // RinvAug staged once per launch behind the tile when it fits (KP <= 64)
+  double* rinv_lds = (rinv && KP <= 64) ? lds + T * S : nullptr;
+  if (rinv_lds)
+    for (int idx = tid; idx < KP * KP; idx += BLOCK) rinv_lds[idx] = rinv[idx];
   __syncthreads();
 
   // fill geometry: thread -> (row t, column phase jh); a wave covers 64 consecutive rows
@@ -573,40 +642,50 @@ __global__ __launch_bounds__(BLOCK) void k_gram(const double* __restrict__ u, co
   constexpr int B = 6;                  // columns per batch: 5 B loads in flight per thread
 
   for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    // Branch-free fill: every load is unconditional (clamped address; ghost rows and
+    // the +-1 neighbours are always inside the slab) and masked afterwards with selects,
+    // so all 5*B loads of a batch are in flight together (a load under a runtime branch
+    // makes hipcc drain vmcnt at the join).
     const int64_t e = (tile << logT) + t;
     const bool valid = e < nown;
-    const int64_t i = base + (valid ? e : 0);
-    const int64_t iy = valid ? e % N : 0;
-    const bool hw = valid && iy > 0, he = valid && iy < N - 1;
-    const double dd = valid ? jdiag(c, u[i]) : 0.0;
-    for (int j0 = jh; j0 < K1; j0 += B * tpr) {
+    const int64_t i = base + (valid ? e : nown - 1);
+    const int64_t iy = (valid ? e : nown - 1) % N;
+    const bool hw = iy > 0, he = iy < N - 1;
+    const double uu = u[i];
+    double dd = 0.0;
+    bool have_dd = false;
+    for (int j0 = jh; j0 < k; j0 += B * tpr) {
       double vn[B], vw[B], vc[B], ve[B], vs[B];
 #pragma unroll
       for (int q = 0; q < B; ++q) {
-        const int j = j0 + q * tpr;
-        vn[q] = vw[q] = vc[q] = ve[q] = vs[q] = 0.0;
-        if (valid && j < k) {
-          const double* v = V + j * ldv;
-          vn[q] = v[i - N];
-          vc[q] = v[i];
-          vs[q] = v[i + N];
-          if (hw) vw[q] = v[i - 1];
-          if (he) ve[q] = v[i + 1];
-        } else if (valid && j == k && r) {
-          vc[q] = r[i];
-        }
+        const int j = min(j0 + q * tpr, k - 1);
+        const double* v = V + j * ldv + i;
+        vn[q] = v[-N];
+        vw[q] = v[-1];
+        vc[q] = v[0];
+        ve[q] = v[1];
+        vs[q] = v[N];
+      }
+      if (!have_dd) {
+        dd = jdiag(c, uu);
+        have_dd = true;
       }
 #pragma unroll
       for (int q = 0; q < B; ++q) {
         const int j = j0 + q * tpr;
-        if (j < K1) Wt[t * S + j] = (j < k) ? (valid ? jvp_pt(c, dd, vn[q], vw[q], hw, vc[q], ve[q], he, vs[q]) : 0.0)
-                                            : vc[q];
+        const double w = jvp_pt(c, dd, vn[q], hw ? vw[q] : 0.0, hw, vc[q], he ? ve[q] : 0.0, he, vs[q]);
+        if (j < k) Wt[t * S + j] = valid ? w : 0.0;
       }
+    }
+    if (r && (k % tpr) == jh) {
+      const double rv = r[i];
+      Wt[t * S + k] = valid ? rv : 0.0;
     }
     __syncthreads();
     if (rinv) {
       // in-place W <- W @ RinvAug; column blocks descending so each block reads only
       // not-yet-overwritten blocks a <= cb. Rows split over the 4 waves.
+      const double* rv = rinv_lds ? rinv_lds : rinv;
       const int rq4 = T / 4;
       for (int c16 = wave * rq4; c16 < (wave + 1) * rq4; c16 += 16) {
         for (int cb = nb - 1; cb >= 0; --cb) {
@@ -616,7 +695,7 @@ __global__ __launch_bounds__(BLOCK) void k_gram(const double* __restrict__ u, co
             for (int ks = 0; ks < 4; ++ks) {
               const int kk = ab * 16 + ks * 4 + (lane >> 4);
               const double a = Wt[(c16 + (lane & 15)) * S + kk];
-              const double b = rinv[kk * KP + cb * 16 + (lane & 15)];
+              const double b = rv[kk * KP + cb * 16 + (lane & 15)];
               qv = mfma64(a, b, qv);
             }
           }
@@ -667,6 +746,164 @@ __global__ __launch_bounds__(BLOCK) void k_gram(const double* __restrict__ u, co
       }
     }
   }
+}
+
+// Wave-independent Gram pass (KP <= 64).  Every wave streams its own 64-row chunks:
+//   lane = row, one basis column per load instruction (the column base is wave-uniform and
+//   lives in SGPRs; the three row offsets i-N, i, i+N are 32-bit VGPRs shared by every column,
+//   so a load costs no address arithmetic), the J V stencil in registers with the row-edge
+//   masks folded into the coefficients, then the wave's private LDS transpose tile
+//   [64 rows][KP] -> (pass 2: in-place W <- W RinvAug on MFMA) -> Gram MFMAs accumulating
+//   all P pair tiles in registers.  No workgroup barrier inside the chunk loop (a wave's LDS
+//   accesses are processed in issue order), so one wave's loads overlap another's MFMAs.
+
+typedef unsigned int u2v __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ double bld(__amdgpu_buffer_rsrc_t rs, unsigned off) {
+  return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rs, off, 0, 0));
+}
+
+template <int PPW, int BC, int CHT>
+__global__ __launch_bounds__(BLOCK) void k_gram_w(const double* __restrict__ u, const double* __restrict__ V,
+                                                  int64_t ldv, int k, const double* __restrict__ rinv,
+                                                  const double* __restrict__ r, Geo geo, Coef c, int KP, int P,
+                                                  int64_t nchunks, double* __restrict__ partial, int dbg) {
+  // CHT rows per wave chunk; a lane holds 2 consecutive rows (16-B loads); LPC = CHT/2 lanes
+  // cover one column of the chunk, so one load instruction covers CG = 64/LPC columns.
+  constexpr int LPC = CHT / 2, CG = 64 / LPC;
+  extern __shared__ __attribute__((aligned(16))) double lds[];
+  const int S = KP + 1;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int nwave = blockDim.x >> 6;
+  const int nb = KP / 16;
+  double* Wt = lds + wave * (CHT * S);
+  double* rinv_lds = rinv ? lds + nwave * CHT * S : nullptr;
+  const int64_t N = geo.N;
+  const int64_t nown = geo.nrows * N;
+  const int64_t base = int64_t(G) * N;
+  const int K1 = k + (r ? 1 : 0);
+
+  int pa[PPW], pb[PPW];
+#pragma unroll
+  for (int q = 0; q < PPW; ++q) pair_ab(q < P ? q : 0, nb, pa[q], pb[q]);
+  d4 acc[PPW];
+#pragma unroll
+  for (int q = 0; q < PPW; ++q) acc[q] = d4{0.0, 0.0, 0.0, 0.0};
+
+  for (int idx = lane; idx < CHT * S; idx += 64) Wt[idx] = 0.0;     // padding columns stay 0
+  if (rinv_lds)
+    for (int idx = tid; idx < KP * KP; idx += blockDim.x) rinv_lds[idx] = rinv[idx];
+  __syncthreads();
+
+  const int64_t nw = int64_t(gridDim.x) * nwave;
+  const double up = -c.j_lin_up;
+  const int p2 = (lane % LPC) * 2, cg = lane / LPC;
+
+  for (int64_t ch = int64_t(blockIdx.x) * nwave + wave; ch < nchunks; ch += nw) {
+    const int64_t e0 = ch * CHT;
+    int64_t iy0 = int64_t(uint64_t(e0) % uint64_t(N)) + p2;
+    while (iy0 >= N) iy0 -= N;
+    int64_t iy1 = iy0 + 1;
+    if (iy1 >= N) iy1 -= N;
+    const bool val0 = e0 + p2 < nown, val1 = e0 + p2 + 1 < nown;
+    // pair start; a fully-invalid tail pair is clamped (its values are discarded); a half-valid
+    // pair reads one row into the trailing ghost rows, which always exist
+    const int64_t i = base + (val0 ? e0 + p2 : nown - 2);
+    const double cw0 = iy0 > 0 ? c.hm2 : 0.0, ce0 = iy0 + 1 < N ? c.hm2 : 0.0;   // s + 0*v == s
+    const double cw1 = iy1 > 0 ? c.hm2 : 0.0, ce1 = iy1 + 1 < N ? c.hm2 : 0.0;
+    const d2 uu = *reinterpret_cast<const d2*>(u + i);
+    const double dn0 = -jdiag(c, uu.x), dn1 = -jdiag(c, uu.y);
+    for (int j0 = 0; j0 < k; j0 += CG * BC) {
+      d2 vn[BC], vw[BC], vc[BC], ve[BC], vs[BC];
+      if (dbg & 1) {
+#pragma unroll
+        for (int q = 0; q < BC; ++q) {
+          const double t = 1e-3 * (lane + q + j0);
+          vn[q] = vw[q] = vc[q] = ve[q] = vs[q] = d2{t, -t};
+        }
+      } else {
+#pragma unroll
+        for (int q = 0; q < BC; ++q) {
+          const double* cp = V + min(j0 + CG * q + cg, k - 1) * ldv + i;
+          vn[q] = *reinterpret_cast<const d2*>(cp - N);
+          vw[q] = *reinterpret_cast<const d2*>(cp - 1);    // (i-1, i)
+          vc[q] = *reinterpret_cast<const d2*>(cp);
+          ve[q] = *reinterpret_cast<const d2*>(cp + 1);    // (i+1, i+2)
+          vs[q] = *reinterpret_cast<const d2*>(cp + N);
+        }
+      }
+#pragma unroll
+      for (int q = 0; q < BC; ++q) {
+        double s0 = 0.0 + c.hm2 * vn[q].x;
+        s0 = s0 + cw0 * vw[q].x;
+        s0 = s0 + dn0 * vc[q].x;
+        s0 = s0 + ce0 * ve[q].x;
+        s0 = s0 + up * vs[q].x;
+        double s1 = 0.0 + c.hm2 * vn[q].y;
+        s1 = s1 + cw1 * vw[q].y;
+        s1 = s1 + dn1 * vc[q].y;
+        s1 = s1 + ce1 * ve[q].y;
+        s1 = s1 + up * vs[q].y;
+        const int j = j0 + CG * q + cg;
+        if (j < k) {
+          Wt[p2 * S + j] = val0 ? s0 : 0.0;
+          Wt[(p2 + 1) * S + j] = val1 ? s1 : 0.0;
+        }
+      }
+    }
+    if (r && cg == 0) {
+      const d2 rv = *reinterpret_cast<const d2*>(r + i);
+      Wt[p2 * S + k] = val0 ? rv.x : 0.0;
+      Wt[(p2 + 1) * S + k] = val1 ? rv.y : 0.0;
+    }
+    if (rinv) {
+      // in place W <- W @ RinvAug, column blocks descending (block cb reads blocks a <= cb only)
+#pragma unroll
+      for (int c16 = 0; c16 < CHT; c16 += 16) {
+        for (int cb = nb - 1; cb >= 0; --cb) {
+          d4 qv = d4{0.0, 0.0, 0.0, 0.0};
+          for (int ab = 0; ab <= cb; ++ab) {
+#pragma unroll
+            for (int ks = 0; ks < 4; ++ks) {
+              if (ab * 16 + ks * 4 >= K1) break;     // RinvAug rows >= K1 are zero
+              const int kk = ab * 16 + ks * 4 + (lane >> 4);
+              qv = mfma64(Wt[(c16 + (lane & 15)) * S + kk], rinv_lds[kk * KP + cb * 16 + (lane & 15)], qv);
+            }
+          }
+#pragma unroll
+          for (int ii = 0; ii < 4; ++ii) Wt[(c16 + (lane >> 4) + 4 * ii) * S + cb * 16 + (lane & 15)] = qv[ii];
+        }
+      }
+    }
+    if (!(dbg & 2)) {
+#pragma unroll
+      for (int r4 = 0; r4 < CHT; r4 += 4) {
+        const double* row = Wt + (r4 + (lane >> 4)) * S + (lane & 15);
+#pragma unroll
+        for (int q = 0; q < PPW; ++q)
+          if (q < P) acc[q] = mfma64(row[pa[q] * 16], row[pb[q] * 16], acc[q]);
+      }
+    }
+  }
+
+  // block partial = ((w0 + w1) + w2) + ... through LDS, layout [block][pair][lane*4 + i]
+  __syncthreads();
+  double* red = lds;
+  for (int w = 0; w < nwave; ++w) {
+    if (wave == w) {
+#pragma unroll
+      for (int q = 0; q < PPW; ++q)
+        if (q < P)
+#pragma unroll
+          for (int ii = 0; ii < 4; ++ii) {
+            double* dst = red + q * 256 + lane * 4 + ii;
+            *dst = (w == 0) ? acc[q][ii] : *dst + acc[q][ii];
+          }
+    }
+    __syncthreads();
+  }
+  double* out = partial + size_t(blockIdx.x) * size_t(P) * 256;
+  for (int idx = tid; idx < P * 256; idx += blockDim.x) out[idx] = red[idx];
 }
 
 // Sum Gram partials over blocks (block order) and scatter into G[KP][KP] (symmetric).
@@ -791,8 +1028,7 @@ struct TimedLaunch {
 };
 
 int reduce(gnk_ctx* ctx, const double* partial, int nblk, int len, int stride, const int* is_max, double* out) {
-  hipLaunchKernelGGL(k_reduce, dim3((len + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, ctx->stream, partial, nblk, len,
-                     stride, is_max, out);
+  hipLaunchKernelGGL(k_reduce, dim3(len), dim3(BLOCK), 0, ctx->stream, partial, nblk, len, stride, is_max, out);
   return check_launch(ctx, "reduce");
 }
 
@@ -946,16 +1182,31 @@ int gnk_vjp_gemv_t(gnk_ctx* ctx, const double* u, const double* r, const double*
                    double* g, double* h_out) {
   if (!ready(ctx)) return -1;
   if (k < 0) return fail(ctx, "vjp_gemv_t: k < 0");
-  const int nchunk = std::max(1, (k + KC - 1) / KC);
-  RowLaunch L = rows(ctx, G, ctx->geo.nrows, vec_of(ctx), std::max(64, MAX_RED_BLOCKS / nchunk));
+  if (k > 0 && !V) return fail(ctx, "vjp_gemv_t: V is NULL");
+  if (vec_of(ctx) == 2 && (ldv % 2 != 0)) return fail(ctx, "vjp_gemv_t: ldv must be even");
+  const int kct = k <= 8 ? 8 : 16;
+  const int nchunk = std::max(1, (k + kct - 1) / kct);
+  RowLaunch L = rows(ctx, G, ctx->geo.nrows, vec_of(ctx), std::max(64, 2048 / nchunk));
   L.grid.z = nchunk;
   const int nblk = L.grid.x * L.grid.y;
-  if (size_t(nblk) * nchunk * KC > SCRATCH_DOUBLES) return fail(ctx, "vjp_gemv_t: scratch too small");
-  DISPATCH_VEC(ctx, k_vjp_gemv_t, L, 0, u, r, V, ldv, k, g, ctx->geo, ctx->coef, L.lr0, L.nlr, ctx->scratch);
+  if (size_t(nblk) * nchunk * kct > SCRATCH_DOUBLES) return fail(ctx, "vjp_gemv_t: scratch too small");
+  if (vec_of(ctx) == 2) {
+    if (kct == 8) hipLaunchKernelGGL((k_vjp_gemv_t<2, 8>), L.grid, dim3(BLOCK), 0, ctx->stream, u, r, V, ldv, k, g,
+                                     ctx->geo, ctx->coef, L.lr0, L.nlr, ctx->scratch);
+    else hipLaunchKernelGGL((k_vjp_gemv_t<2, 16>), L.grid, dim3(BLOCK), 0, ctx->stream, u, r, V, ldv, k,
+                            g, ctx->geo, ctx->coef, L.lr0, L.nlr, ctx->scratch);
+
+  } else {
+    if (kct == 8) hipLaunchKernelGGL((k_vjp_gemv_t<1, 8>), L.grid, dim3(BLOCK), 0, ctx->stream, u, r, V, ldv, k, g,
+                                     ctx->geo, ctx->coef, L.lr0, L.nlr, ctx->scratch);
+    else hipLaunchKernelGGL((k_vjp_gemv_t<1, 16>), L.grid, dim3(BLOCK), 0, ctx->stream, u, r, V, ldv, k,
+                            g, ctx->geo, ctx->coef, L.lr0, L.nlr, ctx->scratch);
+
+  }
   int rc = check_launch(ctx, "vjp_gemv_t");
   if (rc || k == 0 || !h_out) return rc;
   hipLaunchKernelGGL(k_reduce_chunks, dim3((k + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, ctx->stream, ctx->scratch, nblk,
-                     k, h_out);
+                     k, kct, h_out);
   return check_launch(ctx, "vjp_gemv_t reduce");
 }
 
@@ -1008,6 +1259,52 @@ int gnk_gram(gnk_ctx* ctx, const double* u, const double* V, int64_t ldv, int k,
   if (rinv && ldr != KP) return fail(ctx, "gram: rinv must be the kp x kp augmented inverse (ldr == kp)");
   const int nb = KP / 16;
   const int P = nb * (nb + 1) / 2;
+  if (KP <= 64) {
+    // wave-independent streaming kernel (GNK_DEBUG_GRAM: tooling-only ablation switch,
+    // 1 = no loads, 2 = no Gram MFMAs)
+    static const int dbg = getenv("GNK_DEBUG_GRAM") ? atoi(getenv("GNK_DEBUG_GRAM")) : 0;
+    static const int bc_env = getenv("GNK_GRAM_BC") ? atoi(getenv("GNK_GRAM_BC")) : 0;   // tooling A/B switch
+    static const int ch_env = getenv("GNK_GRAM_CH") ? atoi(getenv("GNK_GRAM_CH")) : 0;
+    // chunk height: 64 rows for one column block, 32 rows above (LDS tile 32 x (KP+1) per wave)
+    const int chv = ch_env ? ch_env : (KP <= 32 ? 64 : 32);
+    const int nwave = 4;
+    size_t ldsw = size_t(nwave) * chv * (KP + 1) * 8 + (rinv ? size_t(KP) * KP * 8 : 0);
+    ldsw = std::max(ldsw, size_t(P) * 256 * 8);
+    ldsw = (ldsw + 15) & ~size_t(15);
+    if (ldsw > 160 * 1024) return fail(ctx, "gram: LDS tile too large");
+    const int64_t nown = ctx->geo.nrows * ctx->geo.N;
+    const int64_t nch = (nown + chv - 1) / chv;
+    const int wg_per_cu = std::max<int>(1, std::min<int>(8, int((160 * 1024) / ldsw)));
+    int64_t nblk = std::min<int64_t>((nch + nwave - 1) / nwave, int64_t(ctx->num_cus) * wg_per_cu);
+    nblk = std::max<int64_t>(nblk, 1);
+    if (size_t(nblk) * P * 256 > SCRATCH_DOUBLES) return fail(ctx, "gram: scratch too small");
+    const int bc = bc_env ? bc_env : (chv == 64 ? 4 : 2);
+    TimedLaunch tl(ctx, GNK_TIMER_GRAM, 8.0 * double(nown) * double(k + 1 + (r ? 1 : 0)));
+#define GRAMW1(PP, BCV, CHV) hipLaunchKernelGGL((k_gram_w<PP, BCV, CHV>), dim3(unsigned(nblk)), dim3(64 * nwave),   \
+                                                ldsw, ctx->stream, u, V, ldv, k, rinv, r, ctx->geo, ctx->coef, KP, \
+                                                P, nch, ctx->scratch, dbg)
+#define GRAMW(PP)                                                  \
+  do {                                                             \
+    if (chv == 64) {                                               \
+      if (bc == 2) GRAMW1(PP, 2, 64); else GRAMW1(PP, 4, 64);      \
+    } else {                                                       \
+      if (bc == 1) GRAMW1(PP, 1, 32); else GRAMW1(PP, 2, 32);      \
+    }                                                              \
+  } while (0)
+    if (P == 1) GRAMW(1);
+    else if (P <= 3) GRAMW(3);
+    else if (P <= 6) GRAMW(6);
+    else GRAMW(10);
+#undef GRAMW
+#undef GRAMW1
+    tl.done();
+    int rc = check_launch(ctx, "gram_w");
+    if (rc) return rc;
+    (void)hipMemsetAsync(G_out, 0, size_t(KP) * KP * sizeof(double), ctx->stream);
+    hipLaunchKernelGGL(k_gram_reduce, dim3((P * 256 + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, ctx->stream, ctx->scratch,
+                       int(nblk), P, 1, KP, G_out);
+    return check_launch(ctx, "gram reduce");
+  }
   const int rowsplit = P <= PPW_MAX ? 1 : 0;
   const int groups = rowsplit ? 1 : (P + 4 * PPW_MAX - 1) / (4 * PPW_MAX);
   // tile rows: LDS tile <= ~40 KB for small KP (several WGs per CU), 64 rows otherwise
@@ -1015,7 +1312,7 @@ int gnk_gram(gnk_ctx* ctx, const double* u, const double* V, int64_t ldv, int k,
   while (T > 64 && size_t(T) * (KP + 1) * 8 > 40 * 1024) T >>= 1;
   int logT = 0;
   while ((1 << logT) < T) ++logT;
-  size_t lds = size_t(T) * (KP + 1) * 8;
+  size_t lds = size_t(T) * (KP + 1) * 8 + ((rinv && KP <= 64) ? size_t(KP) * KP * 8 : 0);
   lds = (lds + 15) & ~size_t(15);
   if (rowsplit && size_t(P) * 256 > size_t(T) * (KP + 1)) return fail(ctx, "gram: reduction staging does not fit");
   if (lds > 160 * 1024) return fail(ctx, "gram: k too large for the LDS tile");
