@@ -534,6 +534,34 @@ __global__ __launch_bounds__(BLOCK) void k_cg_p(double beta, int first, const do
 }
 
 // ---------------------------------------------------------------- deterministic partial reduction
+// Wave-per-output deterministic reduction over a fixed partition of the partials.
+// Output j reads partial[base(j) + b * sb] for b in [split * span, min(nblk, (split+1) * span)),
+// base(j) = (j / cw) * cs + (j % cw).  Lane l folds b = l, l + 64, ... with 8 independent
+// (clamped, branch-free) loads in flight, then a fixed xor-tree.  out[j * nsplit + split].
+__global__ __launch_bounds__(64) void k_wave_reduce(const double* __restrict__ partial, int nblk, int span, int64_t sb,
+                                                    int cw, int64_t cs, const int* __restrict__ is_max,
+                                                    double* __restrict__ out) {
+  const int j = blockIdx.x, split = blockIdx.y, nsplit = gridDim.y, lane = threadIdx.x;
+  const bool mx = is_max ? is_max[j] != 0 : false;
+  const double* src = partial + int64_t(j / cw) * cs + (j % cw);
+  const int b0 = split * span, b1 = min(nblk, b0 + span);
+  double s = mx ? -1.0 : 0.0;    // identity (max is taken over |x| >= 0)
+  for (int b = b0 + lane; b < b1; b += 64 * 8) {
+    double v[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) v[q] = src[int64_t(min(b + 64 * q, b1 - 1)) * sb];
+#pragma unroll
+    for (int q = 0; q < 8; ++q)
+      if (b + 64 * q < b1) s = mx ? nan_max(s, v[q]) : s + v[q];
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const double t = __shfl_xor(s, o);
+    s = mx ? nan_max(s, t) : s + t;
+  }
+  if (lane == 0) out[int64_t(j) * nsplit + split] = (mx && s < 0.0) ? 0.0 : s;
+}
+
 // out[j] = sum over b of partial[b * stride + j] (mode is_max[j]: NaN-propagating max).
 // One block per output; thread t folds b = t, t + 256, ... in order, then a fixed tree:
 // the summation order depends only on nblk, so results are bitwise reproducible.
@@ -907,6 +935,23 @@ __global__ __launch_bounds__(BLOCK) void k_gram_w(const double* __restrict__ u, 
 }
 
 // Sum Gram partials over blocks (block order) and scatter into G[KP][KP] (symmetric).
+// scatter the reduced pair tiles (red[pair * 256 + lane * 4 + i]) into symmetric G[KP][KP]
+__global__ __launch_bounds__(BLOCK) void k_gram_scatter(const double* __restrict__ red, int P, int KP,
+                                                        double* __restrict__ Gout) {
+  const int nb = KP / 16;
+  for (int idx = blockIdx.x * BLOCK + threadIdx.x; idx < P * 256; idx += gridDim.x * BLOCK) {
+    const int p = idx >> 8, li = idx & 255, lane = li >> 2, i = li & 3;
+    int a, bb;
+    pair_ab(p, nb, a, bb);
+    const int row = a * 16 + (lane >> 4) + 4 * i;
+    const int col = bb * 16 + (lane & 15);
+    if (a != bb || row <= col) {
+      Gout[row * KP + col] = red[idx];
+      Gout[col * KP + row] = red[idx];
+    }
+  }
+}
+
 __global__ __launch_bounds__(BLOCK) void k_gram_reduce(const double* __restrict__ partial, int nblk, int P,
                                                        int rowsplit, int KP, double* __restrict__ Gout) {
   const int nb = KP / 16;
@@ -1027,9 +1072,30 @@ struct TimedLaunch {
   }
 };
 
+// Deterministic reduction of nblk partial blocks into out[0..len): output j reads
+// partial[(j / cw) * cs + (j % cw) + b * sb].  Above 4096 partials a first stage folds
+// fixed ranges of 4096 into a scratch tail, a second stage folds those.
+int wreduce(gnk_ctx* ctx, const double* partial, int nblk, int len, int64_t sb, int cw, int64_t cs,
+            const int* is_max, double* out) {
+  constexpr int SPAN = 4096;
+  if (nblk <= SPAN) {
+    hipLaunchKernelGGL(k_wave_reduce, dim3(len, 1), dim3(64), 0, ctx->stream, partial, nblk, nblk, sb, cw, cs, is_max,
+                       out);
+    return check_launch(ctx, "reduce");
+  }
+  const int nsplit = (nblk + SPAN - 1) / SPAN;
+  double* tmp = ctx->scratch + (SCRATCH_DOUBLES - size_t(len) * nsplit);
+  hipLaunchKernelGGL(k_wave_reduce, dim3(len, nsplit), dim3(64), 0, ctx->stream, partial, nblk, SPAN, sb, cw, cs,
+                     is_max, tmp);
+  int rc = check_launch(ctx, "reduce stage 1");
+  if (rc) return rc;
+  hipLaunchKernelGGL(k_wave_reduce, dim3(len, 1), dim3(64), 0, ctx->stream, tmp, nsplit, nsplit, int64_t(1), 1,
+                     int64_t(nsplit), is_max, out);
+  return check_launch(ctx, "reduce stage 2");
+}
+
 int reduce(gnk_ctx* ctx, const double* partial, int nblk, int len, int stride, const int* is_max, double* out) {
-  hipLaunchKernelGGL(k_reduce, dim3(len), dim3(BLOCK), 0, ctx->stream, partial, nblk, len, stride, is_max, out);
-  return check_launch(ctx, "reduce");
+  return wreduce(ctx, partial, nblk, len, stride, len, 0, is_max, out);
 }
 
 // device constant {0, 1} flags for {sum, max} reductions
@@ -1205,9 +1271,7 @@ int gnk_vjp_gemv_t(gnk_ctx* ctx, const double* u, const double* r, const double*
   }
   int rc = check_launch(ctx, "vjp_gemv_t");
   if (rc || k == 0 || !h_out) return rc;
-  hipLaunchKernelGGL(k_reduce_chunks, dim3((k + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, ctx->stream, ctx->scratch, nblk,
-                     k, kct, h_out);
-  return check_launch(ctx, "vjp_gemv_t reduce");
+  return wreduce(ctx, ctx->scratch, nblk, k, kct, kct, int64_t(nblk) * kct, nullptr, h_out);
 }
 
 int gnk_cgs_update(gnk_ctx* ctx, const double* V, int64_t ldv, int k, const double* h, double* g,
@@ -1301,9 +1365,13 @@ int gnk_gram(gnk_ctx* ctx, const double* u, const double* V, int64_t ldv, int k,
     int rc = check_launch(ctx, "gram_w");
     if (rc) return rc;
     (void)hipMemsetAsync(G_out, 0, size_t(KP) * KP * sizeof(double), ctx->stream);
-    hipLaunchKernelGGL(k_gram_reduce, dim3((P * 256 + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, ctx->stream, ctx->scratch,
-                       int(nblk), P, 1, KP, G_out);
-    return check_launch(ctx, "gram reduce");
+    // partials [block][P * 256] -> red[P * 256] (scratch tail) -> symmetric G
+    double* red = ctx->scratch + (SCRATCH_DOUBLES - size_t(P) * 256);
+    rc = wreduce(ctx, ctx->scratch, int(nblk), P * 256, int64_t(P) * 256, P * 256, 0, nullptr, red);
+    if (rc) return rc;
+    hipLaunchKernelGGL(k_gram_scatter, dim3((P * 256 + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, ctx->stream, red, P, KP,
+                       G_out);
+    return check_launch(ctx, "gram scatter");
   }
   const int rowsplit = P <= PPW_MAX ? 1 : 0;
   const int groups = rowsplit ? 1 : (P + 4 * PPW_MAX - 1) / (4 * PPW_MAX);
