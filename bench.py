@@ -62,11 +62,12 @@ def bratu_inputs(N, seed=42):
     return prob, u_true, u0
 
 
-def step_bytes(n, k, a):
+def step_bytes(n, k, a, passes=1.0):
     """Algorithmic HBM bytes of one outer iteration as implemented:
-    2 Gram passes (k+1, k+2 vectors), a trials x (GEMV k+1 + residual 3),
-    fused VJP + V^T g (k+3), CGS update (k+2), normalise (2)."""
-    return 8.0 * n * (4 * k + 10 + a * (k + 4))
+    `passes` preconditioned Gram passes (k + 2 vectors each), a trials x (GEMV k+1 +
+    residual 3), fused VJP + V^T g (k+3), CGS update (k+2), normalise (2),
+    ||J v_new|| (JVP 3 + norm 1)."""
+    return 8.0 * n * (passes * (k + 2) + 2 * k + 11 + a * (k + 4))
 
 
 def cpu_baseline(N, seconds, version, restart):
@@ -150,6 +151,7 @@ def main():
     cap = 4 * (args.steps + 1)
     be.timer_start(_native.TIMER_GRAM, cap)
     k_trace0 = len(solver.trace)
+    passes0 = solver.lls.passes
     comm.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -169,7 +171,9 @@ def main():
 
     # whole-step algorithmic bytes (global grid) over the timed steps
     tr = solver.trace[k_trace0:]
-    total_bytes = sum(step_bytes(n, s["k"], s["trials"]) for s in tr)
+    passes = solver.lls.passes - passes0
+    ppi = passes / max(len(tr), 1)
+    total_bytes = sum(step_bytes(n, s["k"], s["trials"], ppi) for s in tr)
     # dominant kernel: Gram pass (per-launch events; bytes are this rank's slab)
     g_ms = [m for m, _ in launches]
     g_by = [b for _, b in launches]
@@ -222,6 +226,7 @@ def main():
         "jvp": {"kernel": "k_jvp (J(u) v, 5-point stencil)", "grid": N, "median_ms": j_ms, "GBs": j_gbs,
                 "frac_of_peak": j_gbs / HBM_PEAK_GBS, "algorithmic_bytes": jl[0][1]},
         "step_algorithmic_GBs": total_bytes / elapsed / 1e9,
+        "gram_passes_per_step": ppi,
     }
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
         try:

@@ -801,7 +801,8 @@ __global__ __launch_bounds__(BLOCK) void k_gram_w(const double* __restrict__ u, 
   constexpr int LPC = CHT / 2, CG = 64 / LPC;
   extern __shared__ __attribute__((aligned(16))) double lds[];
   const int S = KP + 1;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);    // provably wave-uniform
   const int nwave = blockDim.x >> 6;
   const int nb = KP / 16;
   double* Wt = lds + wave * (CHT * S);
@@ -827,12 +828,22 @@ __global__ __launch_bounds__(BLOCK) void k_gram_w(const double* __restrict__ u, 
   const double up = -c.j_lin_up;
   const int p2 = (lane % LPC) * 2, cg = lane / LPC;
 
-  for (int64_t ch = int64_t(blockIdx.x) * nwave + wave; ch < nchunks; ch += nw) {
+  // row position of the chunk start, advanced incrementally (scalar; no per-chunk division)
+  const int64_t ch0 = int64_t(blockIdx.x) * nwave + wave;
+  const int64_t step = (nw * CHT) % N;
+  int64_t iyb = (ch0 * CHT) % N;
+  for (int64_t ch = ch0; ch < nchunks; ch += nw) {
     const int64_t e0 = ch * CHT;
-    int64_t iy0 = int64_t(uint64_t(e0) % uint64_t(N)) + p2;
-    while (iy0 >= N) iy0 -= N;
+    int64_t iy0 = iyb + p2;
+    if (N >= 64) {
+      if (iy0 >= N) iy0 -= N;
+    } else {
+      while (iy0 >= N) iy0 -= N;
+    }
     int64_t iy1 = iy0 + 1;
     if (iy1 >= N) iy1 -= N;
+    iyb += step;
+    if (iyb >= N) iyb -= N;
     const bool val0 = e0 + p2 < nown, val1 = e0 + p2 + 1 < nown;
     // pair start; a fully-invalid tail pair is clamped (its values are discarded); a half-valid
     // pair reads one row into the trailing ghost rows, which always exist
@@ -862,16 +873,18 @@ __global__ __launch_bounds__(BLOCK) void k_gram_w(const double* __restrict__ u, 
       }
 #pragma unroll
       for (int q = 0; q < BC; ++q) {
-        double s0 = 0.0 + c.hm2 * vn[q].x;
-        s0 = s0 + cw0 * vw[q].x;
-        s0 = s0 + dn0 * vc[q].x;
-        s0 = s0 + ce0 * ve[q].x;
-        s0 = s0 + up * vs[q].x;
-        double s1 = 0.0 + c.hm2 * vn[q].y;
-        s1 = s1 + cw1 * vw[q].y;
-        s1 = s1 + dn1 * vc[q].y;
-        s1 = s1 + ce1 * ve[q].y;
-        s1 = s1 + up * vs[q].y;
+        // J V with explicit FMAs (same CSR term order; the Gram's own summation order already
+        // differs from the reference's, so the per-element rounding is not observable)
+        double s0 = c.hm2 * vn[q].x;
+        s0 = fma(cw0, vw[q].x, s0);
+        s0 = fma(dn0, vc[q].x, s0);
+        s0 = fma(ce0, ve[q].x, s0);
+        s0 = fma(up, vs[q].x, s0);
+        double s1 = c.hm2 * vn[q].y;
+        s1 = fma(cw1, vw[q].y, s1);
+        s1 = fma(dn1, vc[q].y, s1);
+        s1 = fma(ce1, ve[q].y, s1);
+        s1 = fma(up, vs[q].y, s1);
         const int j = j0 + CG * q + cg;
         if (j < k) {
           Wt[p2 * S + j] = val0 ? s0 : 0.0;

@@ -7,9 +7,10 @@ test, the four ``version`` update rules, restart, every printed message and
 every exception -- and runs each n-sized operation on the GPU:
 
   per outer iteration (k basis columns, a Armijo trials)
-    2 Gram passes (fp64 MFMA, J V on the fly)   -> CholQR2 LS solve   (lls.py)
+    1 Gram pass (fp64 MFMA, J V P^-1 on the fly; P = previous R factor, a 2nd pass
+      only when the preconditioned factor is not well conditioned) -> LS solve (lls.py)
     a x [basis GEMV + fused residual/||r||^2]   -> Armijo trials
-    fused -J^T r + V^T g, CGS update + stats, normalise, halo  -> basis update
+    fused -J^T r + V^T g, CGS update + stats, normalise, halo, ||J v_new|| -> basis update
 
 Host <-> device traffic per iteration is O(k^2) doubles (Gram matrices, k
 coefficients, a few scalars).  ``GNKSolver`` exposes the same loop one outer
@@ -75,12 +76,22 @@ class GNKSolver:
         self.xb = [self.dev.vec() for _ in range(3)]
         self.rb = [self.dev.vec() for _ in range(2)]
         self._n2 = self.dev.scalar(1)
+        self._st = self.dev.scalar(2)
         self.trace = []          # per-iteration (t, k, trials) for tests / diagnostics
 
     # -- pieces -------------------------------------------------------------------------
     def _residual(self, x, r) -> float:
         self.be.residual(x, self.y, r, self._n2)
         return float(self.comm.sum(self._n2)[0])
+
+    def _precondition_new_column(self):
+        """s = ||J(u) v_new|| for the next least-squares pass's preconditioner (lls.py)."""
+        k = self.basis.k
+        tmp = self.xb[self._free_x(self.uJ)]
+        self.be.jvp(self.xb[self.uJ], self.basis.V[k - 1], tmp)
+        self.be.vec_stats(tmp, self._st)
+        ss, _ = self.comm.sum_max(self._st)
+        self.lls.on_append(np.sqrt(ss))
 
     def _free_x(self, *busy):
         for i in range(3):
@@ -158,6 +169,7 @@ class GNKSolver:
                 raise ValueError(
                     "Variable version must be in ['res_old','res_new','jac_old_res_old','jac_old_res_new']")
             self.c = np.append(self.c, 0)                                 # :124
+            self._precondition_new_column()
         except GeneralizedKrylowSubspaceBreakdown:
             print(f"Generalized krylow subspace breakdown at iteration = {it}, basis.shape = {basis.shape}")
         except GeneralizedKrylowSubspaceSpansEntireSpace:
@@ -169,6 +181,7 @@ class GNKSolver:
             xr = self._free_x(self.uJ)
             basis.x(self.c, self.xb[xr])
             self.c = basis.start(self.xb[xr])
+            self.lls.on_restart()
         if it >= self.max_iter - 1:
             self.done = True
         return self.done

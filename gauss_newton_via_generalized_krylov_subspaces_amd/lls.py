@@ -2,16 +2,22 @@
 
 The reference factors A = -J @ V (n x k) with LAPACK Householder QR and solves
 R d = Q^T r.  The build never materialises J @ V: the fp64-MFMA Gram kernel
-(gnk_gram) streams V once per pass, applies the Bratu stencil on the fly and
-returns W^T W.  CholeskyQR2 on those Gram matrices gives the same R (up to row
-signs) and Q^T r to O(u) orthogonality for cond(J V) up to ~1e7:
+(gnk_gram) streams V once per pass, applies the Bratu stencil on the fly, applies
+an upper-triangular preconditioner P^-1 on MFMA (W <- W P^-1) and returns the Gram
+matrix of [J V P^-1 | r].  Cholesky QR on a well-conditioned Y = J V P^-1 gives
+R = R_Y P and Q^T r = R_Y^-T (Y^T r) to O(u) orthogonality.
 
-  pass 1:  G1 = (J V)^T (J V)                      -> R1 = chol(G1)
-  pass 2:  G2 = [J V R1^-1 | r]^T [J V R1^-1 | r]   -> R2 = chol(G2[:k,:k]),
-           z = R2^-T G2[:k, k] = Q^T r,  R = R2 R1,  d = -R^-1 z.
-
-If pass 1 is not numerically SPD the first factorisation is shifted
-(shifted CholeskyQR3, Fukaya et al. 2020) and one more pass is made.
+Preconditioner P (one pass per iteration in the common case):
+  * CholQR2 (two passes: P = I, then P = R1) when there is no usable previous
+    factor -- first iteration, after a restart;
+  * otherwise P = blockdiag(R_prev, s): the previous iteration's R of J_prev V
+    (the basis only gained one column and J changed only in its diagonal
+    LAMBDA exp(u)) and s = ||J v_new|| for the appended column, so Y is close to
+    orthonormal and ONE pass suffices.
+The pass is accepted when cond(R_Y) <= COND_ACCEPT (then the O(cond^2 u)
+CholQR error is below 1e-13 relative); otherwise another pass runs with the
+current R -- classical CholQR2 -- and, if a Gram is not numerically SPD, the
+factorisation is shifted (shifted CholeskyQR3, Fukaya et al. 2020).
 Across ranks each Gram is an all-gather of (k+1)^2 doubles summed in rank order
 (the "one-reduce" of TSQR, once per pass).
 
@@ -24,10 +30,22 @@ import numpy as np
 import scipy.linalg
 
 EPS = np.finfo(np.float64).eps
+COND_ACCEPT = 30.0
+MAX_PASSES = 4
 
 
 def _chol_upper(G):
-    return scipy.linalg.cholesky(G, lower=False, check_finite=False)
+    R = scipy.linalg.cholesky(G, lower=False, check_finite=False)
+    if not np.all(np.isfinite(R)):
+        raise np.linalg.LinAlgError("non-finite Cholesky factor")
+    return R
+
+
+def _cond_upper(R):
+    d = np.abs(np.diagonal(R))
+    if d.min() == 0.0:
+        return np.inf
+    return float(np.linalg.cond(R))
 
 
 class CholQR2Solver:
@@ -38,14 +56,26 @@ class CholQR2Solver:
         self._G = self.be.zeros(kp * kp)
         self._rinv = self.be.zeros(kp * kp)
         self.passes = 0
+        self.solves = 0
+        self.fallbacks = 0
+        self.R_prev = None          # R of the last solve (k_prev x k_prev)
+        self.s_new = None           # ||J v_new|| of the column appended since then
 
-    def _gram(self, u, basis, k, rinv_host, r):
+    # -- basis events (the solver tells us how V changed since the last solve) -------
+    def on_append(self, s_new: float):
+        self.s_new = float(s_new)
+
+    def on_restart(self):
+        self.R_prev = None
+        self.s_new = None
+
+    def _gram(self, u, basis, k, P, r):
         be = self.be
         kp = be.gram_dim(k, r is not None)
         rinv_dev = None
-        if rinv_host is not None:
+        if P is not None:
             aug = np.zeros((kp, kp))
-            aug[:k, :k] = rinv_host
+            aug[:k, :k] = scipy.linalg.solve_triangular(P, np.eye(k), lower=False)
             if r is not None:
                 aug[k, k] = 1.0
             rinv_dev = self._rinv[:kp * kp]
@@ -55,32 +85,55 @@ class CholQR2Solver:
         self.passes += 1
         return self.dev.comm.sum(G).reshape(kp, kp)
 
+    def _initial_preconditioner(self, k):
+        R = self.R_prev
+        if R is None:
+            return None
+        kp = R.shape[0]
+        if kp == k:
+            return R                                   # basis unchanged (breakdown / spans space)
+        if kp == k - 1 and self.s_new is not None and self.s_new > 0.0:
+            P = np.zeros((k, k))
+            P[:kp, :kp] = R
+            P[kp, kp] = self.s_new
+            return P
+        return None
+
     def solve(self, u, basis, r):
         """Returns (d, jdd, R) for min ||-J(u) V d - r||."""
         k = basis.k
-        G1 = self._gram(u, basis, k, None, None)[:k, :k]
-        shifted = False
-        try:
-            R = _chol_upper(G1)
-            if not np.all(np.isfinite(R)):
-                raise np.linalg.LinAlgError
-        except (np.linalg.LinAlgError, ValueError):
-            n = self.dev.slab.n_global
-            s = 11.0 * (n * k + k * (k + 1)) * EPS * np.trace(G1)
-            R = _chol_upper(G1 + s * np.eye(k))
-            shifted = True
-        npass = 3 if shifted else 2
-        for p in range(1, npass):
-            last = p == npass - 1
-            Rinv = scipy.linalg.solve_triangular(R, np.eye(k), lower=False)
-            Gp = self._gram(u, basis, k, Rinv, r if last else None)
-            Rp = _chol_upper(Gp[:k, :k])
-            if last:
-                z = scipy.linalg.solve_triangular(Rp, Gp[:k, k], trans="T", lower=False)
-            R = Rp @ R
+        self.solves += 1
+        P = self._initial_preconditioner(k)
+        if P is None:
+            # classical CholQR2: first pass unpreconditioned (P = I, no r column)
+            G1 = self._gram(u, basis, k, None, None)[:k, :k]
+            try:
+                P = _chol_upper(G1)
+            except (np.linalg.LinAlgError, ValueError):
+                n = self.dev.slab.n_global
+                shift = 11.0 * (n * k + k * (k + 1)) * EPS * np.trace(G1)
+                P = _chol_upper(G1 + shift * np.eye(k))
+        for it in range(MAX_PASSES):
+            Gp = self._gram(u, basis, k, P, r)
+            try:
+                Ry = _chol_upper(Gp[:k, :k])
+            except (np.linalg.LinAlgError, ValueError):
+                n = self.dev.slab.n_global
+                shift = 11.0 * (n * k + k * (k + 1)) * EPS * np.trace(Gp[:k, :k])
+                P = _chol_upper(Gp[:k, :k] + shift * np.eye(k)) @ P
+                self.fallbacks += 1
+                continue
+            if _cond_upper(Ry) <= COND_ACCEPT or it == MAX_PASSES - 1:
+                z = scipy.linalg.solve_triangular(Ry, Gp[:k, k], trans="T", lower=False)
+                R = Ry @ P
+                break
+            P = Ry @ P                                   # one more pass with the improved factor
+            self.fallbacks += 1
         for r_kk in np.diagonal(R):                                  # ref:gauss_newton_krylow.py:32-34
             if np.isclose(r_kk, 0, atol=1e-8):
                 print("A is rank deficient")
         d = -scipy.linalg.solve_triangular(R, z, lower=False)
         jdd = float(np.sum((R @ d) ** 2))
+        self.R_prev = R
+        self.s_new = None
         return d, jdd, R
