@@ -791,20 +791,32 @@ __device__ __forceinline__ double bld(__amdgpu_buffer_rsrc_t rs, unsigned off) {
   return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rs, off, 0, 0));
 }
 
-template <int PPW, int BC, int CHT>
+constexpr int pair_a(int p, int nb) {
+  int a = 0;
+  while (p >= nb - a) { p -= nb - a; ++a; }
+  return a;
+}
+constexpr int pair_b(int p, int nb) {
+  int a = 0;
+  while (p >= nb - a) { p -= nb - a; ++a; }
+  return a + p;
+}
+
+template <int NB, int BC, int CHT>
 __global__ __launch_bounds__(BLOCK) void k_gram_w(const double* __restrict__ u, const double* __restrict__ V,
                                                   int64_t ldv, int k, const double* __restrict__ rinv,
-                                                  const double* __restrict__ r, Geo geo, Coef c, int KP, int P,
+                                                  const double* __restrict__ r, Geo geo, Coef c,
                                                   int64_t nchunks, double* __restrict__ partial, int dbg) {
+  // NB column blocks of 16 (KP = 16 NB), P = NB (NB + 1) / 2 Gram pair tiles; every block / pair
+  // loop below is compile-time so the MFMA loops unroll and their LDS reads issue ahead.
   // CHT rows per wave chunk; a lane holds 2 consecutive rows (16-B loads); LPC = CHT/2 lanes
   // cover one column of the chunk, so one load instruction covers CG = 64/LPC columns.
+  constexpr int KP = 16 * NB, S = KP + 1, P = NB * (NB + 1) / 2;
   constexpr int LPC = CHT / 2, CG = 64 / LPC;
   extern __shared__ __attribute__((aligned(16))) double lds[];
-  const int S = KP + 1;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);    // provably wave-uniform
   const int nwave = blockDim.x >> 6;
-  const int nb = KP / 16;
   double* Wt = lds + wave * (CHT * S);
   double* rinv_lds = rinv ? lds + nwave * CHT * S : nullptr;
   const int64_t N = geo.N;
@@ -812,12 +824,9 @@ __global__ __launch_bounds__(BLOCK) void k_gram_w(const double* __restrict__ u, 
   const int64_t base = int64_t(G) * N;
   const int K1 = k + (r ? 1 : 0);
 
-  int pa[PPW], pb[PPW];
+  d4 acc[P];
 #pragma unroll
-  for (int q = 0; q < PPW; ++q) pair_ab(q < P ? q : 0, nb, pa[q], pb[q]);
-  d4 acc[PPW];
-#pragma unroll
-  for (int q = 0; q < PPW; ++q) acc[q] = d4{0.0, 0.0, 0.0, 0.0};
+  for (int q = 0; q < P; ++q) acc[q] = d4{0.0, 0.0, 0.0, 0.0};
 
   for (int idx = lane; idx < CHT * S; idx += 64) Wt[idx] = 0.0;     // padding columns stay 0
   if (rinv_lds)
@@ -901,14 +910,17 @@ __global__ __launch_bounds__(BLOCK) void k_gram_w(const double* __restrict__ u, 
       // in place W <- W @ RinvAug, column blocks descending (block cb reads blocks a <= cb only)
 #pragma unroll
       for (int c16 = 0; c16 < CHT; c16 += 16) {
-        for (int cb = nb - 1; cb >= 0; --cb) {
+#pragma unroll
+        for (int cb = NB - 1; cb >= 0; --cb) {
           d4 qv = d4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
           for (int ab = 0; ab <= cb; ++ab) {
 #pragma unroll
             for (int ks = 0; ks < 4; ++ks) {
-              if (ab * 16 + ks * 4 >= K1) break;     // RinvAug rows >= K1 are zero
-              const int kk = ab * 16 + ks * 4 + (lane >> 4);
-              qv = mfma64(Wt[(c16 + (lane & 15)) * S + kk], rinv_lds[kk * KP + cb * 16 + (lane & 15)], qv);
+              if (ab * 16 + ks * 4 < K1) {     // RinvAug rows >= K1 are zero (wave-uniform test)
+                const int kk = ab * 16 + ks * 4 + (lane >> 4);
+                qv = mfma64(Wt[(c16 + (lane & 15)) * S + kk], rinv_lds[kk * KP + cb * 16 + (lane & 15)], qv);
+              }
             }
           }
 #pragma unroll
@@ -917,12 +929,15 @@ __global__ __launch_bounds__(BLOCK) void k_gram_w(const double* __restrict__ u, 
       }
     }
     if (!(dbg & 2)) {
+      const double* rowbase = Wt + (lane >> 4) * S + (lane & 15);
 #pragma unroll
       for (int r4 = 0; r4 < CHT; r4 += 4) {
-        const double* row = Wt + (r4 + (lane >> 4)) * S + (lane & 15);
+        const double* row = rowbase + r4 * S;
+        double a[NB];
 #pragma unroll
-        for (int q = 0; q < PPW; ++q)
-          if (q < P) acc[q] = mfma64(row[pa[q] * 16], row[pb[q] * 16], acc[q]);
+        for (int bb = 0; bb < NB; ++bb) a[bb] = row[bb * 16];
+#pragma unroll
+        for (int q = 0; q < P; ++q) acc[q] = mfma64(a[pair_a(q, NB)], a[pair_b(q, NB)], acc[q]);
       }
     }
   }
@@ -933,13 +948,164 @@ __global__ __launch_bounds__(BLOCK) void k_gram_w(const double* __restrict__ u, 
   for (int w = 0; w < nwave; ++w) {
     if (wave == w) {
 #pragma unroll
-      for (int q = 0; q < PPW; ++q)
-        if (q < P)
+      for (int q = 0; q < P; ++q)
 #pragma unroll
-          for (int ii = 0; ii < 4; ++ii) {
-            double* dst = red + q * 256 + lane * 4 + ii;
-            *dst = (w == 0) ? acc[q][ii] : *dst + acc[q][ii];
+        for (int ii = 0; ii < 4; ++ii) {
+          double* dst = red + q * 256 + lane * 4 + ii;
+          *dst = (w == 0) ? acc[q][ii] : *dst + acc[q][ii];
+        }
+    }
+    __syncthreads();
+  }
+  double* out = partial + size_t(blockIdx.x) * size_t(P) * 256;
+  for (int idx = tid; idx < P * 256; idx += blockDim.x) out[idx] = red[idx];
+}
+
+// Marching Gram pass (N % CHT == 0, k <= 8 CG).  Wave gw owns the vertical strip
+// s = gw % nstrips (CHT consecutive grid columns) and walks a contiguous range of grid rows.
+// Each lane keeps, for each of its <= 8 basis columns, the values of the current row and the
+// row below in registers, so a step loads ONE new row per column (16 B / lane) instead of the
+// five stencil loads; the in-row neighbours come from the adjacent lanes (ds_bpermute), only
+// the strip's edge lanes load their outer neighbour.  Then the same LDS transpose tile,
+// optional in-place W <- W P^-1 and Gram MFMAs as k_gram_w.
+template <int NB, int CHT, int MC>
+__global__ __launch_bounds__(BLOCK) void k_gram_m(const double* __restrict__ u, const double* __restrict__ V,
+                                                  int64_t ldv, int k, const double* __restrict__ rinv,
+                                                  const double* __restrict__ r, Geo geo, Coef c,
+                                                  double* __restrict__ partial) {
+  constexpr int KP = 16 * NB, S = KP + 1, P = NB * (NB + 1) / 2;
+  constexpr int LPC = CHT / 2, CG = 64 / LPC;     // <= MC columns per lane
+  extern __shared__ __attribute__((aligned(16))) double lds[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int nwave = blockDim.x >> 6;
+  double* Wt = lds + wave * (CHT * S);
+  double* rinv_lds = rinv ? lds + nwave * CHT * S : nullptr;
+  const int64_t N = geo.N;
+  const int64_t base = int64_t(G) * N;
+  const int K1 = k + (r ? 1 : 0);
+  const double up = -c.j_lin_up;
+
+  d4 acc[P];
+#pragma unroll
+  for (int q = 0; q < P; ++q) acc[q] = d4{0.0, 0.0, 0.0, 0.0};
+  for (int idx = lane; idx < CHT * S; idx += 64) Wt[idx] = 0.0;
+  if (rinv_lds)
+    for (int idx = tid; idx < KP * KP; idx += blockDim.x) rinv_lds[idx] = rinv[idx];
+  __syncthreads();
+
+  const int64_t nw = int64_t(gridDim.x) * nwave;
+  const int64_t gw = int64_t(blockIdx.x) * nwave + wave;
+  const int64_t nstrips = N / CHT;
+  const int64_t nranges = nw / nstrips;
+  const int64_t s_id = gw % nstrips, r_id = gw / nstrips;
+  const int64_t rpr = (geo.nrows + nranges - 1) / nranges;
+  const int64_t jx0 = r_id * rpr, jx1 = min(geo.nrows, jx0 + rpr);
+  const int pl = lane % LPC, cg = lane / LPC;
+  const int p2 = pl * 2;
+  const int64_t iy0 = s_id * CHT + p2;                 // strip is inside one grid row
+  const bool hw0 = iy0 > 0, he1 = iy0 + 2 < N;
+  const double cw0 = hw0 ? c.hm2 : 0.0, ce1 = he1 ? c.hm2 : 0.0;
+  const bool edge_w = pl == 0, edge_e = pl == LPC - 1;
+
+  if (r_id < nranges && jx0 < jx1) {
+    // prologue: rows jx0-1 (vn) and jx0 (vc) of every column (ghost rows exist)
+    d2 vn[MC], vc[MC];
+    int64_t i = base + jx0 * N + iy0;
+#pragma unroll
+    for (int q = 0; q < MC; ++q) {
+      const double* cp = V + min(cg + CG * q, k - 1) * ldv + i;
+      vn[q] = *reinterpret_cast<const d2*>(cp - N);
+      vc[q] = *reinterpret_cast<const d2*>(cp);
+    }
+    for (int64_t jx = jx0; jx < jx1; ++jx, i += N) {
+      d2 vs[MC];
+      double ew[MC], ee[MC];
+#pragma unroll
+      for (int q = 0; q < MC; ++q) {
+        const double* cp = V + min(cg + CG * q, k - 1) * ldv + i;
+        vs[q] = *reinterpret_cast<const d2*>(cp + N);
+        // outer neighbours of the strip (one lane per column group loads; others get 0 here)
+        ew[q] = edge_w ? cp[-1] : 0.0;
+        ee[q] = edge_e ? cp[2] : 0.0;
+      }
+      const d2 uu = *reinterpret_cast<const d2*>(u + i);
+      const double dn0 = -jdiag(c, uu.x), dn1 = -jdiag(c, uu.y);
+#pragma unroll
+      for (int q = 0; q < MC; ++q) {
+        // in-row neighbours from the adjacent lanes of the same column group
+        double w = __shfl_up(vc[q].y, 1, LPC);
+        double e = __shfl_down(vc[q].x, 1, LPC);
+        if (edge_w) w = ew[q];
+        if (edge_e) e = ee[q];
+        double s0 = c.hm2 * vn[q].x;
+        s0 = fma(cw0, w, s0);
+        s0 = fma(dn0, vc[q].x, s0);
+        s0 = fma(c.hm2, vc[q].y, s0);
+        s0 = fma(up, vs[q].x, s0);
+        double s1 = c.hm2 * vn[q].y;
+        s1 = fma(c.hm2, vc[q].x, s1);
+        s1 = fma(dn1, vc[q].y, s1);
+        s1 = fma(ce1, e, s1);
+        s1 = fma(up, vs[q].y, s1);
+        const int j = cg + CG * q;
+        if (j < k) {
+          Wt[p2 * S + j] = s0;
+          Wt[(p2 + 1) * S + j] = s1;
+        }
+        vn[q] = vc[q];
+        vc[q] = vs[q];
+      }
+      if (r && cg == 0) {
+        const d2 rv = *reinterpret_cast<const d2*>(r + i);
+        Wt[p2 * S + k] = rv.x;
+        Wt[(p2 + 1) * S + k] = rv.y;
+      }
+      if (rinv) {
+#pragma unroll
+        for (int c16 = 0; c16 < CHT; c16 += 16) {
+#pragma unroll
+          for (int cb = NB - 1; cb >= 0; --cb) {
+            d4 qv = d4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+            for (int ab = 0; ab <= cb; ++ab) {
+#pragma unroll
+              for (int ks = 0; ks < 4; ++ks) {
+                if (ab * 16 + ks * 4 < K1) {
+                  const int kk = ab * 16 + ks * 4 + (lane >> 4);
+                  qv = mfma64(Wt[(c16 + (lane & 15)) * S + kk], rinv_lds[kk * KP + cb * 16 + (lane & 15)], qv);
+                }
+              }
+            }
+#pragma unroll
+            for (int ii = 0; ii < 4; ++ii) Wt[(c16 + (lane >> 4) + 4 * ii) * S + cb * 16 + (lane & 15)] = qv[ii];
           }
+        }
+      }
+      const double* rowbase = Wt + (lane >> 4) * S + (lane & 15);
+#pragma unroll
+      for (int r4 = 0; r4 < CHT; r4 += 4) {
+        const double* row = rowbase + r4 * S;
+        double a[NB];
+#pragma unroll
+        for (int bb = 0; bb < NB; ++bb) a[bb] = row[bb * 16];
+#pragma unroll
+        for (int q = 0; q < P; ++q) acc[q] = mfma64(a[pair_a(q, NB)], a[pair_b(q, NB)], acc[q]);
+      }
+    }
+  }
+
+  __syncthreads();
+  double* red = lds;
+  for (int w = 0; w < nwave; ++w) {
+    if (wave == w) {
+#pragma unroll
+      for (int q = 0; q < P; ++q)
+#pragma unroll
+        for (int ii = 0; ii < 4; ++ii) {
+          double* dst = red + q * 256 + lane * 4 + ii;
+          *dst = (w == 0) ? acc[q][ii] : *dst + acc[q][ii];
+        }
     }
     __syncthreads();
   }
@@ -1355,11 +1521,59 @@ int gnk_gram(gnk_ctx* ctx, const double* u, const double* V, int64_t ldv, int k,
     int64_t nblk = std::min<int64_t>((nch + nwave - 1) / nwave, int64_t(ctx->num_cus) * wg_per_cu);
     nblk = std::max<int64_t>(nblk, 1);
     if (size_t(nblk) * P * 256 > SCRATCH_DOUBLES) return fail(ctx, "gram: scratch too small");
-    const int bc = bc_env ? bc_env : (chv == 64 ? 4 : 2);
+    const int bc = bc_env ? bc_env : (chv == 64 ? (nb == 1 ? 2 : 4) : 2);
+    static const int march_env = getenv("GNK_GRAM_MARCH") ? atoi(getenv("GNK_GRAM_MARCH")) : 1;
+    // marching kernel: NB <= 2, strips of 64 (NB = 1) / 32 (NB = 2) columns, <= 8 columns per lane
+    const int chm = nb == 1 ? 64 : 32;
+    const int64_t nstrips = ctx->geo.N / chm;
+    // (NB = 2 with the in-place transform keeps too few waves resident to win: chunked kernel)
+    if (march_env && (nb == 1 || (nb == 2 && !rinv)) && !dbg && ctx->geo.N % chm == 0 &&
+        k <= 8 * (64 / (chm / 2))) {
+      const int nwm = 4;
+      size_t ldsm = size_t(nwm) * chm * (KP + 1) * 8 + (rinv ? size_t(KP) * KP * 8 : 0);
+      ldsm = std::max(ldsm, size_t(P) * 256 * 8);
+      ldsm = (ldsm + 15) & ~size_t(15);
+      const int wgm = std::max<int>(1, std::min<int>(8, int((160 * 1024) / ldsm)));
+      int64_t nbm = int64_t(ctx->num_cus) * wgm;
+      // whole number of row ranges per strip, at least one wave per strip
+      int64_t nwv = nbm * nwm;
+      if (nwv >= nstrips) {
+        nwv = (nwv / nstrips) * nstrips;
+        nbm = nwv / nwm;
+        if (nbm * nwm == nwv && nbm >= 1) {
+          TimedLaunch tlm(ctx, GNK_TIMER_GRAM, 8.0 * double(nown) * double(k + 1 + (r ? 1 : 0)));
+          const int cgm = 64 / (chm / 2);
+          const int mcn = (k + cgm - 1) / cgm;      // columns per lane
+#define GRAMM(NBV, CHV, MCV)                                                                                   \
+  hipLaunchKernelGGL((k_gram_m<NBV, CHV, MCV>), dim3(unsigned(nbm)), dim3(64 * nwm), ldsm, ctx->stream, u, V, ldv, \
+                     k, rinv, r, ctx->geo, ctx->coef, ctx->scratch)
+          if (nb == 1) {
+            if (mcn <= 2) GRAMM(1, 64, 2);
+            else if (mcn <= 4) GRAMM(1, 64, 4);
+            else GRAMM(1, 64, 8);
+          } else {
+            if (mcn <= 4) GRAMM(2, 32, 4);
+            else if (mcn <= 6) GRAMM(2, 32, 6);
+            else GRAMM(2, 32, 8);
+          }
+#undef GRAMM
+          tlm.done();
+          int rcm = check_launch(ctx, "gram_m");
+          if (rcm) return rcm;
+          (void)hipMemsetAsync(G_out, 0, size_t(KP) * KP * sizeof(double), ctx->stream);
+          double* red = ctx->scratch + (SCRATCH_DOUBLES - size_t(P) * 256);
+          rcm = wreduce(ctx, ctx->scratch, int(nbm), P * 256, int64_t(P) * 256, P * 256, 0, nullptr, red);
+          if (rcm) return rcm;
+          hipLaunchKernelGGL(k_gram_scatter, dim3((P * 256 + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, ctx->stream, red, P,
+                             KP, G_out);
+          return check_launch(ctx, "gram scatter");
+        }
+      }
+    }
     TimedLaunch tl(ctx, GNK_TIMER_GRAM, 8.0 * double(nown) * double(k + 1 + (r ? 1 : 0)));
-#define GRAMW1(PP, BCV, CHV) hipLaunchKernelGGL((k_gram_w<PP, BCV, CHV>), dim3(unsigned(nblk)), dim3(64 * nwave),   \
-                                                ldsw, ctx->stream, u, V, ldv, k, rinv, r, ctx->geo, ctx->coef, KP, \
-                                                P, nch, ctx->scratch, dbg)
+#define GRAMW1(NBV, BCV, CHV) hipLaunchKernelGGL((k_gram_w<NBV, BCV, CHV>), dim3(unsigned(nblk)), dim3(64 * nwave), \
+                                                 ldsw, ctx->stream, u, V, ldv, k, rinv, r, ctx->geo, ctx->coef,     \
+                                                 nch, ctx->scratch, dbg)
 #define GRAMW(PP)                                                  \
   do {                                                             \
     if (chv == 64) {                                               \
@@ -1368,10 +1582,10 @@ int gnk_gram(gnk_ctx* ctx, const double* u, const double* V, int64_t ldv, int k,
       if (bc == 1) GRAMW1(PP, 1, 32); else GRAMW1(PP, 2, 32);      \
     }                                                              \
   } while (0)
-    if (P == 1) GRAMW(1);
-    else if (P <= 3) GRAMW(3);
-    else if (P <= 6) GRAMW(6);
-    else GRAMW(10);
+    if (nb == 1) GRAMW(1);
+    else if (nb == 2) GRAMW(2);
+    else if (nb == 3) GRAMW(3);
+    else GRAMW(4);
 #undef GRAMW
 #undef GRAMW1
     tl.done();

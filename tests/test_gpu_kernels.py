@@ -127,7 +127,10 @@ def test_cgs_max_propagates_nan():
 
 @pytest.mark.parametrize("N,k,with_r,with_rinv", [(24, 1, False, False), (24, 5, True, True), (100, 20, False, False),
                                                   (100, 20, True, True), (64, 47, True, True), (64, 70, True, False),
-                                                  (1024, 20, True, True)])
+                                                  (1024, 20, True, True),
+                                                  # marching kernel (N % 64 == 0): NB = 1 both passes, NB = 2 pass 1
+                                                  (1024, 3, False, False), (1024, 12, True, True), (128, 15, False, True),
+                                                  (1024, 25, False, False), (256, 31, False, False)])
 def test_gram_mfma(N, k, with_r, with_rinv):
     """W = [J V | r] @ RinvAug on fp64 MFMA vs an fp64 NumPy Gram (host BLAS)."""
     prob, dev, ref = make(N)
