@@ -41,6 +41,7 @@ SIGNATURES = {
     "gnk_cgs_update": (_c_int, [_c_vp, _c_vp, _c_i64, _c_int, _c_vp, _c_vp, _c_vp]),
     "gnk_vec_stats": (_c_int, [_c_vp, _c_vp, _c_vp]),
     "gnk_vec_div": (_c_int, [_c_vp, _c_vp, _c_dbl, _c_vp, _c_int]),
+    "gnk_normalize_jnorm": (_c_int, [_c_vp, _c_vp, _c_vp, _c_dbl, _c_vp, _c_vp]),
     "gnk_vec_axpy": (_c_int, [_c_vp, _c_vp, _c_dbl, _c_vp, _c_vp, _c_int]),
     "gnk_gram_padded_dim": (_c_int, [_c_int, _c_int]),
     "gnk_gram": (_c_int, [_c_vp, _c_vp, _c_vp, _c_i64, _c_int, _c_vp, _c_i64, _c_vp, _c_vp]),
@@ -176,6 +177,9 @@ class HipBackend:
 
     def vec_div(self, src, denom, dst, full_slab):
         self._call("gnk_vec_div", _p(src), float(denom), _p(dst), int(bool(full_slab)))
+
+    def normalize_jnorm(self, u, g, denom, v, jn2):
+        self._call("gnk_normalize_jnorm", _p(u), _p(g), float(denom), _p(v), _p(jn2))
 
     def vec_axpy(self, x, alpha, d, out, full_slab):
         self._call("gnk_vec_axpy", _p(x), float(alpha), _p(d), _p(out), int(bool(full_slab)))

@@ -440,6 +440,55 @@ __global__ __launch_bounds__(BLOCK) void k_div(const double* __restrict__ src, d
   ROW_LOOP_END
 }
 
+// v = g / denom on the whole slab (g's ghost rows already exchanged, so each rank's
+// ghost copy equals its neighbour's owned value bit for bit) and, on owned rows,
+// partial sum of (J(u) g)^2 from the same loads; the host divides by denom^2 to get
+// ||J v_new||^2, the appended column's scale in the next least-squares preconditioner
+// (not a parity quantity: one division per point instead of five).  v must not alias g.
+template <int VEC>
+__global__ __launch_bounds__(BLOCK) void k_div_jnorm(const double* __restrict__ u, const double* __restrict__ g,
+                                                     double denom, double* __restrict__ v, Geo geo, Coef c,
+                                                     int64_t lr0, int64_t nlr, double* __restrict__ partial) {
+  __shared__ double sh[BLOCK / 64];
+  const int lane = threadIdx.x & 63;
+  double acc[1] = {0.0};
+  ROW_LOOP_BEGIN(VEC)
+  const bool owned = lr >= G && lr < G + geo.nrows;   // block-uniform
+  if (!owned) {
+    for (int q = 0; q < VEC && iy + q < N; ++q) v[li + q] = g[li + q] / denom;
+    continue;
+  }
+  if (VEC == 2 && iy + 1 < N) {
+    const d2 uc = *reinterpret_cast<const d2*>(u + li);
+    const d2 gc = *reinterpret_cast<const d2*>(g + li);
+    const d2 gn = *reinterpret_cast<const d2*>(g + li - N);
+    const d2 gs = *reinterpret_cast<const d2*>(g + li + N);
+    const bool hw = iy > 0, he = iy + 2 < N;
+    double gw = __shfl_up(gc.y, 1);
+    double ge = __shfl_down(gc.x, 1);
+    if (lane == 0) gw = hw ? g[li - 1] : 0.0;
+    if (lane == 63 || iy + 2 >= N) ge = he ? g[li + 2] : 0.0;
+    *reinterpret_cast<d2*>(v + li) = d2{gc.x / denom, gc.y / denom};
+    const double j0 = jvp_pt(c, jdiag(c, uc.x), gn.x, gw, hw, gc.x, gc.y, true, gs.x);
+    const double j1 = jvp_pt(c, jdiag(c, uc.y), gn.y, gc.x, true, gc.y, ge, he, gs.y);
+    acc[0] += j0 * j0;
+    acc[0] += j1 * j1;
+  } else {
+    for (int q = 0; q < VEC; ++q) {
+      const int64_t i = li + q;
+      const int64_t y = iy + q;
+      if (y >= N) break;
+      const bool hw = y > 0, he = y < N - 1;
+      v[i] = g[i] / denom;
+      const double gw = hw ? g[i - 1] : 0.0, ge = he ? g[i + 1] : 0.0;
+      const double jg = jvp_pt(c, jdiag(c, u[i]), g[i - N], gw, hw, g[i], ge, he, g[i + N]);
+      acc[0] += jg * jg;
+    }
+  }
+  ROW_LOOP_END
+  block_sum_store<1>(acc, 1, partial + (blockIdx.y * gridDim.x + blockIdx.x), sh);
+}
+
 // out = x + (alpha * d): the two roundings of NumPy's `x + step_length * descent_direction`
 template <int VEC>
 __global__ __launch_bounds__(BLOCK) void k_axpy(const double* __restrict__ x, double alpha, const double* __restrict__ d,
@@ -1113,6 +1162,237 @@ __global__ __launch_bounds__(BLOCK) void k_gram_m(const double* __restrict__ u, 
   for (int idx = tid; idx < P * 256; idx += blockDim.x) out[idx] = red[idx];
 }
 
+// ---------------------------------------------------------------- staged Gram pass (LDS-DMA ring)
+// One workgroup (8 waves) walks a vertical strip of GS_SW = 128 grid points down a range of grid
+// rows.  The raw rows of every basis column, u and r stream global -> LDS by LDS-DMA
+// (global_load_lds_dwordx4, no VGPR staging) two grid rows ahead into a 5-slot ring:
+//   slot(x) = x mod 5 holds row x of [V_0 .. V_{k-1}, u, (r)] (column stride GS_CS doubles) and a
+//   halo block (the strip's outer neighbours of every column).
+// Wave w owns points 16w .. 16w+15 of each step.  It builds its A fragments of W = [J V | r]
+// straight in the MFMA operand layout (lane: point l&15, column block l>>4) from five LDS reads
+// per value, transforms them on MFMA with the RinvAug B fragments held in VGPRs (W <- W P^-1),
+// and -- because the transform's C/D layout equals the Gram's A/B operand layout -- feeds the
+// transformed rows to the Gram MFMAs directly from registers.  No LDS tile round trip, no
+// producer/consumer hand-off: the barrier per step only retires the ring slots.
+// GS_CS = 144 == 16 (mod 32): the A-fragment reads of a half-wave (16 points x 2 columns) hit
+// 64 distinct banks.
+#ifndef GNK_SDBG
+#define GNK_SDBG 0      // tooling-only ablation builds (tools/abl_build.sh): 1 = no DMA in the step
+#endif                  // loop, 2 = no stencil fragments, 4 = no MFMAs
+constexpr int GS_SW = 128;
+constexpr int GS_CS = 144;
+constexpr int GS_R = 5;
+constexpr int GS_NW = 8;
+
+typedef __attribute__((address_space(3))) void* lds_vp;
+typedef __attribute__((address_space(1))) const void* glb_cvp;
+
+// s_waitcnt with vmcnt(n) and lgkmcnt(0), expcnt untouched (gfx9 encoding)
+constexpr unsigned waitcnt_vm_lgkm0(int n) { return unsigned((n & 0xF) | ((n >> 4) << 14) | (0x7 << 4)); }
+
+template <int NB, int L, int KSL>
+__global__ __launch_bounds__(64 * GS_NW) void k_gram_s(const double* __restrict__ u, const double* __restrict__ V,
+                                                       int64_t ldv, int k, const double* __restrict__ rinv,
+                                                       const double* __restrict__ r, Geo geo, Coef cf,
+                                                       int64_t rpr, double* __restrict__ partial) {
+  constexpr int KP = 16 * NB, P = NB * (NB + 1) / 2;
+  extern __shared__ __attribute__((aligned(16))) double lds[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int64_t N = geo.N;
+  const int nrow = k + 1 + (r ? 1 : 0);             // LDS rows per slot: V_0..V_{k-1}, u, (r)
+  const int slotd = nrow * GS_CS + 128;             // + halo block: 64 lanes x 16 B
+  const int ninst = nrow + 1;                       // DMA instructions per grid row (rows + halo)
+
+  // block -> (row range, strip); consecutive range-major tiles share an XCD (blockIdx % 8),
+  // so strip neighbours read each other's halo lines from the same L2
+  const int nstrips = int(N / GS_SW);
+  const int nwg = gridDim.x, b = blockIdx.x;
+  const int idx = (nwg % 8 == 0) ? (b % 8) * (nwg / 8) + b / 8 : b;
+  const int64_t x0 = int64_t(idx / nstrips) * rpr;
+  const int64_t x1 = min(geo.nrows, x0 + rpr);
+  const int64_t col0 = int64_t(idx % nstrips) * GS_SW;
+
+  // KSL = 4-column k-steps of the last column block holding columns < K1 (compile time: the
+  // transform below is straight-line, no guards)
+  auto nks = [](int ab) constexpr { return ab == NB - 1 ? KSL : 4; };
+  // RinvAug B fragments [cb][ab][ks] (ordinary loads, before any DMA is in flight)
+  double rB[NB][NB][4];
+#pragma unroll
+  for (int cb = 0; cb < NB; ++cb)
+#pragma unroll
+    for (int ab = 0; ab <= cb; ++ab)
+#pragma unroll
+      for (int ks = 0; ks < nks(ab); ++ks) {
+        rB[cb][ab][ks] = rinv[(ab * 16 + ks * 4 + (lane >> 4)) * KP + cb * 16 + (lane & 15)];
+        // opaque use: the load retires here, before the first DMA (a VGPR load still counted
+        // when a DMA is in flight makes hipcc wait vmcnt(0) at its first use in the step loop)
+        asm volatile("" : "+v"(rB[cb][ab][ks]));
+      }
+  d4 acc[P];
+#pragma unroll
+  for (int q = 0; q < P; ++q) acc[q] = d4{0.0, 0.0, 0.0, 0.0};
+
+  // This wave's DMA instructions q = wave + 8m (a q past the end re-loads the u row: same bytes,
+  // same place).  Per instruction: a wave-uniform source base (row 0 of the column at the strip),
+  // a per-lane offset and the LDS offset inside a slot -- all fixed; a step only adds the row.
+  const double* dsrc[L];                            // per lane: row 0 of the source at the strip
+  int ddst[L];
+#pragma unroll
+  for (int m = 0; m < L; ++m) {
+    int q = wave + GS_NW * m;
+    if (q >= ninst) q = k;
+    if (q < nrow) {
+      const double* rowp = q < k ? V + int64_t(q) * ldv : (q == k ? u : r);
+      dsrc[m] = rowp + col0 + 2 * lane;
+      ddst[m] = q * GS_CS;
+    } else {
+      const int cc = min(lane >> 1, k - 1);          // halo: lane -> column lane/2, side lane&1
+      dsrc[m] = V + int64_t(cc) * ldv + col0 + ((lane & 1) ? GS_SW : -2);
+      ddst[m] = nrow * GS_CS;
+    }
+  }
+  const int64_t rmax = geo.nrows + G - 1;           // last slab row (ghost)
+  auto issue_row = [&](int64_t xr, int slot) {     // rows past the slab re-load the last one
+    const int64_t roff = (G + min(xr, rmax)) * N;
+    double* sbase = lds + slot * slotd;
+#pragma unroll
+    for (int m = 0; m < L; ++m)
+      __builtin_amdgcn_global_load_lds((glb_cvp)(dsrc[m] + roff), (lds_vp)(sbase + ddst[m]), 16, 0, 0);
+  };
+
+  // fixed per-lane stencil offsets of every fragment (column j = 16ab + 4ks + l>>4, point e)
+  const int e = wave * 16 + (lane & 15);            // this lane's point in the strip
+  const int cq = lane >> 4;
+  const double cwm = (col0 + e > 0) ? cf.hm2 : 0.0;
+  const double cem = (col0 + e + 1 < N) ? cf.hm2 : 0.0;
+  const double up = -cf.j_lin_up;
+  int fo[NB][4], fw[NB][4], fe[NB][4];
+  unsigned fv = 0, fr = 0;                          // per fragment bit: V column / r column
+#pragma unroll
+  for (int ab = 0; ab < NB; ++ab)
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      const int j = ab * 16 + ks * 4 + cq;
+      const bool isV = j < k, isR = (r != nullptr) && j == k;
+      const int jr = isV ? j : (isR ? k + 1 : 0);
+      fo[ab][ks] = jr * GS_CS + e;
+      fw[ab][ks] = e > 0 ? jr * GS_CS + e - 1 : nrow * GS_CS + 4 * jr + 1;             // halo: element -1
+      fe[ab][ks] = e < GS_SW - 1 ? jr * GS_CS + e + 1 : nrow * GS_CS + 4 * jr + 2;     // halo: element 128
+      fv |= unsigned(isV) << (ab * 4 + ks);
+      fr |= unsigned(isR) << (ab * 4 + ks);
+    }
+  const int ou = k * GS_CS + e;
+
+  // Software pipeline inside the wave (2 waves/SIMD cannot hide the latency chains):
+  //   step x: A fragments of row x (LDS reads, FMAs) with dn(x) computed during step x-1;
+  //           dn(x+1) = -jdiag(u(x+1)) (the exp chain runs under the MFMAs);
+  //           transform(x) interleaved with the independent Gram MFMAs of row x-1.
+  double a[NB][4];
+  d4 qp[NB];                                        // transformed rows of the previous step
+  auto transform = [&](d4 (&qv)[NB]) {
+#pragma unroll
+    for (int cb = 0; cb < NB; ++cb) {
+      qv[cb] = d4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+      for (int ab = 0; ab <= cb; ++ab)
+#pragma unroll
+        for (int ks = 0; ks < nks(ab); ++ks) qv[cb] = mfma64(a[ab][ks], rB[cb][ab][ks], qv[cb]);
+    }
+  };
+  // qv[cb][i] = Y[16w + (l>>4) + 4i][16cb + (l&15)] == the Gram operand of rows 4i..4i+3
+  auto gram = [&](const d4 (&qv)[NB]) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int q = 0; q < P; ++q) acc[q] = mfma64(qv[pair_a(q, NB)][i], qv[pair_b(q, NB)][i], acc[q]);
+  };
+  if (x0 < x1) {
+    // ring slots rotate: sn/sc/ss = rows x-1, x, x+1; sd = row x+3 (the slot of row x-2)
+    int sn = int((x0 - 1 + GS_R) % GS_R), sc = int(x0 % GS_R), ss = int((x0 + 1) % GS_R);
+    int sp = int((x0 + 2) % GS_R), sd = int((x0 + 3) % GS_R);
+    issue_row(x0 - 1, sn);
+    issue_row(x0, sc);
+    issue_row(x0 + 1, ss);
+    issue_row(x0 + 2, sp);
+    __builtin_amdgcn_s_waitcnt(waitcnt_vm_lgkm0(L));    // rows x0-1 .. x0+1 landed
+    __builtin_amdgcn_s_barrier();
+    double dn = -jdiag(cf, lds[sc * slotd + ou]);
+    // fragments of row x from the ring (slots n/c/s) with dn(x); then dn(x+1) from slot s
+    auto fragments = [&](const double* Ln, const double* Lc, const double* Ls) {
+#pragma unroll
+      for (int ab = 0; ab < NB; ++ab)
+#pragma unroll
+        for (int ks = 0; ks < nks(ab); ++ks) {
+          if (GNK_SDBG & 2) { a[ab][ks] = dn; continue; }
+          const int o = fo[ab][ks];
+          const double vn = Ln[o], vw = Lc[fw[ab][ks]], vc = Lc[o], ve = Lc[fe[ab][ks]], vs = Ls[o];
+          const bool isV = (fv >> (ab * 4 + ks)) & 1, isR = (fr >> (ab * 4 + ks)) & 1;
+          // J V with explicit FMAs in CSR term order (as k_gram_w); the r column is
+          // 0*n + 0*w + 1*c + 0*e + 0*s == r exactly, padding columns are 0
+          const double cn = isV ? cf.hm2 : 0.0, cw = isV ? cwm : 0.0;
+          const double cc = isV ? dn : (isR ? 1.0 : 0.0);
+          const double ce = isV ? cem : 0.0, cs = isV ? up : 0.0;
+          double sv = cn * vn;
+          sv = fma(cw, vw, sv);
+          sv = fma(cc, vc, sv);
+          sv = fma(ce, ve, sv);
+          sv = fma(cs, vs, sv);
+          a[ab][ks] = sv;
+        }
+      dn = -jdiag(cf, Ls[ou]);
+    };
+    // transform of the current fragments, interleaved with the Gram of the previous rows
+    auto mfmas = [&](bool with_prev) {
+      d4 qv[NB];
+      if (GNK_SDBG & 4) {
+#pragma unroll
+        for (int cb = 0; cb < NB; ++cb) qv[cb] = d4{a[0][0], a[0][0], a[0][0], a[0][0]};
+      } else {
+        transform(qv);
+        if (with_prev) gram(qp);
+      }
+#pragma unroll
+      for (int cb = 0; cb < NB; ++cb) qp[cb] = qv[cb];
+    };
+    // (A stagger -- waves 4-7 running MFMAs(x-1) before fragments(x) beside waves 0-3 -- measured
+    // 10-50 % slower on MI355X than this in-wave pipeline; not used.)
+    for (int64_t x = x0; x < x1; ++x) {
+      if (!(GNK_SDBG & 1)) issue_row(x + 3, sd);
+      fragments(lds + sn * slotd, lds + sc * slotd, lds + ss * slotd);
+      mfmas(x > x0);
+      const int t = sn;
+      sn = sc;
+      sc = ss;
+      ss = sp;
+      sp = sd;
+      sd = t;
+      __builtin_amdgcn_s_waitcnt(waitcnt_vm_lgkm0(L));  // row x+2 landed; only row x+3 in flight
+      __builtin_amdgcn_s_barrier();
+    }
+    if (!(GNK_SDBG & 4)) gram(qp);
+  }
+  __builtin_amdgcn_s_waitcnt(waitcnt_vm_lgkm0(0));
+  __builtin_amdgcn_s_barrier();
+
+  // block partial = ((w0 + w1) + w2) + ... through LDS, layout [block][pair][lane*4 + i]
+  double* red = lds;
+  for (int w = 0; w < GS_NW; ++w) {
+    if (wave == w) {
+#pragma unroll
+      for (int q = 0; q < P; ++q)
+#pragma unroll
+        for (int ii = 0; ii < 4; ++ii) {
+          double* dst = red + q * 256 + lane * 4 + ii;
+          *dst = (w == 0) ? acc[q][ii] : *dst + acc[q][ii];
+        }
+    }
+    __syncthreads();
+  }
+  double* out = partial + size_t(blockIdx.x) * size_t(P) * 256;
+  for (int t = tid; t < P * 256; t += blockDim.x) out[t] = red[t];
+}
+
 // Sum Gram partials over blocks (block order) and scatter into G[KP][KP] (symmetric).
 // scatter the reduced pair tiles (red[pair * 256 + lane * 4 + i]) into symmetric G[KP][KP]
 __global__ __launch_bounds__(BLOCK) void k_gram_scatter(const double* __restrict__ red, int P, int KP,
@@ -1175,6 +1455,7 @@ struct gnk_ctx {
   Geo geo{0, 0, 0};
   Coef coef{};
   double* scratch = nullptr;
+  double* ident = nullptr;     // 16x16 and 32x32 identities (RinvAug of an unpreconditioned pass)
   int num_cus = 256;
   std::string err;
   // per-launch timer (tooling, see gnk_timer_start)
@@ -1306,6 +1587,18 @@ int gnk_ctx_create(int device, gnk_ctx** out) {
     delete ctx;
     return -3;
   }
+  {
+    std::vector<double> id(256 + 1024, 0.0);
+    for (int i = 0; i < 16; ++i) id[i * 16 + i] = 1.0;
+    for (int i = 0; i < 32; ++i) id[256 + i * 32 + i] = 1.0;
+    e = hipMalloc(&ctx->ident, id.size() * sizeof(double));
+    if (e == hipSuccess) e = hipMemcpy(ctx->ident, id.data(), id.size() * sizeof(double), hipMemcpyHostToDevice);
+    if (e != hipSuccess) {
+      (void)hipFree(ctx->scratch);
+      delete ctx;
+      return -3;
+    }
+  }
   *out = ctx;
   return 0;
 }
@@ -1314,6 +1607,7 @@ void gnk_ctx_destroy(gnk_ctx* ctx) {
   if (!ctx) return;
   for (hipEvent_t e : ctx->timer_ev) (void)hipEventDestroy(e);
   if (ctx->scratch) (void)hipFree(ctx->scratch);
+  if (ctx->ident) (void)hipFree(ctx->ident);
   delete ctx;
 }
 
@@ -1429,25 +1723,33 @@ int gnk_vjp_gemv_t(gnk_ctx* ctx, const double* u, const double* r, const double*
   if (k < 0) return fail(ctx, "vjp_gemv_t: k < 0");
   if (k > 0 && !V) return fail(ctx, "vjp_gemv_t: V is NULL");
   if (vec_of(ctx) == 2 && (ldv % 2 != 0)) return fail(ctx, "vjp_gemv_t: ldv must be even");
-  const int kct = k <= 8 ? 8 : 16;
+  // one chunk of the smallest compiled width >= k up to 24 columns, else 16-column chunks
+  const int kct = k <= 24 ? std::max(4, (k + 3) / 4 * 4) : 16;
   const int nchunk = std::max(1, (k + kct - 1) / kct);
-  RowLaunch L = rows(ctx, G, ctx->geo.nrows, vec_of(ctx), std::max(64, 2048 / nchunk));
+  static const int cap_env = getenv("GNK_VJPG_CAP") ? atoi(getenv("GNK_VJPG_CAP")) : 0;  // tooling A/B switch
+  RowLaunch L = rows(ctx, G, ctx->geo.nrows, vec_of(ctx), cap_env ? cap_env : std::max(64, 2048 / nchunk));
   L.grid.z = nchunk;
   const int nblk = L.grid.x * L.grid.y;
   if (size_t(nblk) * nchunk * kct > SCRATCH_DOUBLES) return fail(ctx, "vjp_gemv_t: scratch too small");
-  if (vec_of(ctx) == 2) {
-    if (kct == 8) hipLaunchKernelGGL((k_vjp_gemv_t<2, 8>), L.grid, dim3(BLOCK), 0, ctx->stream, u, r, V, ldv, k, g,
-                                     ctx->geo, ctx->coef, L.lr0, L.nlr, ctx->scratch);
-    else hipLaunchKernelGGL((k_vjp_gemv_t<2, 16>), L.grid, dim3(BLOCK), 0, ctx->stream, u, r, V, ldv, k,
-                            g, ctx->geo, ctx->coef, L.lr0, L.nlr, ctx->scratch);
-
-  } else {
-    if (kct == 8) hipLaunchKernelGGL((k_vjp_gemv_t<1, 8>), L.grid, dim3(BLOCK), 0, ctx->stream, u, r, V, ldv, k, g,
-                                     ctx->geo, ctx->coef, L.lr0, L.nlr, ctx->scratch);
-    else hipLaunchKernelGGL((k_vjp_gemv_t<1, 16>), L.grid, dim3(BLOCK), 0, ctx->stream, u, r, V, ldv, k,
-                            g, ctx->geo, ctx->coef, L.lr0, L.nlr, ctx->scratch);
-
+#define VJPG_LAUNCH(V_, K_)                                                                                 \
+  hipLaunchKernelGGL((k_vjp_gemv_t<V_, K_>), L.grid, dim3(BLOCK), 0, ctx->stream, u, r, V, ldv, k, g, ctx->geo, \
+                     ctx->coef, L.lr0, L.nlr, ctx->scratch)
+#define VJPG_SWITCH(V_)                  \
+  switch (kct) {                         \
+    case 4: VJPG_LAUNCH(V_, 4); break;   \
+    case 8: VJPG_LAUNCH(V_, 8); break;   \
+    case 12: VJPG_LAUNCH(V_, 12); break; \
+    case 16: VJPG_LAUNCH(V_, 16); break; \
+    case 20: VJPG_LAUNCH(V_, 20); break; \
+    default: VJPG_LAUNCH(V_, 24); break; \
   }
+  if (vec_of(ctx) == 2) {
+    VJPG_SWITCH(2)
+  } else {
+    VJPG_SWITCH(1)
+  }
+#undef VJPG_SWITCH
+#undef VJPG_LAUNCH
   int rc = check_launch(ctx, "vjp_gemv_t");
   if (rc || k == 0 || !h_out) return rc;
   return wreduce(ctx, ctx->scratch, nblk, k, kct, kct, int64_t(nblk) * kct, nullptr, h_out);
@@ -1484,6 +1786,19 @@ int gnk_vec_div(gnk_ctx* ctx, const double* src, double denom, double* dst, int 
   return check_launch(ctx, "vec_div");
 }
 
+int gnk_normalize_jnorm(gnk_ctx* ctx, const double* u, const double* g, double denom, double* v,
+                        double* jnorm2_out) {
+  if (!ready(ctx)) return -1;
+  if (!u || !g || !v) return fail(ctx, "normalize_jnorm: NULL vector");
+  if (g == v) return fail(ctx, "normalize_jnorm: v must not alias g (stencil reads of g)");
+  RowLaunch L = rows(ctx, 0, ctx->geo.nrows + 2 * G, vec_of(ctx));
+  const int nblk = L.grid.x * L.grid.y;
+  DISPATCH_VEC(ctx, k_div_jnorm, L, 0, u, g, denom, v, ctx->geo, ctx->coef, L.lr0, L.nlr, ctx->scratch);
+  int rc = check_launch(ctx, "normalize_jnorm");
+  if (rc || !jnorm2_out) return rc;
+  return reduce(ctx, ctx->scratch, nblk, 1, 1, nullptr, jnorm2_out);   // sum (J g)^2
+}
+
 int gnk_vec_axpy(gnk_ctx* ctx, const double* x, double alpha, const double* d, double* out, int full_slab) {
   if (!ready(ctx)) return -1;
   RowLaunch L = full_slab ? rows(ctx, 0, ctx->geo.nrows + 2 * G, vec_of(ctx), 1 << 30)
@@ -1502,6 +1817,62 @@ int gnk_gram(gnk_ctx* ctx, const double* u, const double* V, int64_t ldv, int k,
   if (rinv && ldr != KP) return fail(ctx, "gram: rinv must be the kp x kp augmented inverse (ldr == kp)");
   const int nb = KP / 16;
   const int P = nb * (nb + 1) / 2;
+  // partials [block][P * 256] -> red[P * 256] (scratch tail) -> symmetric G
+  auto finish = [&](int nblocks) -> int {
+    (void)hipMemsetAsync(G_out, 0, size_t(KP) * KP * sizeof(double), ctx->stream);
+    double* red = ctx->scratch + (SCRATCH_DOUBLES - size_t(P) * 256);
+    int rc = wreduce(ctx, ctx->scratch, nblocks, P * 256, int64_t(P) * 256, P * 256, 0, nullptr, red);
+    if (rc) return rc;
+    hipLaunchKernelGGL(k_gram_scatter, dim3((P * 256 + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, ctx->stream, red, P, KP,
+                       G_out);
+    return check_launch(ctx, "gram scatter");
+  };
+  const char* staged_s = getenv("GNK_GRAM_STAGED");        // read per call: tests force the kernel
+  const int staged_env = staged_s ? atoi(staged_s) : 1;
+  // staged kernel for the preconditioned pass (measured: faster than the chunked / marching
+  // kernels from k = 4 up; the marching kernel stays faster for the plain pass);
+  // GNK_GRAM_STAGED=2 forces it for every pass (tests), 0 disables it
+  if (staged_env && (staged_env == 2 || (rinv && k >= 4)) && nb <= 2 && ctx->geo.N % GS_SW == 0 &&
+      !getenv("GNK_DEBUG_GRAM")) {
+    const int nrow = k + 1 + (r ? 1 : 0);
+    const int L = (nrow + 1 + GS_NW - 1) / GS_NW;
+    const size_t lds = size_t(GS_R) * (size_t(nrow) * GS_CS + 128) * sizeof(double);
+    if (L <= 4 && lds <= 160 * 1024) {
+      const double* rv = rinv ? rinv : ctx->ident + (nb == 1 ? 0 : 256);
+      const int wgpc = std::max(1, std::min(2, int((160 * 1024) / lds)));
+      const int64_t nstrips = ctx->geo.N / GS_SW;
+      const int64_t nrows = ctx->geo.nrows;
+      int64_t nranges = std::max<int64_t>(1, std::min<int64_t>(nrows, int64_t(ctx->num_cus) * wgpc / nstrips));
+      const int64_t rpr = (nrows + nranges - 1) / nranges;
+      nranges = (nrows + rpr - 1) / rpr;
+      const int64_t nwg = nstrips * nranges;
+      if (nwg > (1 << 20) || size_t(nwg) * P * 256 > SCRATCH_DOUBLES - size_t(P) * 256)
+        return fail(ctx, "gram: scratch too small (staged)");
+      const int64_t nown = nrows * ctx->geo.N;
+      TimedLaunch tls(ctx, GNK_TIMER_GRAM, 8.0 * double(nown) * double(k + 1 + (r ? 1 : 0)));
+#define GRAMS(NBV, LV, KV)                                                                                    \
+  hipLaunchKernelGGL((k_gram_s<NBV, LV, KV>), dim3(unsigned(nwg)), dim3(64 * GS_NW), lds, ctx->stream, u, V, ldv, k, \
+                     rv, r, ctx->geo, ctx->coef, rpr, ctx->scratch)
+#define GRAMS_K(NBV, LV)                                                    \
+  do {                                                                      \
+    if (ksl == 1) GRAMS(NBV, LV, 1); else if (ksl == 2) GRAMS(NBV, LV, 2);  \
+    else if (ksl == 3) GRAMS(NBV, LV, 3); else GRAMS(NBV, LV, 4);           \
+  } while (0)
+      // 4-column k-steps of the last column block that hold columns < K1
+      const int ksl = ((k + (r ? 1 : 0) - 16 * (nb - 1)) + 3) / 4;
+      if (nb == 1) {
+        if (L == 1) GRAMS_K(1, 1); else if (L == 2) GRAMS_K(1, 2); else if (L == 3) GRAMS_K(1, 3); else GRAMS_K(1, 4);
+      } else {
+        if (L == 1) GRAMS_K(2, 1); else if (L == 2) GRAMS_K(2, 2); else if (L == 3) GRAMS_K(2, 3); else GRAMS_K(2, 4);
+      }
+#undef GRAMS_K
+#undef GRAMS
+      tls.done();
+      const int rcs = check_launch(ctx, "gram_s");
+      if (rcs) return rcs;
+      return finish(int(nwg));
+    }
+  }
   if (KP <= 64) {
     // wave-independent streaming kernel (GNK_DEBUG_GRAM: tooling-only ablation switch,
     // 1 = no loads, 2 = no Gram MFMAs)

@@ -10,7 +10,7 @@ every exception -- and runs each n-sized operation on the GPU:
     1 Gram pass (fp64 MFMA, J V P^-1 on the fly; P = previous R factor, a 2nd pass
       only when the preconditioned factor is not well conditioned) -> LS solve (lls.py)
     a x [basis GEMV + fused residual/||r||^2]   -> Armijo trials
-    fused -J^T r + V^T g, CGS update + stats, normalise, halo, ||J v_new|| -> basis update
+    fused -J^T r + V^T g, CGS update + stats, halo, normalise + ||J v_new|| -> basis update
 
 Host <-> device traffic per iteration is O(k^2) doubles (Gram matrices, k
 coefficients, a few scalars).  ``GNKSolver`` exposes the same loop one outer
@@ -76,22 +76,12 @@ class GNKSolver:
         self.xb = [self.dev.vec() for _ in range(3)]
         self.rb = [self.dev.vec() for _ in range(2)]
         self._n2 = self.dev.scalar(1)
-        self._st = self.dev.scalar(2)
         self.trace = []          # per-iteration (t, k, trials) for tests / diagnostics
 
     # -- pieces -------------------------------------------------------------------------
     def _residual(self, x, r) -> float:
         self.be.residual(x, self.y, r, self._n2)
         return float(self.comm.sum(self._n2)[0])
-
-    def _precondition_new_column(self):
-        """s = ||J(u) v_new|| for the next least-squares pass's preconditioner (lls.py)."""
-        k = self.basis.k
-        tmp = self.xb[self._free_x(self.uJ)]
-        self.be.jvp(self.xb[self.uJ], self.basis.V[k - 1], tmp)
-        self.be.vec_stats(tmp, self._st)
-        ss, _ = self.comm.sum_max(self._st)
-        self.lls.on_append(np.sqrt(ss))
 
     def _free_x(self, *busy):
         for i in range(3):
@@ -156,20 +146,21 @@ class GNKSolver:
             return True
         uJ_old, self.uJ = self.uJ, xi                                     # :106-108
         self.njev += 1
+        u_new = self.xb[self.uJ]      # the next LS solve's J; s = ||J(u_new) v_new|| (lls.py)
         try:
             if self.version == "res_old":
-                basis.update(self.xb[self.uJ], r_old)
+                s_new = basis.update(u_new, r_old, u_new)
             elif self.version == "res_new":
-                basis.update(self.xb[self.uJ], r_t)
+                s_new = basis.update(u_new, r_t, u_new)
             elif self.version == "jac_old_res_old":
-                basis.update(self.xb[uJ_old], r_old)
+                s_new = basis.update(self.xb[uJ_old], r_old, u_new)
             elif self.version == "jac_old_res_new":
-                basis.update(self.xb[uJ_old], r_t)
+                s_new = basis.update(self.xb[uJ_old], r_t, u_new)
             else:
                 raise ValueError(
                     "Variable version must be in ['res_old','res_new','jac_old_res_old','jac_old_res_new']")
             self.c = np.append(self.c, 0)                                 # :124
-            self._precondition_new_column()
+            self.lls.on_append(s_new)
         except GeneralizedKrylowSubspaceBreakdown:
             print(f"Generalized krylow subspace breakdown at iteration = {it}, basis.shape = {basis.shape}")
         except GeneralizedKrylowSubspaceSpansEntireSpace:

@@ -35,6 +35,8 @@ class DeviceKrylovBasis:
         self._c = self.be.zeros(self.kmax)
         self._h = self.be.zeros(self.kmax)
         self._stats = self.be.zeros(2)
+        self._g = dev.vec()              # new column before normalisation (stencil source)
+        self._jn2 = self.be.zeros(1)
 
     @property
     def shape(self):
@@ -59,14 +61,17 @@ class DeviceKrylovBasis:
         self.be.gemv(self.V, k, self._c, out)
         return out
 
-    def update(self, u_jac, r):
-        """ref:krylow.py:55-73 with jac_ev = J(u_jac), res_ev = r (slab vectors)."""
+    def update(self, u_jac, r, u_next=None):
+        """ref:krylow.py:55-73 with jac_ev = J(u_jac), res_ev = r (slab vectors).
+
+        Returns ||J(u_next) v_new|| (u_next defaults to u_jac), computed in the same
+        pass that normalises the new column (the next least-squares preconditioner)."""
         k = self.k
         if k == self.dev.slab.n_global:                       # :59-60
             raise GeneralizedKrylowSubspaceSpansEntireSpace
         if k >= self.kmax:
             raise RuntimeError("Krylov basis storage exhausted")
-        g = self.V[k]                                         # new column built in place
+        g = self._g
         self.be.vjp_gemv_t(u_jac, r, self.V, k, g, self._h)   # g = -J^T r ; h = V^T g (:62, :64)
         h = self.dev.comm.sum(self._h[:k])
         self._h[:k].copy_(self.be.to_device(h))
@@ -77,6 +82,9 @@ class DeviceKrylovBasis:
                 "Normal residual is allready inside generalized Krylow Subspcae, there for gauss newton "
                 "krylow algorithm has to proceed without enlarging the subspace.")
         nrm = math.sqrt(sumsq)                                # :71
-        self.be.vec_div(g, nrm, g, False)
         self.dev.comm.halo(g, self.dev.slab.N, self.dev.slab.nrows)
+        # V[k] = g / nrm on the whole slab (ghost rows divide the neighbours' g, so they
+        # equal the neighbours' V[k] rows bit for bit) + sum (J g)^2 on owned rows
+        self.be.normalize_jnorm(u_jac if u_next is None else u_next, g, nrm, self.V[k], self._jn2)
         self.k = k + 1
+        return math.sqrt(float(self.dev.comm.sum(self._jn2)[0])) / nrm

@@ -58,7 +58,9 @@ class CholQR2Solver:
         self.passes = 0
         self.solves = 0
         self.fallbacks = 0
-        self.R_prev = None          # R of the last solve (k_prev x k_prev)
+        self.history = []           # per solve: (k, passes, cond(R_Y) of each pass) -- diagnostics
+        self.R_prev = None          # R of the last solve (k_prev x k_prev); None after a restart
+        self.R_last = None          # R of the last solve (diagnostics)
         self.s_new = None           # ||J v_new|| of the column appended since then
 
     # -- basis events (the solver tells us how V changed since the last solve) -------
@@ -103,6 +105,8 @@ class CholQR2Solver:
         """Returns (d, jdd, R) for min ||-J(u) V d - r||."""
         k = basis.k
         self.solves += 1
+        p0 = self.passes
+        conds = []
         P = self._initial_preconditioner(k)
         if P is None:
             # classical CholQR2: first pass unpreconditioned (P = I, no r column)
@@ -123,7 +127,8 @@ class CholQR2Solver:
                 P = _chol_upper(Gp[:k, :k] + shift * np.eye(k)) @ P
                 self.fallbacks += 1
                 continue
-            if _cond_upper(Ry) <= COND_ACCEPT or it == MAX_PASSES - 1:
+            conds.append(_cond_upper(Ry))
+            if conds[-1] <= COND_ACCEPT or it == MAX_PASSES - 1:
                 z = scipy.linalg.solve_triangular(Ry, Gp[:k, k], trans="T", lower=False)
                 R = Ry @ P
                 break
@@ -134,6 +139,7 @@ class CholQR2Solver:
                 print("A is rank deficient")
         d = -scipy.linalg.solve_triangular(R, z, lower=False)
         jdd = float(np.sum((R @ d) ** 2))
-        self.R_prev = R
+        self.history.append((k, self.passes - p0, conds))
+        self.R_prev = self.R_last = R
         self.s_new = None
         return d, jdd, R

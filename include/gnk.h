@@ -91,6 +91,14 @@ int gnk_vec_stats(gnk_ctx* ctx, const double* x, double* stats_out);
  *                                               ref:krylow.py:37,71 */
 int gnk_vec_div(gnk_ctx* ctx, const double* src, double denom, double* dst, int full_slab);
 
+/* v = g / denom on the whole slab (g's ghost rows must already hold the
+ * neighbours' rows) and *jnorm2_out = sum over owned rows of (J(u) g)^2 in one
+ * pass: the new basis column of ref:krylow.py:71 plus ||J v_new||^2 * denom^2,
+ * the column scale of the next least-squares preconditioner.
+ * v != g. */
+int gnk_normalize_jnorm(gnk_ctx* ctx, const double* u, const double* g, double denom, double* v,
+                        double* jnorm2_out);
+
 /* out = x + (alpha * d) (two roundings, as NumPy's x + t * d) on owned rows or
  * the whole slab                                ref:gauss_newton.py:125,
  *                                               ref:armijo_goldstein.py:56 */

@@ -176,6 +176,13 @@ class NumpyBackend:
         sl = slice(None) if full_slab else slice(GHOST * self.N, (GHOST + self.nrows) * self.N)
         dst.numpy()[sl] = src.numpy()[sl] / denom
 
+    def normalize_jnorm(self, u, g, denom, v, jn2):
+        assert g.data_ptr() != v.data_ptr()
+        v.numpy()[:] = g.numpy() / denom
+        lo, hi = GHOST, GHOST + self.nrows
+        jg = self._jvp_block(self._diag(self._m(u)[lo:hi]), *self._nb(self._m(g), lo, hi))
+        jn2[0] = float(np.sum(jg * jg))
+
     def vec_axpy(self, x, alpha, d, out, full_slab):
         sl = slice(None) if full_slab else slice(GHOST * self.N, (GHOST + self.nrows) * self.N)
         out.numpy()[sl] = x.numpy()[sl] + alpha * d.numpy()[sl]

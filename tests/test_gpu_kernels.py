@@ -115,6 +115,25 @@ def test_basis_kernels(N, k):
     np.testing.assert_array_equal(own(dev, x), u + 0.25 * r)
 
 
+@pytest.mark.parametrize("N,lam", [(8, 10.0), (25, 10.0), (64, 0.0), (1024, 10.0), (1023, 10.0)])
+def test_normalize_jnorm(N, lam):
+    """v = g / denom bit for bit on the whole slab (ghost rows included) and
+    sum (J(u) g)^2 within reduction-order rounding (1e-12 relative)."""
+    prob, dev, ref = make(N, lam)
+    be = dev.backend
+    rng = np.random.default_rng(N)
+    u = 0.3 * rng.standard_normal(N * N)
+    g = dev.load(rng.standard_normal(N * N))
+    v = dev.vec()
+    jn2 = be.zeros(1)
+    be.normalize_jnorm(dev.load(u), g, 3.7, v, jn2)
+    np.testing.assert_array_equal(v.cpu().numpy(), g.cpu().numpy() / 3.7)
+    jg = ref.jvp(u, own(dev, g))
+    np.testing.assert_allclose(jn2.item(), np.sum(jg ** 2), rtol=1e-12)
+    with pytest.raises(RuntimeError, match="alias"):
+        be.normalize_jnorm(dev.load(u), g, 3.7, g, jn2)
+
+
 def test_cgs_max_propagates_nan():
     prob, dev, ref = make(24)
     be = dev.backend
@@ -131,8 +150,14 @@ def test_cgs_max_propagates_nan():
                                                   # marching kernel (N % 64 == 0): NB = 1 both passes, NB = 2 pass 1
                                                   (1024, 3, False, False), (1024, 12, True, True), (128, 15, False, True),
                                                   (1024, 25, False, False), (256, 31, False, False)])
-def test_gram_mfma(N, k, with_r, with_rinv):
-    """W = [J V | r] @ RinvAug on fp64 MFMA vs an fp64 NumPy Gram (host BLAS)."""
+@pytest.mark.parametrize("staged", ["default", "forced"])
+def test_gram_mfma(N, k, with_r, with_rinv, staged, monkeypatch):
+    """W = [J V | r] @ RinvAug on fp64 MFMA vs an fp64 NumPy Gram (host BLAS).  "forced" runs
+    the staged LDS-DMA kernel for every pass it supports (N % 128 == 0, K1 <= 32, k <= 24)."""
+    if staged == "forced":
+        if N % 128 or k > 24:
+            pytest.skip("staged kernel does not cover this shape")
+        monkeypatch.setenv("GNK_GRAM_STAGED", "2")
     prob, dev, ref = make(N)
     be = dev.backend
     rng = np.random.default_rng(N + k)
@@ -170,7 +195,9 @@ def test_gram_mfma(N, k, with_r, with_rinv):
     np.testing.assert_array_equal(Gdev, Gdev.T)
 
 
-def test_gram_deterministic():
+@pytest.mark.parametrize("staged", ["1", "2"])
+def test_gram_deterministic(staged, monkeypatch):
+    monkeypatch.setenv("GNK_GRAM_STAGED", staged)
     prob, dev, ref = make(512)
     be = dev.backend
     rng = np.random.default_rng(3)
@@ -181,12 +208,15 @@ def test_gram_deterministic():
     u = dev.load(0.1 * rng.standard_normal(512 * 512))
     r = dev.load(rng.standard_normal(512 * 512))
     outs = []
+    kp = be.gram_dim(k, True)
+    rinv = be.to_device(np.eye(kp).reshape(-1) * 0.5)
     for _ in range(3):
-        Gd = be.zeros(be.gram_dim(k, True) ** 2)
-        be.gram(u, V, k, None, r, Gd)
-        outs.append(Gd.cpu().numpy())
-    np.testing.assert_array_equal(outs[0], outs[1])
-    np.testing.assert_array_equal(outs[0], outs[2])
+        for ri in (None, rinv):
+            Gd = be.zeros(kp ** 2)
+            be.gram(u, V, k, ri, r, Gd)
+            outs.append(Gd.cpu().numpy())
+    for i in range(2, 6):
+        np.testing.assert_array_equal(outs[i % 2], outs[i])
 
 
 @pytest.mark.parametrize("N", [24, 101, 512])

@@ -1,6 +1,6 @@
 """Per-kernel microbenchmark on the 8192^2 slab (for rocprofv3 counter passes and A/B tests).
 
-python tools/kbench.py [--grid N] [--k K] [--reps R] [--kernels gram1,gram2,jvp,gemv,vjpg,cgs,resid,cg]
+python tools/kbench.py [--grid N] [--k K] [--reps R] [--kernels gram1,gram2,jvp,gemv,vjpg,norm,cgs,resid,cg]
 Prints one JSON line with the median ms and algorithmic GB/s per kernel.
 """
 import argparse
@@ -51,7 +51,8 @@ def main():
         "gram2": (lambda: be.gram(u, V, k, rinv_d, r, G), 8.0 * n * (k + 2)),
         "jvp": (lambda: be.jvp(u, r, t1), 24.0 * n),
         "gemv": (lambda: be.gemv(V, k, c, x), 8.0 * (sl.length * (k + 1))),
-        "vjpg": (lambda: be.vjp_gemv_t(u, r, V, k, V[k], h), 8.0 * n * (k + 3)),
+        "vjpg": (lambda: be.vjp_gemv_t(u, r, V, k, V[k], h), 8.0 * n * (k + 4)),
+        "norm": (lambda: be.normalize_jnorm(u, r, 3.0, t1, st), 24.0 * n),
         "cgs": (lambda: be.cgs_update(V, k, h, V[k], st), 8.0 * n * (k + 2)),
         "resid": (lambda: be.residual(x, y, t1, st), 24.0 * n),
         "cg": (lambda: be.cg_matvec(d, r, q, st), 24.0 * n),
