@@ -62,12 +62,19 @@ def bratu_inputs(N, seed=42):
     return prob, u_true, u0
 
 
-def step_bytes(n, k, a, passes=1.0):
-    """Algorithmic HBM bytes of one outer iteration as implemented:
-    `passes` preconditioned Gram passes (k + 2 vectors each), a trials x (GEMV k+1 +
-    residual 3), fused VJP + V^T g (k+3), CGS update (k+2), normalise (2),
-    ||J v_new|| (JVP 3 + norm 1)."""
-    return 8.0 * n * (passes * (k + 2) + 2 * k + 11 + a * (k + 4))
+def step_bytes(n, k, a, passes=1.0, fused=False):
+    """Algorithmic HBM bytes of one outer iteration as implemented, in units of
+    8 n bytes (one grid vector):
+      Gram passes            passes * (k + 2)      V, u, r
+      first trial, fused     (k + 1) + 2           V -> x, plus r read / g written  (res_old)
+      other trials           a' * (k + 1)          basis GEMV
+      residual per trial     a * 3                 x, y -> r
+      update products        k + 4 unless fused    u, r, V -> g, h
+      CGS update             k + 2                 V, g -> g
+      normalise + ||J v||    3                     g, u -> v"""
+    trials = a * 3 + (a - 1) * (k + 1) + ((k + 3) if fused else (k + 1))
+    update = (0 if fused else k + 4) + (k + 2) + 3
+    return 8.0 * n * (passes * (k + 2) + trials + update)
 
 
 def cpu_baseline(N, seconds, version, restart):
@@ -173,7 +180,9 @@ def main():
     tr = solver.trace[k_trace0:]
     passes = solver.lls.passes - passes0
     ppi = passes / max(len(tr), 1)
-    total_bytes = sum(step_bytes(n, s["k"], s["trials"], ppi) for s in tr)
+    fuse_ok = args.version == "res_old"
+    total_bytes = sum(step_bytes(n, s["k"], s["trials"], ppi, fused=fuse_ok and s["trials"] == 1 and s["k"] <= 24)
+                      for s in tr)
     # dominant kernel: Gram pass (per-launch events; bytes are this rank's slab)
     g_ms = [m for m, _ in launches]
     g_by = [b for _, b in launches]

@@ -41,6 +41,7 @@ SIGNATURES = {
     "gnk_cgs_update": (_c_int, [_c_vp, _c_vp, _c_i64, _c_int, _c_vp, _c_vp, _c_vp]),
     "gnk_vec_stats": (_c_int, [_c_vp, _c_vp, _c_vp]),
     "gnk_vec_div": (_c_int, [_c_vp, _c_vp, _c_dbl, _c_vp, _c_int]),
+    "gnk_basis_gemv_vjp_gemv_t": (_c_int, [_c_vp, _c_vp, _c_i64, _c_int, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp]),
     "gnk_normalize_jnorm": (_c_int, [_c_vp, _c_vp, _c_vp, _c_dbl, _c_vp, _c_vp]),
     "gnk_vec_axpy": (_c_int, [_c_vp, _c_vp, _c_dbl, _c_vp, _c_vp, _c_int]),
     "gnk_gram_padded_dim": (_c_int, [_c_int, _c_int]),
@@ -168,6 +169,9 @@ class HipBackend:
     def vjp_gemv_t(self, u, r, V, k, g, h):
         ldv = V.stride(0) if V is not None else 0
         self._call("gnk_vjp_gemv_t", _p(u), _p(r), _p(V), ldv, int(k), _p(g), _p(h))
+
+    def gemv_vjp_gemv_t(self, V, k, c, r, x, g, h):
+        self._call("gnk_basis_gemv_vjp_gemv_t", _p(V), V.stride(0), int(k), _p(c), _p(r), _p(x), _p(g), _p(h))
 
     def cgs_update(self, V, k, h, g, stats):
         self._call("gnk_cgs_update", _p(V), V.stride(0), int(k), _p(h), _p(g), _p(stats))

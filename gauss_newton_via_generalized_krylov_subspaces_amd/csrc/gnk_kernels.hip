@@ -356,6 +356,85 @@ __global__ __launch_bounds__(BLOCK) void k_vjp_gemv_t(const double* __restrict__
   block_sum_store<KCT>(acc, kc, partial + (size_t(blockIdx.z) * nblk + blockIdx.y * gridDim.x + blockIdx.x) * KCT, sh);
 }
 
+// Fused trial step + basis-update products (version res_old, first Armijo trial):
+//   x = V[:, :k] @ c on the whole slab (same arithmetic as k_gemv), and on owned rows
+//   g = -(J(x)^T r) (J at the trial point: only x_i enters the diagonal) and partial h = V^T g,
+// from ONE read of V (k_gemv + k_vjp_gemv_t read it twice and read u = x back).
+// One chunk of KCT >= k columns; surplus columns are clamped loads with c = 0 and discarded
+// partials (no loads under a branch).
+template <int VEC, int KCT>
+__global__ __launch_bounds__(BLOCK) void k_gemv_vjpg(const double* __restrict__ V, int64_t ldv, int k,
+                                                     const double* __restrict__ cvec, const double* __restrict__ r,
+                                                     double* __restrict__ x, double* __restrict__ g, Geo geo, Coef c,
+                                                     int64_t lr0, int64_t nlr, double* __restrict__ partial) {
+  __shared__ double sh[(BLOCK / 64) * KCT];
+  const int lane = threadIdx.x & 63;
+  const int jmax = k - 1;
+  double cj[KCT];
+#pragma unroll
+  for (int j = 0; j < KCT; ++j) cj[j] = j < k ? cvec[j] : 0.0;
+  double acc[KCT];
+#pragma unroll
+  for (int j = 0; j < KCT; ++j) acc[j] = 0.0;
+  ROW_LOOP_BEGIN(VEC)
+  const bool owned = lr >= G && lr < G + geo.nrows;       // block-uniform
+  if (VEC == 2 && iy + 1 < N) {
+    d2 vv[KCT];
+#pragma unroll
+    for (int j = 0; j < KCT; ++j) vv[j] = *reinterpret_cast<const d2*>(V + min(j, jmax) * ldv + li);
+    d2 xs = {0.0, 0.0};
+#pragma unroll
+    for (int j = 0; j < KCT; ++j) {
+      // the rounding of k_gemv: acc + v_j * c_j in column order (c_j = 0 past k adds a zero)
+      xs.x = xs.x + vv[j].x * cj[j];
+      xs.y = xs.y + vv[j].y * cj[j];
+    }
+    *reinterpret_cast<d2*>(x + li) = xs;
+    if (owned) {
+      const d2 rc = *reinterpret_cast<const d2*>(r + li);
+      const d2 rn = *reinterpret_cast<const d2*>(r + li - N);
+      const d2 rs = *reinterpret_cast<const d2*>(r + li + N);
+      const bool hw = iy > 0, he = iy + 2 < N;
+      double rw = __shfl_up(rc.y, 1);
+      double re = __shfl_down(rc.x, 1);
+      if (lane == 0) rw = hw ? r[li - 1] : 0.0;
+      if (lane == 63 || iy + 2 >= N) re = he ? r[li + 2] : 0.0;
+      const double g0 = -vjp_pt(c, jdiag(c, xs.x), rn.x, rw, hw, rc.x, rc.y, true, rs.x);
+      const double g1 = -vjp_pt(c, jdiag(c, xs.y), rn.y, rc.x, true, rc.y, re, he, rs.y);
+      *reinterpret_cast<d2*>(g + li) = d2{g0, g1};
+#pragma unroll
+      for (int j = 0; j < KCT; ++j) {
+        acc[j] = acc[j] + vv[j].x * g0;
+        acc[j] = acc[j] + vv[j].y * g1;
+      }
+    }
+  } else {
+    for (int q = 0; q < VEC; ++q) {
+      const int64_t i = li + q;
+      const int64_t yy = iy + q;
+      if (yy >= N) break;
+      double vv[KCT];
+      double xs = 0.0;
+#pragma unroll
+      for (int j = 0; j < KCT; ++j) {
+        vv[j] = V[min(j, jmax) * ldv + i];
+        xs = xs + vv[j] * cj[j];
+      }
+      x[i] = xs;
+      if (owned) {
+        const bool hw = yy > 0, he = yy < N - 1;
+        const double rw = hw ? r[i - 1] : 0.0, re = he ? r[i + 1] : 0.0;
+        const double gi = -vjp_pt(c, jdiag(c, xs), r[i - N], rw, hw, r[i], re, he, r[i + N]);
+        g[i] = gi;
+#pragma unroll
+        for (int j = 0; j < KCT; ++j) acc[j] = acc[j] + vv[j] * gi;
+      }
+    }
+  }
+  ROW_LOOP_END
+  block_sum_store<KCT>(acc, k, partial + size_t(blockIdx.y * gridDim.x + blockIdx.x) * KCT, sh);
+}
+
 // g -= V[:, :k] @ h ; partial {sum g^2, max|g|}
 template <int VEC>
 __global__ __launch_bounds__(BLOCK) void k_cgs(const double* __restrict__ V, int64_t ldv, int k,
@@ -1168,12 +1247,17 @@ __global__ __launch_bounds__(BLOCK) void k_gram_m(const double* __restrict__ u, 
 // (global_load_lds_dwordx4, no VGPR staging) two grid rows ahead into a 5-slot ring:
 //   slot(x) = x mod 5 holds row x of [V_0 .. V_{k-1}, u, (r)] (column stride GS_CS doubles) and a
 //   halo block (the strip's outer neighbours of every column).
-// Wave w owns points 16w .. 16w+15 of each step.  It builds its A fragments of W = [J V | r]
-// straight in the MFMA operand layout (lane: point l&15, column block l>>4) from five LDS reads
-// per value, transforms them on MFMA with the RinvAug B fragments held in VGPRs (W <- W P^-1),
-// and -- because the transform's C/D layout equals the Gram's A/B operand layout -- feeds the
-// transformed rows to the Gram MFMAs directly from registers.  No LDS tile round trip, no
-// producer/consumer hand-off: the barrier per step only retires the ring slots.
+// Wave w owns points 16w .. 16w+15 of each step.  It builds its A fragments of J V straight in
+// the MFMA operand layout (lane: point l&15, column block l>>4) from five LDS reads per value,
+// transforms them on MFMA with the RinvAug B fragments held in VGPRs (Y = J V P^-1), and --
+// because the transform's C/D layout equals the Gram's A/B operand layout -- feeds Y to the Gram
+// directly from registers.  Only the 16 x 16 tile of columns 0..15 runs on MFMA (f64 MFMA is no
+// faster than f64 VALU on MI355X and the two pipes run side by side):
+//   * columns 16..k-1 (k <= GS_KMAX): Y[p][t] is broadcast along its 16-lane row (DPP row_newbcast)
+//     and every lane accumulates Y[p][t] * Y[p][c] for its column c on VALU;
+//   * the r column (RinvAug is the identity there): Y[p][c] * r[p] and r[p]^2 on VALU.
+// Those per-lane sums (4 points per step, fixed order) are reduced over the lane groups, waves
+// and blocks in a fixed order, like the MFMA tile.
 // GS_CS = 144 == 16 (mod 32): the A-fragment reads of a half-wave (16 points x 2 columns) hit
 // 64 distinct banks.
 #ifndef GNK_SDBG
@@ -1183,6 +1267,8 @@ constexpr int GS_SW = 128;
 constexpr int GS_CS = 144;
 constexpr int GS_R = 5;
 constexpr int GS_NW = 8;
+constexpr int GS_KMAX = 20;     // V columns the staged kernel covers (k 21..24 would fit the LDS
+                                // ring but the two-block instance then spills past 256 VGPRs)
 
 typedef __attribute__((address_space(3))) void* lds_vp;
 typedef __attribute__((address_space(1))) const void* glb_cvp;
@@ -1190,12 +1276,27 @@ typedef __attribute__((address_space(1))) const void* glb_cvp;
 // s_waitcnt with vmcnt(n) and lgkmcnt(0), expcnt untouched (gfx9 encoding)
 constexpr unsigned waitcnt_vm_lgkm0(int n) { return unsigned((n & 0xF) | ((n >> 4) << 14) | (0x7 << 4)); }
 
+// lane j of each 16-lane row, broadcast to the row (DPP row_newbcast)
+template <int J>
+__device__ __forceinline__ double bcast_row(double v) {
+  const int2 b = __builtin_bit_cast(int2, v);
+  const int lo = __builtin_amdgcn_update_dpp(0, b.x, 0x150 + J, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, b.y, 0x150 + J, 0xF, 0xF, false);
+  return __builtin_bit_cast(double, int2{lo, hi});
+}
+
+// per-lane VALU Gram accumulators of the staged kernel: [tail t < 4 KSL][column block] (NB = 2),
+// then r . Y[:, block] per block, then r . r
+constexpr int gs_nacc(int nb, int ksl) { return nb == 1 ? 2 : 2 * 4 * ksl + 2 + 1; }
+
 template <int NB, int L, int KSL>
 __global__ __launch_bounds__(64 * GS_NW) void k_gram_s(const double* __restrict__ u, const double* __restrict__ V,
                                                        int64_t ldv, int k, const double* __restrict__ rinv,
-                                                       const double* __restrict__ r, Geo geo, Coef cf,
+                                                       int ldr, const double* __restrict__ r, Geo geo, Coef cf,
                                                        int64_t rpr, double* __restrict__ partial) {
-  constexpr int KP = 16 * NB, P = NB * (NB + 1) / 2;
+  constexpr int NACC = gs_nacc(NB, KSL);
+  constexpr int TMAX = NB == 2 ? 4 * KSL : 0;             // tail columns this instance covers
+  constexpr int ER = NB * TMAX, RR = ER + NB;             // accumulator slots of r . Y and r . r
   extern __shared__ __attribute__((aligned(16))) double lds[];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -1203,6 +1304,7 @@ __global__ __launch_bounds__(64 * GS_NW) void k_gram_s(const double* __restrict_
   const int nrow = k + 1 + (r ? 1 : 0);             // LDS rows per slot: V_0..V_{k-1}, u, (r)
   const int slotd = nrow * GS_CS + 128;             // + halo block: 64 lanes x 16 B
   const int ninst = nrow + 1;                       // DMA instructions per grid row (rows + halo)
+  const int tail = NB == 2 ? k - 16 : 0;            // columns 16..k-1 (VALU Gram)
 
   // block -> (row range, strip); consecutive range-major tiles share an XCD (blockIdx % 8),
   // so strip neighbours read each other's halo lines from the same L2
@@ -1213,7 +1315,7 @@ __global__ __launch_bounds__(64 * GS_NW) void k_gram_s(const double* __restrict_
   const int64_t x1 = min(geo.nrows, x0 + rpr);
   const int64_t col0 = int64_t(idx % nstrips) * GS_SW;
 
-  // KSL = 4-column k-steps of the last column block holding columns < K1 (compile time: the
+  // KSL = 4-column k-steps of the last column block holding V columns (compile time: the
   // transform below is straight-line, no guards)
   auto nks = [](int ab) constexpr { return ab == NB - 1 ? KSL : 4; };
   // RinvAug B fragments [cb][ab][ks] (ordinary loads, before any DMA is in flight)
@@ -1224,19 +1326,20 @@ __global__ __launch_bounds__(64 * GS_NW) void k_gram_s(const double* __restrict_
     for (int ab = 0; ab <= cb; ++ab)
 #pragma unroll
       for (int ks = 0; ks < nks(ab); ++ks) {
-        rB[cb][ab][ks] = rinv[(ab * 16 + ks * 4 + (lane >> 4)) * KP + cb * 16 + (lane & 15)];
+        rB[cb][ab][ks] = rinv[(ab * 16 + ks * 4 + (lane >> 4)) * ldr + cb * 16 + (lane & 15)];
         // opaque use: the load retires here, before the first DMA (a VGPR load still counted
         // when a DMA is in flight makes hipcc wait vmcnt(0) at its first use in the step loop)
         asm volatile("" : "+v"(rB[cb][ab][ks]));
       }
-  d4 acc[P];
+  d4 acc = d4{0.0, 0.0, 0.0, 0.0}, acc1 = acc;     // MFMA tile: columns 0..15 x 0..15 (2 chains)
+  double ev[NACC];                                  // VALU Gram accumulators (see gs_nacc)
 #pragma unroll
-  for (int q = 0; q < P; ++q) acc[q] = d4{0.0, 0.0, 0.0, 0.0};
+  for (int q = 0; q < NACC; ++q) ev[q] = 0.0;
 
   // This wave's DMA instructions q = wave + 8m (a q past the end re-loads the u row: same bytes,
-  // same place).  Per instruction: a wave-uniform source base (row 0 of the column at the strip),
-  // a per-lane offset and the LDS offset inside a slot -- all fixed; a step only adds the row.
-  const double* dsrc[L];                            // per lane: row 0 of the source at the strip
+  // same place): a per-lane source at row 0 and the LDS offset inside a slot are fixed; a step
+  // only adds the row offset.
+  const double* dsrc[L];
   int ddst[L];
 #pragma unroll
   for (int m = 0; m < L; ++m) {
@@ -1268,44 +1371,83 @@ __global__ __launch_bounds__(64 * GS_NW) void k_gram_s(const double* __restrict_
   const double cem = (col0 + e + 1 < N) ? cf.hm2 : 0.0;
   const double up = -cf.j_lin_up;
   int fo[NB][4], fw[NB][4], fe[NB][4];
-  unsigned fv = 0, fr = 0;                          // per fragment bit: V column / r column
+  unsigned fv = 0;                                  // per fragment bit: a V column (else padding)
 #pragma unroll
   for (int ab = 0; ab < NB; ++ab)
 #pragma unroll
     for (int ks = 0; ks < 4; ++ks) {
       const int j = ab * 16 + ks * 4 + cq;
-      const bool isV = j < k, isR = (r != nullptr) && j == k;
-      const int jr = isV ? j : (isR ? k + 1 : 0);
+      const bool isV = j < k;
+      const int jr = isV ? j : 0;
       fo[ab][ks] = jr * GS_CS + e;
       fw[ab][ks] = e > 0 ? jr * GS_CS + e - 1 : nrow * GS_CS + 4 * jr + 1;             // halo: element -1
       fe[ab][ks] = e < GS_SW - 1 ? jr * GS_CS + e + 1 : nrow * GS_CS + 4 * jr + 2;     // halo: element 128
       fv |= unsigned(isV) << (ab * 4 + ks);
-      fr |= unsigned(isR) << (ab * 4 + ks);
     }
   const int ou = k * GS_CS + e;
+  const int orr = (k + 1) * GS_CS + wave * 16 + cq;  // r at point 16w + (l>>4) (+ 4i)
 
   // Software pipeline inside the wave (2 waves/SIMD cannot hide the latency chains):
   //   step x: A fragments of row x (LDS reads, FMAs) with dn(x) computed during step x-1;
   //           dn(x+1) = -jdiag(u(x+1)) (the exp chain runs under the MFMAs);
-  //           transform(x) interleaved with the independent Gram MFMAs of row x-1.
+  //           transform(x) interleaved with the Gram (MFMA tile + VALU tail / r) of row x-1.
   double a[NB][4];
   d4 qp[NB];                                        // transformed rows of the previous step
+  // two independent accumulation chains per block (f64 MFMA chains stall on the RAW dependency)
   auto transform = [&](d4 (&qv)[NB]) {
 #pragma unroll
     for (int cb = 0; cb < NB; ++cb) {
-      qv[cb] = d4{0.0, 0.0, 0.0, 0.0};
+      d4 h0 = d4{0.0, 0.0, 0.0, 0.0}, h1 = d4{0.0, 0.0, 0.0, 0.0};
+      int n = 0;
 #pragma unroll
       for (int ab = 0; ab <= cb; ++ab)
 #pragma unroll
-        for (int ks = 0; ks < nks(ab); ++ks) qv[cb] = mfma64(a[ab][ks], rB[cb][ab][ks], qv[cb]);
+        for (int ks = 0; ks < nks(ab); ++ks, ++n) {
+          if (n & 1) h1 = mfma64(a[ab][ks], rB[cb][ab][ks], h1);
+          else h0 = mfma64(a[ab][ks], rB[cb][ab][ks], h0);
+        }
+      qv[cb] = h0 + h1;
     }
   };
-  // qv[cb][i] = Y[16w + (l>>4) + 4i][16cb + (l&15)] == the Gram operand of rows 4i..4i+3
-  auto gram = [&](const d4 (&qv)[NB]) {
+  // qv[cb][i] = Y[16w + (l>>4) + 4i][16cb + (l&15)]: the MFMA operand of rows 4i..4i+3, and for
+  // the VALU part this lane's column c = 16cb + (l&15) at point p = 16w + (l>>4) + 4i
+  auto gram = [&](const d4 (&qv)[NB], const double* Lr) {
+    acc = mfma64(qv[0][0], qv[0][0], acc);
+    acc1 = mfma64(qv[0][1], qv[0][1], acc1);
+    acc = mfma64(qv[0][2], qv[0][2], acc);
+    acc1 = mfma64(qv[0][3], qv[0][3], acc1);
+    if (NB == 2) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+      for (int t = 0; t < TMAX; ++t) {
+        if (t < tail) {                              // wave-uniform, registers only
 #pragma unroll
-      for (int q = 0; q < P; ++q) acc[q] = mfma64(qv[pair_a(q, NB)][i], qv[pair_b(q, NB)][i], acc[q]);
+          for (int i = 0; i < 4; ++i) {
+            double yt;
+            switch (t) {
+              case 0: yt = bcast_row<0>(qv[NB - 1][i]); break;
+              case 1: yt = bcast_row<1>(qv[NB - 1][i]); break;
+              case 2: yt = bcast_row<2>(qv[NB - 1][i]); break;
+              case 3: yt = bcast_row<3>(qv[NB - 1][i]); break;
+              case 4: yt = bcast_row<4>(qv[NB - 1][i]); break;
+              case 5: yt = bcast_row<5>(qv[NB - 1][i]); break;
+              case 6: yt = bcast_row<6>(qv[NB - 1][i]); break;
+              default: yt = bcast_row<7>(qv[NB - 1][i]); break;
+            }
+#pragma unroll
+            for (int cb = 0; cb < NB; ++cb) ev[t * NB + cb] = fma(yt, qv[cb][i], ev[t * NB + cb]);
+          }
+        }
+      }
+    }
+    if (r) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const double rv = Lr[orr + 4 * i];
+#pragma unroll
+        for (int cb = 0; cb < NB; ++cb) ev[ER + cb] = fma(rv, qv[cb][i], ev[ER + cb]);
+        ev[RR] = fma(rv, rv, ev[RR]);
+      }
+    }
   };
   if (x0 < x1) {
     // ring slots rotate: sn/sc/ss = rows x-1, x, x+1; sd = row x+3 (the slot of row x-2)
@@ -1318,8 +1460,11 @@ __global__ __launch_bounds__(64 * GS_NW) void k_gram_s(const double* __restrict_
     __builtin_amdgcn_s_waitcnt(waitcnt_vm_lgkm0(L));    // rows x0-1 .. x0+1 landed
     __builtin_amdgcn_s_barrier();
     double dn = -jdiag(cf, lds[sc * slotd + ou]);
-    // fragments of row x from the ring (slots n/c/s) with dn(x); then dn(x+1) from slot s
-    auto fragments = [&](const double* Ln, const double* Lc, const double* Ls) {
+    for (int64_t x = x0; x < x1; ++x) {
+      if (!(GNK_SDBG & 1)) issue_row(x + 3, sd);
+      const double* Ln = lds + sn * slotd;
+      const double* Lc = lds + sc * slotd;
+      const double* Ls = lds + ss * slotd;
 #pragma unroll
       for (int ab = 0; ab < NB; ++ab)
 #pragma unroll
@@ -1327,40 +1472,38 @@ __global__ __launch_bounds__(64 * GS_NW) void k_gram_s(const double* __restrict_
           if (GNK_SDBG & 2) { a[ab][ks] = dn; continue; }
           const int o = fo[ab][ks];
           const double vn = Ln[o], vw = Lc[fw[ab][ks]], vc = Lc[o], ve = Lc[fe[ab][ks]], vs = Ls[o];
-          const bool isV = (fv >> (ab * 4 + ks)) & 1, isR = (fr >> (ab * 4 + ks)) & 1;
-          // J V with explicit FMAs in CSR term order (as k_gram_w); the r column is
-          // 0*n + 0*w + 1*c + 0*e + 0*s == r exactly, padding columns are 0
-          const double cn = isV ? cf.hm2 : 0.0, cw = isV ? cwm : 0.0;
-          const double cc = isV ? dn : (isR ? 1.0 : 0.0);
-          const double ce = isV ? cem : 0.0, cs = isV ? up : 0.0;
-          double sv = cn * vn;
-          sv = fma(cw, vw, sv);
-          sv = fma(cc, vc, sv);
-          sv = fma(ce, ve, sv);
-          sv = fma(cs, vs, sv);
+          // J V with explicit FMAs in CSR term order (as k_gram_w).  Only the last fragment can hold
+          // columns >= k (padding, coefficients 0): every earlier one is all V columns.
+          double sv;
+          if (ab == NB - 1 && ks == nks(ab) - 1) {
+            const bool isV = (fv >> (ab * 4 + ks)) & 1;
+            const double cn = isV ? cf.hm2 : 0.0, cw = isV ? cwm : 0.0, cc = isV ? dn : 0.0;
+            const double ce = isV ? cem : 0.0, cs = isV ? up : 0.0;
+            sv = cn * vn;
+            sv = fma(cw, vw, sv);
+            sv = fma(cc, vc, sv);
+            sv = fma(ce, ve, sv);
+            sv = fma(cs, vs, sv);
+          } else {
+            sv = cf.hm2 * vn;
+            sv = fma(cwm, vw, sv);
+            sv = fma(dn, vc, sv);
+            sv = fma(cem, ve, sv);
+            sv = fma(up, vs, sv);
+          }
           a[ab][ks] = sv;
         }
-      dn = -jdiag(cf, Ls[ou]);
-    };
-    // transform of the current fragments, interleaved with the Gram of the previous rows
-    auto mfmas = [&](bool with_prev) {
+      dn = -jdiag(cf, Ls[ou]);                        // row x+1 (its u is in the ring)
       d4 qv[NB];
       if (GNK_SDBG & 4) {
 #pragma unroll
         for (int cb = 0; cb < NB; ++cb) qv[cb] = d4{a[0][0], a[0][0], a[0][0], a[0][0]};
       } else {
         transform(qv);
-        if (with_prev) gram(qp);
+        if (x > x0) gram(qp, Ln);                     // rows of x-1: r is in slot n
       }
 #pragma unroll
       for (int cb = 0; cb < NB; ++cb) qp[cb] = qv[cb];
-    };
-    // (A stagger -- waves 4-7 running MFMAs(x-1) before fragments(x) beside waves 0-3 -- measured
-    // 10-50 % slower on MI355X than this in-wave pipeline; not used.)
-    for (int64_t x = x0; x < x1; ++x) {
-      if (!(GNK_SDBG & 1)) issue_row(x + 3, sd);
-      fragments(lds + sn * slotd, lds + sc * slotd, lds + ss * slotd);
-      mfmas(x > x0);
       const int t = sn;
       sn = sc;
       sc = ss;
@@ -1370,27 +1513,74 @@ __global__ __launch_bounds__(64 * GS_NW) void k_gram_s(const double* __restrict_
       __builtin_amdgcn_s_waitcnt(waitcnt_vm_lgkm0(L));  // row x+2 landed; only row x+3 in flight
       __builtin_amdgcn_s_barrier();
     }
-    if (!(GNK_SDBG & 4)) gram(qp);
+    if (!(GNK_SDBG & 4)) gram(qp, lds + sn * slotd);  // last row x1-1 (its slot is now sn)
   }
   __builtin_amdgcn_s_waitcnt(waitcnt_vm_lgkm0(0));
   __builtin_amdgcn_s_barrier();
 
-  // block partial = ((w0 + w1) + w2) + ... through LDS, layout [block][pair][lane*4 + i]
+  acc = acc + acc1;
+  // block partial = ((w0 + w1) + w2) + ... through LDS:
+  //   [0, 256): MFMA tile (lane*4 + i), [256, 256 + 64 NACC): VALU sums (lane * NACC + q)
+  constexpr int PL = 256 + 64 * NACC;
   double* red = lds;
   for (int w = 0; w < GS_NW; ++w) {
     if (wave == w) {
 #pragma unroll
-      for (int q = 0; q < P; ++q)
+      for (int ii = 0; ii < 4; ++ii) {
+        double* dst = red + lane * 4 + ii;
+        *dst = (w == 0) ? acc[ii] : *dst + acc[ii];
+      }
 #pragma unroll
-        for (int ii = 0; ii < 4; ++ii) {
-          double* dst = red + q * 256 + lane * 4 + ii;
-          *dst = (w == 0) ? acc[q][ii] : *dst + acc[q][ii];
-        }
+      for (int q = 0; q < NACC; ++q) {
+        double* dst = red + 256 + lane * NACC + q;
+        *dst = (w == 0) ? ev[q] : *dst + ev[q];
+      }
     }
     __syncthreads();
   }
-  double* out = partial + size_t(blockIdx.x) * size_t(P) * 256;
-  for (int t = tid; t < P * 256; t += blockDim.x) out[t] = red[t];
+  double* out = partial + size_t(blockIdx.x) * PL;
+  for (int t = tid; t < PL; t += blockDim.x) out[t] = red[t];
+}
+
+// staged-kernel scatter: red = block-summed partials [256 MFMA tile | 64 lanes x NACC]
+//   G[c][c'] (c, c' < 16) from the MFMA tile, G[16 + t][c] from the tail sums, G[k][c], G[k][k]
+//   from the r sums; lane groups g = l >> 4 (points) summed in order 0..3.
+__global__ __launch_bounds__(BLOCK) void k_gram_scatter_s(const double* __restrict__ red, int nb, int nacc, int k,
+                                                          int has_r, int KP, double* __restrict__ Gout) {
+  const int tail = nb == 2 ? k - 16 : 0;
+  const int er = nb == 1 ? 0 : nacc - 3, rr = er + nb;
+  const double* ev = red + 256;
+  auto lsum = [&](int col_in_block, int q) {
+    double s = 0.0;
+    for (int g = 0; g < 4; ++g) s += ev[(16 * g + col_in_block) * nacc + q];
+    return s;
+  };
+  for (int idx = blockIdx.x * BLOCK + threadIdx.x; idx < 256 + 24 * 33 + 33; idx += gridDim.x * BLOCK) {
+    if (idx < 256) {
+      const int lane = idx >> 2, i = idx & 3;
+      const int row = (lane >> 4) + 4 * i, col = lane & 15;
+      if (row < k && col < k && row <= col) {
+        Gout[row * KP + col] = red[idx];
+        Gout[col * KP + row] = red[idx];
+      }
+    } else if (idx < 256 + 24 * 33) {
+      const int t = (idx - 256) / 33, c = (idx - 256) % 33;   // row 16 + t, column c <= 16 + t
+      if (t < tail && c <= 16 + t) {
+        const double v = lsum(c & 15, t * nb + (c >> 4));
+        Gout[(16 + t) * KP + c] = v;
+        Gout[c * KP + 16 + t] = v;
+      }
+    } else if (has_r) {
+      const int c = idx - 256 - 24 * 33;
+      if (c < k) {
+        const double v = lsum(c & 15, er + (c >> 4));
+        Gout[k * KP + c] = v;
+        Gout[c * KP + k] = v;
+      } else if (c == k) {
+        Gout[k * KP + k] = lsum(0, rr);
+      }
+    }
+  }
 }
 
 // Sum Gram partials over blocks (block order) and scatter into G[KP][KP] (symmetric).
@@ -1755,6 +1945,40 @@ int gnk_vjp_gemv_t(gnk_ctx* ctx, const double* u, const double* r, const double*
   return wreduce(ctx, ctx->scratch, nblk, k, kct, kct, int64_t(nblk) * kct, nullptr, h_out);
 }
 
+int gnk_basis_gemv_vjp_gemv_t(gnk_ctx* ctx, const double* V, int64_t ldv, int k, const double* c, const double* r,
+                              double* x, double* g, double* h_out) {
+  if (!ready(ctx)) return -1;
+  if (k < 1 || k > 24) return fail(ctx, "basis_gemv_vjp_gemv_t: k must be in [1, 24]");
+  if (!V || !c || !r || !x || !g || !h_out) return fail(ctx, "basis_gemv_vjp_gemv_t: NULL argument");
+  if (vec_of(ctx) == 2 && (ldv % 2 != 0)) return fail(ctx, "basis_gemv_vjp_gemv_t: ldv must be even");
+  const int kct = std::max(4, (k + 3) / 4 * 4);
+  RowLaunch L = rows(ctx, 0, ctx->geo.nrows + 2 * G, vec_of(ctx), 2048);
+  const int nblk = L.grid.x * L.grid.y;
+  if (size_t(nblk) * kct > SCRATCH_DOUBLES) return fail(ctx, "basis_gemv_vjp_gemv_t: scratch too small");
+#define GVJ_LAUNCH(V_, K_)                                                                                    \
+  hipLaunchKernelGGL((k_gemv_vjpg<V_, K_>), L.grid, dim3(BLOCK), 0, ctx->stream, V, ldv, k, c, r, x, g, ctx->geo, \
+                     ctx->coef, L.lr0, L.nlr, ctx->scratch)
+#define GVJ_SWITCH(V_)                  \
+  switch (kct) {                        \
+    case 4: GVJ_LAUNCH(V_, 4); break;   \
+    case 8: GVJ_LAUNCH(V_, 8); break;   \
+    case 12: GVJ_LAUNCH(V_, 12); break; \
+    case 16: GVJ_LAUNCH(V_, 16); break; \
+    case 20: GVJ_LAUNCH(V_, 20); break; \
+    default: GVJ_LAUNCH(V_, 24); break; \
+  }
+  if (vec_of(ctx) == 2) {
+    GVJ_SWITCH(2)
+  } else {
+    GVJ_SWITCH(1)
+  }
+#undef GVJ_SWITCH
+#undef GVJ_LAUNCH
+  int rc = check_launch(ctx, "basis_gemv_vjp_gemv_t");
+  if (rc) return rc;
+  return wreduce(ctx, ctx->scratch, nblk, k, kct, kct, int64_t(nblk) * kct, nullptr, h_out);
+}
+
 int gnk_cgs_update(gnk_ctx* ctx, const double* V, int64_t ldv, int k, const double* h, double* g,
                    double* stats_out) {
   if (!ready(ctx)) return -1;
@@ -1817,28 +2041,23 @@ int gnk_gram(gnk_ctx* ctx, const double* u, const double* V, int64_t ldv, int k,
   if (rinv && ldr != KP) return fail(ctx, "gram: rinv must be the kp x kp augmented inverse (ldr == kp)");
   const int nb = KP / 16;
   const int P = nb * (nb + 1) / 2;
-  // partials [block][P * 256] -> red[P * 256] (scratch tail) -> symmetric G
-  auto finish = [&](int nblocks) -> int {
-    (void)hipMemsetAsync(G_out, 0, size_t(KP) * KP * sizeof(double), ctx->stream);
-    double* red = ctx->scratch + (SCRATCH_DOUBLES - size_t(P) * 256);
-    int rc = wreduce(ctx, ctx->scratch, nblocks, P * 256, int64_t(P) * 256, P * 256, 0, nullptr, red);
-    if (rc) return rc;
-    hipLaunchKernelGGL(k_gram_scatter, dim3((P * 256 + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, ctx->stream, red, P, KP,
-                       G_out);
-    return check_launch(ctx, "gram scatter");
-  };
+  // staged kernel (measured faster than the chunked / marching kernels for the preconditioned
+  // pass from k = 4 up; the marching kernel stays faster for the plain pass);
+  // GNK_GRAM_STAGED=2 forces it for every pass (tests), 0 disables it
   const char* staged_s = getenv("GNK_GRAM_STAGED");        // read per call: tests force the kernel
   const int staged_env = staged_s ? atoi(staged_s) : 1;
-  // staged kernel for the preconditioned pass (measured: faster than the chunked / marching
-  // kernels from k = 4 up; the marching kernel stays faster for the plain pass);
-  // GNK_GRAM_STAGED=2 forces it for every pass (tests), 0 disables it
-  if (staged_env && (staged_env == 2 || (rinv && k >= 4)) && nb <= 2 && ctx->geo.N % GS_SW == 0 &&
+  if (staged_env && (staged_env == 2 || (rinv && k >= 4)) && k <= GS_KMAX && ctx->geo.N % GS_SW == 0 &&
       !getenv("GNK_DEBUG_GRAM")) {
+    const int nbs = k <= 16 ? 1 : 2;                        // MFMA transform blocks of the V columns
     const int nrow = k + 1 + (r ? 1 : 0);
     const int L = (nrow + 1 + GS_NW - 1) / GS_NW;
     const size_t lds = size_t(GS_R) * (size_t(nrow) * GS_CS + 128) * sizeof(double);
     if (L <= 4 && lds <= 160 * 1024) {
-      const double* rv = rinv ? rinv : ctx->ident + (nb == 1 ? 0 : 256);
+      const double* rv = rinv ? rinv : ctx->ident + (KP == 16 ? 0 : 256);
+      // 4-column k-steps of the last transform block
+      const int ksl = ((k - 16 * (nbs - 1)) + 3) / 4;
+      const int nacc = gs_nacc(nbs, ksl);
+      const int PL = 256 + 64 * nacc;
       const int wgpc = std::max(1, std::min(2, int((160 * 1024) / lds)));
       const int64_t nstrips = ctx->geo.N / GS_SW;
       const int64_t nrows = ctx->geo.nrows;
@@ -1846,31 +2065,35 @@ int gnk_gram(gnk_ctx* ctx, const double* u, const double* V, int64_t ldv, int k,
       const int64_t rpr = (nrows + nranges - 1) / nranges;
       nranges = (nrows + rpr - 1) / rpr;
       const int64_t nwg = nstrips * nranges;
-      if (nwg > (1 << 20) || size_t(nwg) * P * 256 > SCRATCH_DOUBLES - size_t(P) * 256)
+      if (nwg > (1 << 20) || size_t(nwg) * PL > SCRATCH_DOUBLES - size_t(PL))
         return fail(ctx, "gram: scratch too small (staged)");
       const int64_t nown = nrows * ctx->geo.N;
       TimedLaunch tls(ctx, GNK_TIMER_GRAM, 8.0 * double(nown) * double(k + 1 + (r ? 1 : 0)));
 #define GRAMS(NBV, LV, KV)                                                                                    \
   hipLaunchKernelGGL((k_gram_s<NBV, LV, KV>), dim3(unsigned(nwg)), dim3(64 * GS_NW), lds, ctx->stream, u, V, ldv, k, \
-                     rv, r, ctx->geo, ctx->coef, rpr, ctx->scratch)
+                     rv, KP, r, ctx->geo, ctx->coef, rpr, ctx->scratch)
 #define GRAMS_K(NBV, LV)                                                    \
   do {                                                                      \
     if (ksl == 1) GRAMS(NBV, LV, 1); else if (ksl == 2) GRAMS(NBV, LV, 2);  \
     else if (ksl == 3) GRAMS(NBV, LV, 3); else GRAMS(NBV, LV, 4);           \
   } while (0)
-      // 4-column k-steps of the last column block that hold columns < K1
-      const int ksl = ((k + (r ? 1 : 0) - 16 * (nb - 1)) + 3) / 4;
-      if (nb == 1) {
+      if (nbs == 1) {
         if (L == 1) GRAMS_K(1, 1); else if (L == 2) GRAMS_K(1, 2); else if (L == 3) GRAMS_K(1, 3); else GRAMS_K(1, 4);
       } else {
-        if (L == 1) GRAMS_K(2, 1); else if (L == 2) GRAMS_K(2, 2); else if (L == 3) GRAMS_K(2, 3); else GRAMS_K(2, 4);
+        if (L == 3) GRAMS(2, 3, 1); else GRAMS(2, 4, 1);     // k <= 20: one tail k-step
       }
 #undef GRAMS_K
 #undef GRAMS
       tls.done();
-      const int rcs = check_launch(ctx, "gram_s");
+      int rcs = check_launch(ctx, "gram_s");
       if (rcs) return rcs;
-      return finish(int(nwg));
+      (void)hipMemsetAsync(G_out, 0, size_t(KP) * KP * sizeof(double), ctx->stream);
+      double* red = ctx->scratch + (SCRATCH_DOUBLES - size_t(PL));
+      rcs = wreduce(ctx, ctx->scratch, int(nwg), PL, int64_t(PL), PL, 0, nullptr, red);
+      if (rcs) return rcs;
+      hipLaunchKernelGGL(k_gram_scatter_s, dim3(4), dim3(BLOCK), 0, ctx->stream, red, nbs, nacc, k, r ? 1 : 0, KP,
+                         G_out);
+      return check_launch(ctx, "gram scatter (staged)");
     }
   }
   if (KP <= 64) {

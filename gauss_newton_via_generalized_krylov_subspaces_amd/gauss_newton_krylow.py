@@ -11,6 +11,7 @@ every exception -- and runs each n-sized operation on the GPU:
       only when the preconditioned factor is not well conditioned) -> LS solve (lls.py)
     a x [basis GEMV + fused residual/||r||^2]   -> Armijo trials
     fused -J^T r + V^T g, CGS update + stats, halo, normalise + ||J v_new|| -> basis update
+    (res_old: the first trial's GEMV also yields -J(x)^T r_old and V^T g, from one read of V)
 
 Host <-> device traffic per iteration is O(k^2) doubles (Gram matrices, k
 coefficients, a few scalars).  ``GNKSolver`` exposes the same loop one outer
@@ -126,13 +127,21 @@ class GNKSolver:
         rti = 1 - self.ri
         x_t, r_t = self.xb[xi], self.rb[rti]
         last = {}
+        # res_old: the update after an accepted first trial is g = -J(x_t)^T r_old, h = V^T g --
+        # computed from the same read of V as the trial point itself (speculative; a rejected
+        # first trial falls back to the separate update products)
+        fuse = self.version == "res_old" and 1 <= basis.k <= basis.FUSE_KMAX
 
         def trial(t):
-            basis.x(self.c + t * d, x_t)                                  # res_krylow(x + t d)
+            if fuse and not last:
+                basis.x_with_update_products(self.c + t * d, r_old, x_t)  # res_krylow(x + t d)
+            else:
+                basis.x(self.c + t * d, x_t)
             last["rr"] = self._residual(x_t, r_t)
             return last["rr"]
 
         t, ntrial = armijo_device(trial, self.rr, jdd, d)                 # :91-93
+        products_ready = fuse and ntrial == 1
         self.nfev += ntrial                                               # :94
         s = np.sum(self.c ** 2)                                           # :96
         self.c += t * d                                                   # :98
@@ -149,7 +158,7 @@ class GNKSolver:
         u_new = self.xb[self.uJ]      # the next LS solve's J; s = ||J(u_new) v_new|| (lls.py)
         try:
             if self.version == "res_old":
-                s_new = basis.update(u_new, r_old, u_new)
+                s_new = basis.update(u_new, r_old, u_new, products_ready=products_ready)
             elif self.version == "res_new":
                 s_new = basis.update(u_new, r_t, u_new)
             elif self.version == "jac_old_res_old":

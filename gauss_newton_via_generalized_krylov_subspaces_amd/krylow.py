@@ -61,18 +61,32 @@ class DeviceKrylovBasis:
         self.be.gemv(self.V, k, self._c, out)
         return out
 
-    def update(self, u_jac, r, u_next=None):
+    FUSE_KMAX = 24
+
+    def x_with_update_products(self, c: np.ndarray, r, out):
+        """out = V @ c, and -- from the same read of V -- the products of a basis update at
+        u = out with residual r: g = -J(out)^T r, h = V^T g (this rank's rows).  ``update(...,
+        products_ready=True)`` then continues from them.  Used for the first Armijo trial of
+        version "res_old" (the update after acceptance is exactly this product)."""
+        k = len(c)
+        self._c[:k].copy_(self.be.to_device(c))
+        self.be.gemv_vjp_gemv_t(self.V, k, self._c, r, out, self._g, self._h)
+        return out
+
+    def update(self, u_jac, r, u_next=None, products_ready=False):
         """ref:krylow.py:55-73 with jac_ev = J(u_jac), res_ev = r (slab vectors).
 
         Returns ||J(u_next) v_new|| (u_next defaults to u_jac), computed in the same
-        pass that normalises the new column (the next least-squares preconditioner)."""
+        pass that normalises the new column (the next least-squares preconditioner).
+        ``products_ready``: g and h were produced by ``x_with_update_products`` at u_jac."""
         k = self.k
         if k == self.dev.slab.n_global:                       # :59-60
             raise GeneralizedKrylowSubspaceSpansEntireSpace
         if k >= self.kmax:
             raise RuntimeError("Krylov basis storage exhausted")
         g = self._g
-        self.be.vjp_gemv_t(u_jac, r, self.V, k, g, self._h)   # g = -J^T r ; h = V^T g (:62, :64)
+        if not products_ready:
+            self.be.vjp_gemv_t(u_jac, r, self.V, k, g, self._h)   # g = -J^T r ; h = V^T g (:62, :64)
         h = self.dev.comm.sum(self._h[:k])
         self._h[:k].copy_(self.be.to_device(h))
         self.be.cgs_update(self.V, k, self._h, g, self._stats)   # g -= V h (:64)

@@ -81,6 +81,13 @@ int gnk_basis_gemv(gnk_ctx* ctx, const double* V, int64_t ldv, int k,
  *                                               ref:krylow.py:62,64 */
 int gnk_vjp_gemv_t(gnk_ctx* ctx, const double* u, const double* r,
                    const double* V, int64_t ldv, int k, double* g, double* h_out);
+/* Fused first Armijo trial + basis-update products (version "res_old"): x = V[:, :k] @ c on
+ * the whole slab (rounding of gnk_basis_gemv), then on owned rows g = -(J(x)^T r) and
+ * h = V[:, :k]^T g -- gnk_basis_gemv followed by gnk_vjp_gemv_t(u = x) from one read of V.
+ * 1 <= k <= 24.                      ref:krylow.py:42, :62, :64 + gauss_newton_krylow.py:91,115 */
+int gnk_basis_gemv_vjp_gemv_t(gnk_ctx* ctx, const double* V, int64_t ldv, int k, const double* c, const double* r,
+                              double* x, double* g, double* h_out);
+
 /* g -= V[:, :k] @ h on owned rows; stats_out = {sum g**2, max|g|}
  *                                               ref:krylow.py:64,66,71 */
 int gnk_cgs_update(gnk_ctx* ctx, const double* V, int64_t ldv, int k,

@@ -150,6 +150,10 @@ class NumpyBackend:
         Vn = V.numpy()[:k]
         x.numpy()[:] = np.asarray(c.numpy()[:k]) @ Vn
 
+    def gemv_vjp_gemv_t(self, V, k, c, r, x, g, h):
+        self.gemv(V, k, c, x)
+        self.vjp_gemv_t(x, r, V, k, g, h)
+
     def vjp_gemv_t(self, u, r, V, k, g, h):
         lo, hi = GHOST, GHOST + self.nrows
         G = self._m(g)
