@@ -107,7 +107,8 @@ class GNKSolver:
         self.done = False
         self.uJ = 0                                        # J is evaluated at x0 (:78)
         self.xb[0].copy_(self.dev.load(x0))
-        self.c = self.basis.start(self.xb[0])              # :71
+        self.c, s0 = self.basis.start(self.xb[0], self.xb[self.uJ])   # :71 (+ ||J(x0) v_0||)
+        self.lls.on_restart(s0)
         xi = self._free_x(self.uJ)
         self.basis.x(self.c, self.xb[xi])
         self.ri = 0
@@ -180,8 +181,8 @@ class GNKSolver:
         if it % self.restart == 0:                                        # :135-136
             xr = self._free_x(self.uJ)
             basis.x(self.c, self.xb[xr])
-            self.c = basis.start(self.xb[xr])
-            self.lls.on_restart()
+            self.c, s0 = basis.start(self.xb[xr], self.xb[self.uJ])
+            self.lls.on_restart(s0)
         if it >= self.max_iter - 1:
             self.done = True
         return self.done

@@ -43,16 +43,22 @@ class DeviceKrylovBasis:
         """(n, k) like ``basis.shape`` in the reference (n = global unknowns)."""
         return (self.dev.slab.n_global, self.k)
 
-    def start(self, x) -> np.ndarray:
-        """ref:krylow.py:30-39.  ``x`` is a slab vector valid on owned +-GHOST rows."""
+    def start(self, x, u_jac=None):
+        """ref:krylow.py:30-39.  ``x`` is a slab vector valid on owned +-GHOST rows.
+
+        Returns the coordinates [||x||]; with ``u_jac`` also ||J(u_jac) v_0|| (the first
+        least-squares preconditioner), from the same pass that normalises x."""
         self.be.vec_stats(x, self._stats)
         sumsq, maxabs = self.dev.comm.sum_max(self._stats)
         if maxabs <= 1e-8:                                    # np.allclose(x0, 0) (:31)
             raise ValueError("x0 is not allowed to be 0 in the gauss_newton_krylow algorithm")
         nrm = math.sqrt(sumsq)                                # np.linalg.norm (:36)
-        self.be.vec_div(x, nrm, self.V[0], True)              # whole slab incl. ghosts (:37)
         self.k = 1
-        return np.array([nrm])
+        if u_jac is None:
+            self.be.vec_div(x, nrm, self.V[0], True)          # whole slab incl. ghosts (:37)
+            return np.array([nrm])
+        self.be.normalize_jnorm(u_jac, x, nrm, self.V[0], self._jn2)
+        return np.array([nrm]), math.sqrt(float(self.dev.comm.sum(self._jn2)[0])) / nrm
 
     def x(self, c: np.ndarray, out):
         """out = V @ c over the whole slab (ref:krylow.py:41-42)."""

@@ -9,7 +9,8 @@ R = R_Y P and Q^T r = R_Y^-T (Y^T r) to O(u) orthogonality.
 
 Preconditioner P (one pass per iteration in the common case):
   * CholQR2 (two passes: P = I, then P = R1) when there is no usable previous
-    factor -- first iteration, after a restart;
+    factor and no column scale (after a breakdown-free restart the solver passes
+    s = ||J v_0|| and the first solve is a single pass with P = [s]);
   * otherwise P = blockdiag(R_prev, s): the previous iteration's R of J_prev V
     (the basis only gained one column and J changed only in its diagonal
     LAMBDA exp(u)) and s = ||J v_new|| for the appended column, so Y is close to
@@ -67,9 +68,10 @@ class CholQR2Solver:
     def on_append(self, s_new: float):
         self.s_new = float(s_new)
 
-    def on_restart(self):
-        self.R_prev = None
-        self.s_new = None
+    def on_restart(self, s0: float = None):
+        """The basis restarted with one column v_0; s0 = ||J v_0|| (None: unknown -> CholQR2)."""
+        self.R_prev = None if s0 is None else np.zeros((0, 0))
+        self.s_new = None if s0 is None else float(s0)
 
     def _gram(self, u, basis, k, P, r):
         be = self.be
