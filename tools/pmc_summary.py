@@ -8,6 +8,7 @@ import csv
 import glob
 import json
 import os
+import re
 import sys
 from collections import defaultdict
 
@@ -21,7 +22,10 @@ def load(d, counter):
     return vals
 
 
-def main(d):
+GRAM = re.compile(r"k_gram_[smw]<")     # every Gram-pass kernel (staged / marching / chunked)
+
+
+def main(d, config=None):
     f = load(d, "FETCH_SIZE")
     w = load(d, "WRITE_SIZE")
     out = {"correction": "FETCH_SIZE x2 (16-B/lane reads on gfx950), WRITE_SIZE x1; KiB -> bytes", "kernels": {}}
@@ -33,13 +37,16 @@ def main(d):
         wm = sum(wv) / len(wv) if wv else 0.0
         out["kernels"][name] = {"launches": len(fv), "fetch_bytes_raw": fm, "fetch_bytes_corrected": 2 * fm,
                                 "write_bytes": wm, "traffic_bytes_per_launch": 2 * fm + wm}
-    gram = [k for k in out["kernels"] if "k_gram_w" in k]
+    gram = [k for k in out["kernels"] if GRAM.search(k)]
+    if config:
+        out["config"] = config
     if gram:
         tot = sum(out["kernels"][k]["traffic_bytes_per_launch"] * out["kernels"][k]["launches"] for k in gram)
         n = sum(out["kernels"][k]["launches"] for k in gram)
         out["traffic_bytes_per_launch"] = tot / n
+        out["gram_kernels"] = gram
     print(json.dumps(out, indent=1))
 
 
 if __name__ == "__main__":
-    main(sys.argv[1])
+    main(sys.argv[1], sys.argv[2] if len(sys.argv) > 2 else None)
