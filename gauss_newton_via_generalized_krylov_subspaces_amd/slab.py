@@ -45,15 +45,21 @@ class Comm:
             self.group = group
             self.rank = dist.get_rank(group)
             self.world = dist.get_world_size(group)
+            # gloo moves device tensors only through host copies (no P2P on GPU memory):
+            # stage through the host then (used to rehearse several ranks on one GPU)
+            self.stage = dist.get_backend(group) == "gloo"
         else:
             self.group = None
             self.rank, self.world = 0, 1
+            self.stage = False
 
     # -- reductions -------------------------------------------------------------
     def _gather(self, t: torch.Tensor) -> np.ndarray:
         if self.world == 1:
             return t.detach().to("cpu", torch.float64).numpy()[None]
         t = t.contiguous().reshape(-1)
+        if self.stage:
+            t = t.to("cpu")
         buf = torch.empty(self.world * t.numel(), dtype=t.dtype, device=t.device)
         dist.all_gather_into_tensor(buf, t, group=self.group)
         return buf.to("cpu").numpy().reshape(self.world, -1)
@@ -88,15 +94,22 @@ class Comm:
             return
         g = GHOST * N
         own_end = (GHOST + nrows) * N
+        staged = self.stage and vec.device.type != "cpu"
+        host = vec.to("cpu") if staged else vec
         ops = []
         if self.rank > 0:
-            ops.append(dist.P2POp(dist.isend, vec[g:2 * g], self.rank - 1, self.group))
-            ops.append(dist.P2POp(dist.irecv, vec[0:g], self.rank - 1, self.group))
+            ops.append(dist.P2POp(dist.isend, host[g:2 * g], self.rank - 1, self.group))
+            ops.append(dist.P2POp(dist.irecv, host[0:g], self.rank - 1, self.group))
         if self.rank < self.world - 1:
-            ops.append(dist.P2POp(dist.isend, vec[own_end - g:own_end], self.rank + 1, self.group))
-            ops.append(dist.P2POp(dist.irecv, vec[own_end:own_end + g], self.rank + 1, self.group))
+            ops.append(dist.P2POp(dist.isend, host[own_end - g:own_end], self.rank + 1, self.group))
+            ops.append(dist.P2POp(dist.irecv, host[own_end:own_end + g], self.rank + 1, self.group))
         for req in dist.batch_isend_irecv(ops):
             req.wait()
+        if staged:
+            if self.rank > 0:
+                vec[0:g].copy_(host[0:g])
+            if self.rank < self.world - 1:
+                vec[own_end:own_end + g].copy_(host[own_end:own_end + g])
 
     def gather_rows(self, owned: torch.Tensor, N: int) -> np.ndarray:
         """All ranks' owned rows -> the full host vector (variable slab sizes)."""

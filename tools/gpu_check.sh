@@ -13,6 +13,11 @@ if [[ $STEP == all || $STEP == test ]]; then
   run smoke && timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 &&
   run pytest && timeout -k 10 900 python -m pytest tests -m gpu -x -q > gpurun_out/pytest_gpu.log 2>&1 || exit $?
 fi
+if [[ $STEP == all || $STEP == dist ]]; then
+  # several ranks on this one GPU (gloo, host-staged collectives) vs the single-rank solve
+  run dist && timeout -k 10 600 torchrun --standalone --nproc-per-node 2 tools/dist_rehearsal.py --grid 256 > gpurun_out/dist2.json 2> gpurun_out/dist2.err &&
+  timeout -k 10 600 torchrun --standalone --nproc-per-node 3 tools/dist_rehearsal.py --grid 384 > gpurun_out/dist3.json 2> gpurun_out/dist3.err || exit $?
+fi
 if [[ $STEP == all || $STEP == bench ]]; then
   run bench && timeout -k 10 600 python bench.py > gpurun_out/bench.json 2> gpurun_out/bench.err || exit $?
 fi
