@@ -41,6 +41,17 @@ SIGNATURES = {
     "gnk_cgs_update": (_c_int, [_c_vp, _c_vp, _c_i64, _c_int, _c_vp, _c_vp, _c_vp]),
     "gnk_vec_stats": (_c_int, [_c_vp, _c_vp, _c_vp]),
     "gnk_vec_div": (_c_int, [_c_vp, _c_vp, _c_dbl, _c_vp, _c_int]),
+    "gnk_flat_gemv": (_c_int, [_c_vp, _c_vp, _c_i64, _c_int, _c_vp, _c_vp, _c_i64]),
+    "gnk_flat_gemv_t": (_c_int, [_c_vp, _c_vp, _c_i64, _c_int, _c_vp, _c_i64, _c_vp]),
+    "gnk_flat_cgs_update": (_c_int, [_c_vp, _c_vp, _c_i64, _c_int, _c_vp, _c_vp, _c_i64, _c_vp]),
+    "gnk_flat_stats": (_c_int, [_c_vp, _c_vp, _c_i64, _c_vp]),
+    "gnk_flat_dot": (_c_int, [_c_vp, _c_vp, _c_vp, _c_i64, _c_vp]),
+    "gnk_flat_div": (_c_int, [_c_vp, _c_vp, _c_dbl, _c_vp, _c_i64]),
+    "gnk_flat_axpy": (_c_int, [_c_vp, _c_vp, _c_dbl, _c_vp, _c_vp, _c_i64]),
+    "gnk_flat_cg_update_xr": (_c_int, [_c_vp, _c_dbl, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_i64, _c_vp]),
+    "gnk_flat_cg_update_p": (_c_int, [_c_vp, _c_dbl, _c_int, _c_vp, _c_vp, _c_i64]),
+    "gnk_csr_spmv": (_c_int, [_c_vp, _c_i64, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_int]),
+    "gnk_flat_gram": (_c_int, [_c_vp, _c_vp, _c_i64, _c_int, _c_vp, _c_i64, _c_vp, _c_i64, _c_vp]),
     "gnk_basis_gemv_vjp_gemv_t": (_c_int, [_c_vp, _c_vp, _c_i64, _c_int, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp]),
     "gnk_normalize_jnorm": (_c_int, [_c_vp, _c_vp, _c_vp, _c_dbl, _c_vp, _c_vp]),
     "gnk_vec_axpy": (_c_int, [_c_vp, _c_vp, _c_dbl, _c_vp, _c_vp, _c_int]),
@@ -172,6 +183,42 @@ class HipBackend:
 
     def gemv_vjp_gemv_t(self, V, k, c, r, x, g, h):
         self._call("gnk_basis_gemv_vjp_gemv_t", _p(V), V.stride(0), int(k), _p(c), _p(r), _p(x), _p(g), _p(h))
+
+    # -- flat vectors (generic problems) --------------------------------------------------
+    def flat_gemv(self, V, k, c, x):
+        self._call("gnk_flat_gemv", _p(V), V.stride(0), int(k), _p(c), _p(x), x.numel())
+
+    def flat_gemv_t(self, V, k, g, h):
+        self._call("gnk_flat_gemv_t", _p(V), V.stride(0), int(k), _p(g), g.numel(), _p(h))
+
+    def flat_cgs_update(self, V, k, h, g, stats):
+        self._call("gnk_flat_cgs_update", _p(V), V.stride(0), int(k), _p(h), _p(g), g.numel(), _p(stats))
+
+    def flat_stats(self, x, stats):
+        self._call("gnk_flat_stats", _p(x), x.numel(), _p(stats))
+
+    def flat_dot(self, a, b, out):
+        self._call("gnk_flat_dot", _p(a), _p(b), a.numel(), _p(out))
+
+    def flat_div(self, src, denom, dst):
+        self._call("gnk_flat_div", _p(src), float(denom), _p(dst), src.numel())
+
+    def flat_axpy(self, x, alpha, d, out):
+        self._call("gnk_flat_axpy", _p(x), float(alpha), _p(d), _p(out), x.numel())
+
+    def flat_cg_update_xr(self, alpha, p, q, x, r, dinv, z, out):
+        self._call("gnk_flat_cg_update_xr", float(alpha), _p(p), _p(q), _p(x), _p(r), _p(dinv), _p(z), x.numel(),
+                   _p(out))
+
+    def flat_cg_update_p(self, beta, first, z, p):
+        self._call("gnk_flat_cg_update_p", float(beta), int(bool(first)), _p(z), _p(p), p.numel())
+
+    def csr_spmv(self, nrows, indptr, indices, data, x, y, negate=False):
+        self._call("gnk_csr_spmv", int(nrows), _p(indptr), _p(indices), _p(data), _p(x), _p(y), int(bool(negate)))
+
+    def flat_gram(self, W, k, rinv, r, m, G):
+        kp = self.gram_dim(k, r is not None)
+        self._call("gnk_flat_gram", _p(W), W.stride(0), int(k), _p(rinv), kp, _p(r), int(m), _p(G))
 
     def cgs_update(self, V, k, h, g, stats):
         self._call("gnk_cgs_update", _p(V), V.stride(0), int(k), _p(h), _p(g), _p(stats))

@@ -38,6 +38,8 @@ constexpr int BLOCK = 256;
 constexpr int MAX_RED_BLOCKS = 1 << 20;  // cap on per-block partials of a reduction
 constexpr int PPW_MAX = 10;              // Gram accumulator tiles per wave (pair-split mode)
 constexpr size_t SCRATCH_DOUBLES = size_t(16) << 20;   // 128 MiB arena
+// offset of the (16 nb)^2 identity in gnk_ctx::ident (nb = 1..4; nb = 5 -> total size)
+constexpr int ident_offset(int nb) { return nb == 1 ? 0 : ident_offset(nb - 1) + 256 * (nb - 1) * (nb - 1); }
 
 typedef double d2 __attribute__((ext_vector_type(2)));
 typedef double d4 __attribute__((ext_vector_type(4)));
@@ -1583,6 +1585,126 @@ __global__ __launch_bounds__(BLOCK) void k_gram_scatter_s(const double* __restri
   }
 }
 
+// ---------------------------------------------------------------- generic problems (flat vectors)
+// Problems other than Bratu keep plain length-n iterate vectors and length-m
+// residual vectors; the basis kernels above run on them with a flat geometry (one "row" of n).
+
+// h[j0 + j] partial = V_j . g over a flat vector (the Bratu path fuses this with -J^T r)
+template <int VEC, int KCT>
+__global__ __launch_bounds__(BLOCK) void k_gemv_t(const double* __restrict__ V, int64_t ldv, int k,
+                                                  const double* __restrict__ g, Geo geo, int64_t lr0, int64_t nlr,
+                                                  double* __restrict__ partial) {
+  __shared__ double sh[(BLOCK / 64) * KCT];
+  const int j0 = blockIdx.z * KCT;
+  const int kc = max(0, min(KCT, k - j0));
+  const int jmax = k - 1;
+  double acc[KCT];
+#pragma unroll
+  for (int j = 0; j < KCT; ++j) acc[j] = 0.0;
+  ROW_LOOP_BEGIN(VEC)
+  for (int q = 0; q < VEC && iy + q < N; ++q) {
+    const double gi = g[li + q];
+#pragma unroll
+    for (int j = 0; j < KCT; ++j) acc[j] = acc[j] + V[min(j0 + j, jmax) * ldv + li + q] * gi;
+  }
+  ROW_LOOP_END
+  const int nblk = gridDim.x * gridDim.y;
+  block_sum_store<KCT>(acc, kc, partial + (size_t(blockIdx.z) * nblk + blockIdx.y * gridDim.x + blockIdx.x) * KCT, sh);
+}
+
+// y = A x (neg: y = -(A x)) for a CSR matrix with 32-bit indices; one thread per row, entries in
+// stored order from 0 -- scipy's csr_matvec rounding (compiled without FMA contraction)
+__global__ __launch_bounds__(BLOCK) void k_csr_spmv(int64_t nrows, const int* __restrict__ indptr,
+                                                    const int* __restrict__ indices, const double* __restrict__ data,
+                                                    const double* __restrict__ x, double* __restrict__ y, int neg) {
+  for (int64_t i = int64_t(blockIdx.x) * BLOCK + threadIdx.x; i < nrows; i += int64_t(gridDim.x) * BLOCK) {
+    double s = 0.0;
+    for (int jj = indptr[i]; jj < indptr[i + 1]; ++jj) s = s + data[jj] * x[indices[jj]];
+    y[i] = neg ? -s : s;
+  }
+}
+
+// partial of a . b over a flat vector
+template <int VEC>
+__global__ __launch_bounds__(BLOCK) void k_dot(const double* __restrict__ a, const double* __restrict__ b, Geo geo,
+                                               int64_t lr0, int64_t nlr, double* __restrict__ partial) {
+  __shared__ double sh[BLOCK / 64];
+  double acc[1] = {0.0};
+  ROW_LOOP_BEGIN(VEC)
+  for (int q = 0; q < VEC && iy + q < N; ++q) acc[0] += a[li + q] * b[li + q];
+  ROW_LOOP_END
+  block_sum_store<1>(acc, 1, partial + (blockIdx.y * gridDim.x + blockIdx.x), sh);
+}
+
+// Gram of [W P^-1 | r] for a materialised W (k columns of length m, column stride ldw):
+// 16-row chunks per wave, A fragments loaded in the f64 MFMA operand layout, the transform on
+// MFMA with the RinvAug B fragments in VGPRs and the transformed rows fed to the Gram MFMAs from
+// registers (as k_gram_s); all NB (NB + 1) / 2 pair tiles on MFMA.  Block partials [block][P][256].
+template <int NB>
+__global__ __launch_bounds__(BLOCK) void k_flat_gram(const double* __restrict__ W, int64_t ldw, int k,
+                                                     const double* __restrict__ rinv, int ldr,
+                                                     const double* __restrict__ r, int64_t m,
+                                                     double* __restrict__ partial) {
+  constexpr int P = NB * (NB + 1) / 2;
+  __shared__ double red[P * 256];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  double rB[NB][NB][4];
+#pragma unroll
+  for (int cb = 0; cb < NB; ++cb)
+#pragma unroll
+    for (int ab = 0; ab <= cb; ++ab)
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) rB[cb][ab][ks] = rinv[(ab * 16 + ks * 4 + (lane >> 4)) * ldr + cb * 16 + (lane & 15)];
+  d4 acc[P];
+#pragma unroll
+  for (int q = 0; q < P; ++q) acc[q] = d4{0.0, 0.0, 0.0, 0.0};
+  const int64_t nchunk = (m + 15) / 16;
+  const int64_t nw = int64_t(gridDim.x) * (BLOCK / 64);
+  for (int64_t c = int64_t(blockIdx.x) * (BLOCK / 64) + wave; c < nchunk; c += nw) {
+    const int64_t row = c * 16 + (lane & 15);
+    const bool rv = row < m;
+    const int64_t rowc = rv ? row : m - 1;
+    double a[NB][4];
+#pragma unroll
+    for (int ab = 0; ab < NB; ++ab)
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        const int j = ab * 16 + ks * 4 + (lane >> 4);
+        const double* src = j < k ? W + int64_t(j) * ldw : r;   // a valid row always (clamped)
+        const double v = (r || j < k) ? src[rowc] : 0.0;
+        a[ab][ks] = (rv && (j < k || (r && j == k))) ? v : 0.0;
+      }
+    d4 qv[NB];
+#pragma unroll
+    for (int cb = 0; cb < NB; ++cb) {
+      qv[cb] = d4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+      for (int ab = 0; ab <= cb; ++ab)
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks) qv[cb] = mfma64(a[ab][ks], rB[cb][ab][ks], qv[cb]);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int q = 0; q < P; ++q) acc[q] = mfma64(qv[pair_a(q, NB)][i], qv[pair_b(q, NB)][i], acc[q]);
+  }
+  for (int w = 0; w < BLOCK / 64; ++w) {
+    if (wave == w) {
+#pragma unroll
+      for (int q = 0; q < P; ++q)
+#pragma unroll
+        for (int ii = 0; ii < 4; ++ii) {
+          double* dst = red + q * 256 + lane * 4 + ii;
+          *dst = (w == 0) ? acc[q][ii] : *dst + acc[q][ii];
+        }
+    }
+    __syncthreads();
+  }
+  double* out = partial + size_t(blockIdx.x) * size_t(P) * 256;
+  for (int t = tid; t < P * 256; t += BLOCK) out[t] = red[t];
+}
+
 // Sum Gram partials over blocks (block order) and scatter into G[KP][KP] (symmetric).
 // scatter the reduced pair tiles (red[pair * 256 + lane * 4 + i]) into symmetric G[KP][KP]
 __global__ __launch_bounds__(BLOCK) void k_gram_scatter(const double* __restrict__ red, int P, int KP,
@@ -1645,7 +1767,7 @@ struct gnk_ctx {
   Geo geo{0, 0, 0};
   Coef coef{};
   double* scratch = nullptr;
-  double* ident = nullptr;     // 16x16 and 32x32 identities (RinvAug of an unpreconditioned pass)
+  double* ident = nullptr;     // 16², 32², 48², 64² identities (RinvAug of an unpreconditioned pass)
   int num_cus = 256;
   std::string err;
   // per-launch timer (tooling, see gnk_timer_start)
@@ -1757,6 +1879,19 @@ const int* sum_max_flags() {
   return static_cast<const int*>(p);
 }
 
+// flat geometry helpers (generic problems)
+bool ctx_ok(gnk_ctx* ctx) { return ctx != nullptr; }
+int flat_vec(int64_t n, int64_t ldv = 0) { return (n % 2 == 0 && ldv % 2 == 0) ? 2 : 1; }
+RowLaunch flat_rows(int64_t n, int vec, int cap = MAX_RED_BLOCKS) {
+  RowLaunch L;
+  const int64_t per = int64_t(BLOCK) * vec;
+  const int64_t bx = std::max<int64_t>(1, std::min<int64_t>((n + per - 1) / per, cap));
+  L.grid = dim3(unsigned(bx), 1, 1);
+  L.lr0 = 0;
+  L.nlr = 1;
+  return L;
+}
+
 }  // namespace
 
 extern "C" {
@@ -1778,9 +1913,9 @@ int gnk_ctx_create(int device, gnk_ctx** out) {
     return -3;
   }
   {
-    std::vector<double> id(256 + 1024, 0.0);
-    for (int i = 0; i < 16; ++i) id[i * 16 + i] = 1.0;
-    for (int i = 0; i < 32; ++i) id[256 + i * 32 + i] = 1.0;
+    std::vector<double> id(ident_offset(5), 0.0);
+    for (int b = 1; b <= 4; ++b)
+      for (int i = 0; i < 16 * b; ++i) id[ident_offset(b) + i * 16 * b + i] = 1.0;
     e = hipMalloc(&ctx->ident, id.size() * sizeof(double));
     if (e == hipSuccess) e = hipMemcpy(ctx->ident, id.data(), id.size() * sizeof(double), hipMemcpyHostToDevice);
     if (e != hipSuccess) {
@@ -2053,7 +2188,7 @@ int gnk_gram(gnk_ctx* ctx, const double* u, const double* V, int64_t ldv, int k,
     const int L = (nrow + 1 + GS_NW - 1) / GS_NW;
     const size_t lds = size_t(GS_R) * (size_t(nrow) * GS_CS + 128) * sizeof(double);
     if (L <= 4 && lds <= 160 * 1024) {
-      const double* rv = rinv ? rinv : ctx->ident + (KP == 16 ? 0 : 256);
+      const double* rv = rinv ? rinv : ctx->ident + ident_offset(KP / 16);
       // 4-column k-steps of the last transform block
       const int ksl = ((k - 16 * (nbs - 1)) + 3) / 4;
       const int nacc = gs_nacc(nbs, ksl);
@@ -2230,6 +2365,163 @@ int gnk_gram(gnk_ctx* ctx, const double* u, const double* V, int64_t ldv, int k,
   hipLaunchKernelGGL(k_gram_reduce, dim3((P * 256 + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, ctx->stream, ctx->scratch,
                      int(nblk), P, rowsplit, KP, G_out);
   return check_launch(ctx, "gram reduce");
+}
+
+// ---------------------------------------------------------------- generic problems (flat vectors)
+// No gnk_set_bratu needed: explicit lengths, a flat geometry (one "row" of n points).
+
+#define FLAT_DISPATCH(VEC_, KERNEL, L, ...)                                                            \
+  do {                                                                                                \
+    if ((VEC_) == 2) hipLaunchKernelGGL(KERNEL<2>, L.grid, dim3(BLOCK), 0, ctx->stream, __VA_ARGS__);  \
+    else hipLaunchKernelGGL(KERNEL<1>, L.grid, dim3(BLOCK), 0, ctx->stream, __VA_ARGS__);              \
+  } while (0)
+
+int gnk_flat_gemv(gnk_ctx* ctx, const double* V, int64_t ldv, int k, const double* c, double* x, int64_t n) {
+  if (!ctx_ok(ctx)) return -1;
+  if (k < 1 || n < 1) return fail(ctx, "flat_gemv: k < 1 or n < 1");
+  const int vec = flat_vec(n, ldv);
+  const Geo geo{n, 0, 1};
+  RowLaunch L = flat_rows(n, vec, 1 << 30);
+  FLAT_DISPATCH(vec, k_gemv, L, V, ldv, k, c, x, geo, L.lr0, L.nlr);
+  return check_launch(ctx, "flat_gemv");
+}
+
+int gnk_flat_gemv_t(gnk_ctx* ctx, const double* V, int64_t ldv, int k, const double* g, int64_t n, double* h_out) {
+  if (!ctx_ok(ctx)) return -1;
+  if (k < 1 || n < 1) return fail(ctx, "flat_gemv_t: k < 1 or n < 1");
+  constexpr int KCT = 8;
+  const int nchunk = (k + KCT - 1) / KCT;
+  const int vec = flat_vec(n, ldv);
+  const Geo geo{n, 0, 1};
+  RowLaunch L = flat_rows(n, vec, std::max(64, 4096 / nchunk));
+  L.grid.z = nchunk;
+  const int nblk = L.grid.x;
+  if (size_t(nblk) * nchunk * KCT > SCRATCH_DOUBLES) return fail(ctx, "flat_gemv_t: scratch too small");
+  if (vec == 2)
+    hipLaunchKernelGGL((k_gemv_t<2, KCT>), L.grid, dim3(BLOCK), 0, ctx->stream, V, ldv, k, g, geo, L.lr0, L.nlr,
+                       ctx->scratch);
+  else
+    hipLaunchKernelGGL((k_gemv_t<1, KCT>), L.grid, dim3(BLOCK), 0, ctx->stream, V, ldv, k, g, geo, L.lr0, L.nlr,
+                       ctx->scratch);
+  int rc = check_launch(ctx, "flat_gemv_t");
+  if (rc) return rc;
+  return wreduce(ctx, ctx->scratch, nblk, k, KCT, KCT, int64_t(nblk) * KCT, nullptr, h_out);
+}
+
+int gnk_flat_cgs_update(gnk_ctx* ctx, const double* V, int64_t ldv, int k, const double* h, double* g, int64_t n,
+                        double* stats_out) {
+  if (!ctx_ok(ctx)) return -1;
+  if (k < 1 || n < 1) return fail(ctx, "flat_cgs_update: k < 1 or n < 1");
+  const int vec = flat_vec(n, ldv);
+  const Geo geo{n, 0, 1};
+  RowLaunch L = flat_rows(n, vec);
+  FLAT_DISPATCH(vec, k_cgs, L, V, ldv, k, h, g, geo, L.lr0, L.nlr, ctx->scratch);
+  int rc = check_launch(ctx, "flat_cgs_update");
+  if (rc) return rc;
+  return reduce(ctx, ctx->scratch, int(L.grid.x), 2, 2, sum_max_flags(), stats_out);
+}
+
+int gnk_flat_stats(gnk_ctx* ctx, const double* x, int64_t n, double* stats_out) {
+  if (!ctx_ok(ctx)) return -1;
+  if (n < 1) return fail(ctx, "flat_stats: n < 1");
+  const int vec = flat_vec(n);
+  const Geo geo{n, 0, 1};
+  RowLaunch L = flat_rows(n, vec);
+  FLAT_DISPATCH(vec, k_stats, L, x, geo, L.lr0, L.nlr, ctx->scratch);
+  int rc = check_launch(ctx, "flat_stats");
+  if (rc) return rc;
+  return reduce(ctx, ctx->scratch, int(L.grid.x), 2, 2, sum_max_flags(), stats_out);
+}
+
+int gnk_flat_dot(gnk_ctx* ctx, const double* a, const double* b, int64_t n, double* out) {
+  if (!ctx_ok(ctx)) return -1;
+  if (n < 1) return fail(ctx, "flat_dot: n < 1");
+  const int vec = flat_vec(n);
+  const Geo geo{n, 0, 1};
+  RowLaunch L = flat_rows(n, vec);
+  FLAT_DISPATCH(vec, k_dot, L, a, b, geo, L.lr0, L.nlr, ctx->scratch);
+  int rc = check_launch(ctx, "flat_dot");
+  if (rc) return rc;
+  return reduce(ctx, ctx->scratch, int(L.grid.x), 1, 1, nullptr, out);
+}
+
+int gnk_flat_div(gnk_ctx* ctx, const double* src, double denom, double* dst, int64_t n) {
+  if (!ctx_ok(ctx)) return -1;
+  const int vec = flat_vec(n);
+  const Geo geo{n, 0, 1};
+  RowLaunch L = flat_rows(n, vec, 1 << 30);
+  FLAT_DISPATCH(vec, k_div, L, src, denom, dst, geo, L.lr0, L.nlr);
+  return check_launch(ctx, "flat_div");
+}
+
+int gnk_flat_axpy(gnk_ctx* ctx, const double* x, double alpha, const double* d, double* out, int64_t n) {
+  if (!ctx_ok(ctx)) return -1;
+  const int vec = flat_vec(n);
+  const Geo geo{n, 0, 1};
+  RowLaunch L = flat_rows(n, vec, 1 << 30);
+  FLAT_DISPATCH(vec, k_axpy, L, x, alpha, d, out, geo, L.lr0, L.nlr);
+  return check_launch(ctx, "flat_axpy");
+}
+
+int gnk_flat_cg_update_xr(gnk_ctx* ctx, double alpha, const double* p, const double* q, double* x, double* r,
+                          const double* dinv, double* z, int64_t n, double* out) {
+  if (!ctx_ok(ctx)) return -1;
+  const int vec = flat_vec(n);
+  const Geo geo{n, 0, 1};
+  RowLaunch L = flat_rows(n, vec);
+  FLAT_DISPATCH(vec, k_cg_xr, L, alpha, p, q, x, r, dinv, z, geo, L.lr0, L.nlr, ctx->scratch);
+  int rc = check_launch(ctx, "flat_cg_update_xr");
+  if (rc) return rc;
+  return reduce(ctx, ctx->scratch, int(L.grid.x), 2, 2, nullptr, out);
+}
+
+int gnk_flat_cg_update_p(gnk_ctx* ctx, double beta, int first, const double* z, double* p, int64_t n) {
+  if (!ctx_ok(ctx)) return -1;
+  const int vec = flat_vec(n);
+  const Geo geo{n, 0, 1};
+  RowLaunch L = flat_rows(n, vec, 1 << 30);
+  FLAT_DISPATCH(vec, k_cg_p, L, beta, first, z, p, geo, L.lr0, L.nlr);
+  return check_launch(ctx, "flat_cg_update_p");
+}
+
+int gnk_csr_spmv(gnk_ctx* ctx, int64_t nrows, const int* indptr, const int* indices, const double* data,
+                 const double* x, double* y, int negate) {
+  if (!ctx_ok(ctx)) return -1;
+  if (nrows < 1 || !indptr || !x || !y) return fail(ctx, "csr_spmv: bad arguments");
+  const int64_t nb = std::min<int64_t>((nrows + BLOCK - 1) / BLOCK, 1 << 20);
+  hipLaunchKernelGGL(k_csr_spmv, dim3(unsigned(nb)), dim3(BLOCK), 0, ctx->stream, nrows, indptr, indices, data, x, y,
+                     negate);
+  return check_launch(ctx, "csr_spmv");
+}
+
+int gnk_flat_gram(gnk_ctx* ctx, const double* W, int64_t ldw, int k, const double* rinv, int64_t ldr,
+                  const double* r, int64_t m, double* G_out) {
+  if (!ctx_ok(ctx)) return -1;
+  if (k < 1 || m < 1) return fail(ctx, "flat_gram: k < 1 or m < 1");
+  const int KP = gnk_gram_padded_dim(k, r != nullptr);
+  const int nb = KP / 16;
+  if (nb > 4) return fail(ctx, "flat_gram: at most 63 basis columns (+ r)");
+  if (rinv && ldr != KP) return fail(ctx, "flat_gram: rinv must be the kp x kp augmented inverse (ldr == kp)");
+  const double* rv = rinv ? rinv : ctx->ident + ident_offset(nb);
+  const int P = nb * (nb + 1) / 2;
+  const int64_t nchunk = (m + 15) / 16;
+  const int nblk = int(std::max<int64_t>(1, std::min<int64_t>((nchunk + 3) / 4, 1024)));
+  if (size_t(nblk) * P * 256 > SCRATCH_DOUBLES - size_t(P) * 256) return fail(ctx, "flat_gram: scratch too small");
+  switch (nb) {
+    case 1: hipLaunchKernelGGL(k_flat_gram<1>, dim3(nblk), dim3(BLOCK), 0, ctx->stream, W, ldw, k, rv, KP, r, m, ctx->scratch); break;
+    case 2: hipLaunchKernelGGL(k_flat_gram<2>, dim3(nblk), dim3(BLOCK), 0, ctx->stream, W, ldw, k, rv, KP, r, m, ctx->scratch); break;
+    case 3: hipLaunchKernelGGL(k_flat_gram<3>, dim3(nblk), dim3(BLOCK), 0, ctx->stream, W, ldw, k, rv, KP, r, m, ctx->scratch); break;
+    default: hipLaunchKernelGGL(k_flat_gram<4>, dim3(nblk), dim3(BLOCK), 0, ctx->stream, W, ldw, k, rv, KP, r, m, ctx->scratch); break;
+  }
+  int rc = check_launch(ctx, "flat_gram");
+  if (rc) return rc;
+  (void)hipMemsetAsync(G_out, 0, size_t(KP) * KP * sizeof(double), ctx->stream);
+  double* red = ctx->scratch + (SCRATCH_DOUBLES - size_t(P) * 256);
+  rc = wreduce(ctx, ctx->scratch, nblk, P * 256, int64_t(P) * 256, P * 256, 0, nullptr, red);
+  if (rc) return rc;
+  hipLaunchKernelGGL(k_gram_scatter, dim3((P * 256 + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, ctx->stream, red, P, KP,
+                     G_out);
+  return check_launch(ctx, "flat_gram scatter");
 }
 
 int gnk_cg_normal_matvec(gnk_ctx* ctx, const double* d, const double* p, double* q, double* pq_out) {

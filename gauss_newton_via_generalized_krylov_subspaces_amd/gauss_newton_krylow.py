@@ -17,8 +17,12 @@ Host <-> device traffic per iteration is O(k^2) doubles (Gram matrices, k
 coefficients, a few scalars).  ``GNKSolver`` exposes the same loop one outer
 iteration at a time (used by bench.py to time exact steps).
 
-Problems: the device path needs the residual/Jacobian to come from this
-package's ``BratuPdeProblem.make_res`` / ``make_jac`` (matrix-free Bratu).
+Problems: ``BratuPdeProblem.make_res`` / ``make_jac`` of this package run the
+matrix-free Bratu kernels on row slabs (multi-GPU capable); any other ``res`` /
+``jac`` callables (the reference's duck typing: ``jac(x)`` returning a scipy sparse
+matrix or an ndarray) run through ``generic.HostCallableOps`` -- the user's
+functions are evaluated on their NumPy inputs, J and J^T are uploaded as CSR and
+every n- and m-sized operation of the loop runs in the HIP library (single GPU).
 """
 from __future__ import annotations
 
@@ -45,13 +49,57 @@ def _noop(**kwargs):
 
 
 def resolve_bratu(res, jac):
-    if not isinstance(res, BratuResidual) or not isinstance(jac, BratuJacobianFunction):
-        raise TypeError(
-            "the MI355X solver runs matrix-free problems: pass res = BratuPdeProblem.make_res(y) and "
-            "jac = BratuPdeProblem.make_jac() from gauss_newton_via_generalized_krylov_subspaces_amd")
-    if res.problem is not jac.problem:
-        raise ValueError("res and jac must come from the same BratuPdeProblem")
-    return res.problem, res.y
+    """(problem, y) for the matrix-free Bratu path, None for generic callables."""
+    if isinstance(res, BratuResidual) and isinstance(jac, BratuJacobianFunction):
+        if res.problem is not jac.problem:
+            raise ValueError("res and jac must come from the same BratuPdeProblem")
+        return res.problem, res.y
+    if isinstance(res, BratuResidual) or isinstance(jac, BratuJacobianFunction):
+        raise TypeError("pass both res = BratuPdeProblem.make_res(y) and jac = BratuPdeProblem.make_jac()")
+    return None
+
+
+class BratuOps:
+    """Problem side of the GNK loop for the matrix-free Bratu problem: slab vectors on this rank,
+    fused residual kernel, the Krylov basis and least-squares solver of this package."""
+
+    jacobian_is_free = True        # J(u) is u itself on the device: no evaluation to schedule
+    fuse_trial = True              # the res_old first trial may carry the update products
+
+    def __init__(self, problem, y, comm=None, device=None, backend=None):
+        self.dev = BratuDevice(problem, comm, device, backend)
+        self.be = self.dev.backend
+        self.comm = self.dev.comm
+        self.n_global = self.dev.slab.n_global
+        self.y = self.dev.load(y)
+        self._n2 = self.dev.scalar(1)
+
+    def vec(self):
+        return self.dev.vec()
+
+    rvec = vec
+
+    def load(self, x0):
+        return self.dev.load(x0)
+
+    def residual(self, x, r) -> float:
+        self.be.residual(x, self.y, r, self._n2)
+        return float(self.comm.sum(self._n2)[0])
+
+    def to_host(self, x):
+        return self.dev.slab.to_host(x)
+
+    def own(self, x):
+        return x[self.dev.slab.own]
+
+    def make_basis(self, kmax):
+        return DeviceKrylovBasis(self.dev, kmax)
+
+    def make_lls(self, kmax):
+        return CholQR2Solver(self.dev, kmax)
+
+    def on_jacobian(self, u):
+        pass
 
 
 class GNKSolver:
@@ -59,30 +107,28 @@ class GNKSolver:
 
     def __init__(self, problem, y, krylow_restart=None, tol=1e-8, max_iter=100, version="res_old",
                  comm: Optional[Comm] = None, device=None, backend=None, callback: Callable = None,
-                 callback_format: str = "numpy"):
-        self.dev = BratuDevice(problem, comm, device, backend)
-        self.be = self.dev.backend
-        self.comm = self.dev.comm
+                 callback_format: str = "numpy", ops=None):
+        self.ops = ops if ops is not None else BratuOps(problem, y, comm, device, backend)
+        self.dev = getattr(self.ops, "dev", None)
+        self.be = self.ops.be
+        self.comm = self.ops.comm
         self.tol = tol
         self.max_iter = int(max_iter)
         self.version = version
         self.restart = self.max_iter if krylow_restart is None else int(krylow_restart)
         kmax = min(self.restart, max(self.max_iter - 1, 1)) + 1
-        kmax = min(kmax, self.dev.slab.n_global)
+        kmax = min(kmax, self.ops.n_global)
         self.callback = callback
         self.callback_format = callback_format
-        self.y = self.dev.load(y)
-        self.basis = DeviceKrylovBasis(self.dev, kmax)
-        self.lls = CholQR2Solver(self.dev, kmax)
-        self.xb = [self.dev.vec() for _ in range(3)]
-        self.rb = [self.dev.vec() for _ in range(2)]
-        self._n2 = self.dev.scalar(1)
+        self.basis = self.ops.make_basis(kmax)
+        self.lls = self.ops.make_lls(kmax)
+        self.xb = [self.ops.vec() for _ in range(3)]
+        self.rb = None           # residual buffers: allocated at setup (generic problems learn m there)
         self.trace = []          # per-iteration (t, k, trials) for tests / diagnostics
 
     # -- pieces -------------------------------------------------------------------------
     def _residual(self, x, r) -> float:
-        self.be.residual(x, self.y, r, self._n2)
-        return float(self.comm.sum(self._n2)[0])
+        return self.ops.residual(x, r)
 
     def _free_x(self, *busy):
         for i in range(3):
@@ -93,10 +139,7 @@ class GNKSolver:
     def _emit(self, xslab):
         if self.callback is None:
             return
-        if self.callback_format == "torch":
-            x = xslab[self.dev.slab.own]
-        else:
-            x = self.dev.slab.to_host(xslab)
+        x = self.ops.own(xslab) if self.callback_format == "torch" else self.ops.to_host(xslab)
         self.callback(x=x, nfev=self.nfev, cg_iter=None)
 
     # -- loop ---------------------------------------------------------------------------
@@ -106,14 +149,21 @@ class GNKSolver:
         self.iter = 0
         self.done = False
         self.uJ = 0                                        # J is evaluated at x0 (:78)
-        self.xb[0].copy_(self.dev.load(x0))
-        self.c, s0 = self.basis.start(self.xb[0], self.xb[self.uJ])   # :71 (+ ||J(x0) v_0||)
-        self.lls.on_restart(s0)
+        self.xb[0].copy_(self.ops.load(x0))
+        if self.ops.jacobian_is_free:
+            self.c, s0 = self.basis.start(self.xb[0], self.xb[self.uJ])   # :71 (+ ||J(x0) v_0||)
+            self.lls.on_restart(s0)
+        else:
+            self.c = self.basis.start(self.xb[0])                         # :71
+            self.lls.on_restart(None)
         xi = self._free_x(self.uJ)
         self.basis.x(self.c, self.xb[xi])
+        if self.rb is None:
+            self.rb = [self.ops.rvec() for _ in range(2)]
         self.ri = 0
         self.rr = self._residual(self.xb[xi], self.rb[0])  # :76 (at V @ c)
         self.nfev = 1
+        self.ops.on_jacobian(self.xb[0])                   # :78 jac(x0)
         self.njev = 1
         if self.max_iter < 2:
             raise UnboundLocalError("local variable 'iter' referenced before assignment")
@@ -131,7 +181,7 @@ class GNKSolver:
         # res_old: the update after an accepted first trial is g = -J(x_t)^T r_old, h = V^T g --
         # computed from the same read of V as the trial point itself (speculative; a rejected
         # first trial falls back to the separate update products)
-        fuse = self.version == "res_old" and 1 <= basis.k <= basis.FUSE_KMAX
+        fuse = self.ops.fuse_trial and self.version == "res_old" and 1 <= basis.k <= basis.FUSE_KMAX
 
         def trial(t):
             if fuse and not last:
@@ -155,6 +205,7 @@ class GNKSolver:
             self.done = True
             return True
         uJ_old, self.uJ = self.uJ, xi                                     # :106-108
+        self.ops.on_jacobian(self.xb[self.uJ])
         self.njev += 1
         u_new = self.xb[self.uJ]      # the next LS solve's J; s = ||J(u_new) v_new|| (lls.py)
         try:
@@ -193,7 +244,7 @@ class GNKSolver:
             print("Warning: The gauss_newton_krylow algorithm reached maximal iteration bound before terminating!")
         xi = self._free_x(self.uJ)
         xs = self.basis.x(self.c, self.xb[xi])
-        x = xs[self.dev.slab.own].clone() if result_format == "torch" else self.dev.slab.to_host(xs)
+        x = self.ops.own(xs).clone() if result_format == "torch" else self.ops.to_host(xs)
         return RegressionResult("gauss newton krylow", x, self.success, self.nfev, self.njev, self.iter)
 
 
@@ -208,12 +259,21 @@ def gauss_newton_krylow(res, x0, jac, krylow_restart: Optional[int] = None, args
     ("numpy": full host vector like the reference; "torch": this rank's device rows),
     ``result_format`` (same choice for ``RegressionResult.x``).
     """
-    problem, y = resolve_bratu(res, jac)
-    if args:
-        raise TypeError("<lambda>() takes 1 positional argument but {} were given".format(1 + len(args)))
+    bratu = resolve_bratu(res, jac)
     cb = None if (callback is None or callback is _noop) else callback
+    if bratu is not None:
+        if args:
+            raise TypeError("<lambda>() takes 1 positional argument but {} were given".format(1 + len(args)))
+        problem, y = bratu
+        ops = None
+    else:
+        from .generic import HostCallableOps
+        problem, y = None, None
+        x0h = x0.detach().cpu().numpy() if torch.is_tensor(x0) else np.asarray(x0, dtype=np.float64)
+        ops = HostCallableOps(res, jac, x0h.size, args, device=device, backend=_backend)
     solver = GNKSolver(problem, y, krylow_restart=krylow_restart, tol=tol, max_iter=max_iter, version=version,
-                       comm=comm, device=device, backend=_backend, callback=cb, callback_format=callback_format)
+                       comm=comm, device=device, backend=_backend, callback=cb, callback_format=callback_format,
+                       ops=ops)
     solver.setup(x0 if not torch.is_tensor(x0) else x0.detach().cpu().numpy())
     while not solver.step():
         pass

@@ -1,0 +1,229 @@
+"""Generic problems on the device: any ``res`` / ``jac`` callables.
+
+The reference duck-types its problem (ref:gauss_newton_krylow.py:39-49): ``res(x, *args)``
+returns the residual vector and ``jac(x, *args)`` anything supporting ``J @ V``, ``J @ v`` and
+``J.T @ r`` -- a scipy sparse matrix (``rosenbrock_problem.jac``) or an ndarray.  Those callables
+are user code on NumPy inputs, so ``HostCallableOps`` evaluates them where they live -- once per
+trial point (res) and once per accepted iterate (jac), exactly the reference's calls -- and moves
+the results to the GPU:
+
+  * the residual vector is uploaded (m doubles), its sum of squares is a device reduction;
+  * each Jacobian is uploaded as CSR (32-bit indices) together with the CSR of its transpose;
+    J v and J^T w then run in ``gnk_csr_spmv`` with scipy's csr_matvec summation order;
+  * the Krylov basis (flat length-n columns), the CGS update, the projected least squares
+    (``gnk_flat_gram`` of [J V P^-1 | r] -> lls.CholQR2Solver) and the Armijo trials run in the
+    HIP library exactly as for Bratu.
+
+Single GPU (a user callable has no row partition); at most 63 basis columns per least-squares
+solve (the flat Gram kernel's four 16-column MFMA blocks).
+"""
+from __future__ import annotations
+
+import math
+
+import numpy as np
+import scipy.sparse
+import torch
+
+from ._device import make_backend
+from .krylow import GeneralizedKrylowSubspaceBreakdown, GeneralizedKrylowSubspaceSpansEntireSpace
+from .lls import CholQR2Solver
+from .slab import Comm
+
+FLAT_GRAM_KMAX = 63
+
+
+class DeviceCSR:
+    """A matrix and its transpose as device CSR arrays (int32 indices, fp64 data)."""
+
+    def __init__(self, be, A):
+        if scipy.sparse.issparse(A):
+            A = A.tocsr()
+        else:
+            A = scipy.sparse.csr_array(np.asarray(A, dtype=np.float64))
+        A = A.astype(np.float64)
+        At = A.T.tocsr()
+        self.shape = A.shape
+        if A.nnz >= 2 ** 31:
+            raise ValueError("Jacobian has too many nonzeros for 32-bit CSR indices")
+        dev = be.device
+        self._arrays = []
+        for M in (A, At):
+            M.sort_indices()
+            self._arrays.append((torch.as_tensor(M.indptr.astype(np.int32), device=dev),
+                                 torch.as_tensor(M.indices.astype(np.int32), device=dev),
+                                 torch.as_tensor(M.data, device=dev)))
+        self.be = be
+
+    def matvec(self, x, y, negate=False):
+        ip, ix, d = self._arrays[0]
+        self.be.csr_spmv(self.shape[0], ip, ix, d, x, y, negate)
+
+    def rmatvec(self, w, y, negate=False):
+        ip, ix, d = self._arrays[1]
+        self.be.csr_spmv(self.shape[1], ip, ix, d, w, y, negate)
+
+
+class FlatKrylovBasis:
+    """ref:krylow.py:16-73 on flat device vectors (same interface as krylow.DeviceKrylovBasis)."""
+
+    FUSE_KMAX = 0          # no fused first trial for generic problems
+
+    def __init__(self, ops, kmax: int):
+        self.ops = ops
+        self.be = ops.be
+        self.kmax = int(kmax)
+        self.V = self.be.zeros(self.kmax, ops.n)
+        self.k = 0
+        self._c = self.be.zeros(self.kmax)
+        self._h = self.be.zeros(self.kmax)
+        self._stats = self.be.zeros(2)
+        self._g = self.be.zeros(ops.n)
+        self._jv = None
+
+    @property
+    def shape(self):
+        return (self.ops.n, self.k)
+
+    def _jnorm(self, u, v) -> float:
+        """||J(u) v|| (the least-squares preconditioner's column scale)."""
+        if self._jv is None:
+            self._jv = self.be.zeros(self.ops.m)
+        self.ops.jvp(u, v, self._jv)
+        self.be.flat_stats(self._jv, self._stats)
+        return math.sqrt(float(self._stats[0].item()))
+
+    def start(self, x, u_jac=None):
+        """ref:krylow.py:30-39 (+ ||J(u_jac) v_0|| when u_jac is given)."""
+        self.be.flat_stats(x, self._stats)
+        sumsq, maxabs = (float(v) for v in self._stats.cpu().numpy())
+        if maxabs <= 1e-8:                                    # np.allclose(x0, 0) (:31)
+            raise ValueError("x0 is not allowed to be 0 in the gauss_newton_krylow algorithm")
+        nrm = math.sqrt(sumsq)                                # :36
+        self.be.flat_div(x, nrm, self.V[0])                   # :37
+        self.k = 1
+        if u_jac is None:
+            return np.array([nrm])
+        return np.array([nrm]), self._jnorm(u_jac, self.V[0])
+
+    def x(self, c: np.ndarray, out):
+        k = len(c)
+        self._c[:k].copy_(self.be.to_device(c))
+        self.be.flat_gemv(self.V, k, self._c, out)
+        return out
+
+    def update(self, u_jac, r, u_next=None, products_ready=False):
+        """ref:krylow.py:55-73 with jac_ev = J(u_jac), res_ev = r; returns ||J(u_next) v_new||."""
+        k = self.k
+        if k == self.ops.n:                                   # :59-60
+            raise GeneralizedKrylowSubspaceSpansEntireSpace
+        if k >= self.kmax:
+            raise RuntimeError("Krylov basis storage exhausted")
+        g = self._g
+        self.ops.vjp(u_jac, r, g, negate=True)                # g = -J^T r (:62)
+        self.be.flat_gemv_t(self.V, k, g, self._h)            # h = V^T g (:64)
+        self.be.flat_cgs_update(self.V, k, self._h, g, self._stats)   # g -= V h (:64)
+        sumsq, maxabs = (float(v) for v in self._stats.cpu().numpy())
+        if maxabs <= 1e-8 and not math.isnan(sumsq):          # :66
+            raise GeneralizedKrylowSubspaceBreakdown(
+                "Normal residual is allready inside generalized Krylow Subspcae, there for gauss newton "
+                "krylow algorithm has to proceed without enlarging the subspace.")
+        nrm = math.sqrt(sumsq)                                # :71
+        self.be.flat_div(g, nrm, self.V[k])
+        self.k = k + 1
+        return self._jnorm(u_jac if u_next is None else u_next, self.V[k])
+
+
+class HostCallableOps:
+    """Problem side of the GNK loop (gauss_newton_krylow.GNKSolver) for user callables."""
+
+    jacobian_is_free = False       # jac(x) is user code: evaluated exactly where the reference does
+    fuse_trial = False
+
+    def __init__(self, res, jac, n: int, args=(), device=None, backend=None):
+        self.be = backend if backend is not None else make_backend(device)
+        self.comm = Comm(single=True)
+        self.backend = self.be         # the attribute lls.CholQR2Solver reads
+        self.dev = None
+        self.res, self.jac, self.args = res, jac, tuple(args)
+        self.n = self.n_global = int(n)
+        self.m = None                  # learnt from the first res / jac evaluation
+        self._J = {}                   # iterate buffer -> DeviceCSR of jac at its value
+        self._W = None
+        self._st = self.be.zeros(2)
+
+    # -- vectors -------------------------------------------------------------------------
+    def load(self, x0):
+        x = np.asarray(x0, dtype=np.float64).reshape(-1)
+        if x.size != self.n:
+            raise ValueError(f"x0 has {x.size} entries, expected {self.n}")
+        return self.be.to_device(x)
+
+    def vec(self):
+        return self.be.zeros(self.n)
+
+    def rvec(self):
+        """A residual buffer; sized by the first res evaluation when m is not known yet."""
+        return self.be.zeros(self.m if self.m is not None else 0)
+
+    def to_host(self, x):
+        return x.detach().cpu().numpy().copy()
+
+    def own(self, x):
+        return x
+
+    # -- problem -------------------------------------------------------------------------
+    def residual(self, x, r) -> float:
+        """r = res(x, *args) (the user's function); returns sum(r^2) (device reduction)."""
+        rh = np.asarray(self.res(self.to_host(x), *self.args), dtype=np.float64).reshape(-1)
+        if self.m is None:
+            self.m = rh.size
+        if r.numel() == 0:
+            r.resize_(rh.size)
+        if rh.size != r.numel():
+            raise ValueError(f"res returned {rh.size} values, expected {r.numel()}")
+        r.copy_(self.be.to_device(rh))
+        self.be.flat_stats(r, self._st)
+        return float(self._st[0].item())
+
+    def on_jacobian(self, u):
+        """jac(u, *args) (the user's function) -> device CSR of J and J^T, kept for u's buffer."""
+        J = DeviceCSR(self.be, self.jac(self.to_host(u), *self.args))
+        if J.shape[1] != self.n:
+            raise ValueError(f"jac returned shape {J.shape}, expected (m, {self.n})")
+        if self.m is None:
+            self.m = J.shape[0]
+        elif J.shape[0] != self.m:
+            raise ValueError(f"jac returned {J.shape[0]} rows, res returned {self.m} values")
+        self._J[u.data_ptr()] = J
+
+    def _jac_of(self, u) -> DeviceCSR:
+        try:
+            return self._J[u.data_ptr()]
+        except KeyError:
+            raise RuntimeError("no Jacobian evaluated at this iterate") from None
+
+    def jvp(self, u, v, out):
+        self._jac_of(u).matvec(v, out)
+
+    def vjp(self, u, w, out, negate=False):
+        self._jac_of(u).rmatvec(w, out, negate)
+
+    def gram(self, u, V, k, rinv, r, G):
+        """Gram of [J(u) V RinvAug | r]: k JVPs into a device W, then gnk_flat_gram."""
+        if k > FLAT_GRAM_KMAX:
+            raise NotImplementedError(f"generic problems: at most {FLAT_GRAM_KMAX} basis columns per "
+                                      "least-squares solve (use krylow_restart)")
+        if self._W is None or self._W.shape[0] < k:
+            self._W = self.be.zeros(max(k, 8), self.m)
+        J = self._jac_of(u)
+        for j in range(k):
+            J.matvec(V[j], self._W[j])
+        self.be.flat_gram(self._W, k, rinv, r, self.m, G)
+
+    # -- solver parts --------------------------------------------------------------------
+    def make_basis(self, kmax):
+        return FlatKrylovBasis(self, kmax)
+
+    def make_lls(self, kmax):
+        return CholQR2Solver(self, kmax, gram=self.gram, n_global=self.n)

@@ -50,9 +50,13 @@ def _cond_upper(R):
 
 
 class CholQR2Solver:
-    def __init__(self, dev, kmax: int):
+    def __init__(self, dev, kmax: int, gram=None, n_global=None):
+        """``gram(u, V, k, rinv, r, G)`` fills G with the Gram of [J(u) V RinvAug | r] (default:
+        the Bratu stencil kernel); ``n_global`` = parameter count (for the sCholQR3 shift)."""
         self.dev = dev
         self.be = dev.backend
+        self._gram_fn = gram if gram is not None else self.be.gram
+        self.n_global = n_global if n_global is not None else dev.slab.n_global
         kp = self.be.gram_dim(kmax, True)
         self._G = self.be.zeros(kp * kp)
         self._rinv = self.be.zeros(kp * kp)
@@ -85,7 +89,7 @@ class CholQR2Solver:
             rinv_dev = self._rinv[:kp * kp]
             rinv_dev.copy_(be.to_device(aug.reshape(-1)))
         G = self._G[:kp * kp]
-        be.gram(u, basis.V, k, rinv_dev, r, G)
+        self._gram_fn(u, basis.V, k, rinv_dev, r, G)
         self.passes += 1
         return self.dev.comm.sum(G).reshape(kp, kp)
 
@@ -116,7 +120,7 @@ class CholQR2Solver:
             try:
                 P = _chol_upper(G1)
             except (np.linalg.LinAlgError, ValueError):
-                n = self.dev.slab.n_global
+                n = self.n_global
                 shift = 11.0 * (n * k + k * (k + 1)) * EPS * np.trace(G1)
                 P = _chol_upper(G1 + shift * np.eye(k))
         for it in range(MAX_PASSES):
@@ -124,7 +128,7 @@ class CholQR2Solver:
             try:
                 Ry = _chol_upper(Gp[:k, :k])
             except (np.linalg.LinAlgError, ValueError):
-                n = self.dev.slab.n_global
+                n = self.n_global
                 shift = 11.0 * (n * k + k * (k + 1)) * EPS * np.trace(Gp[:k, :k])
                 P = _chol_upper(Gp[:k, :k] + shift * np.eye(k)) @ P
                 self.fallbacks += 1

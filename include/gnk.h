@@ -136,6 +136,34 @@ int gnk_cg_update_xr(gnk_ctx* ctx, double alpha, const double* p, const double* 
 /* p = z (first) or p = beta * p + z (owned rows) */
 int gnk_cg_update_p(gnk_ctx* ctx, double beta, int first, const double* z, double* p);
 
+/* ---- generic problems: flat length-n vectors, no gnk_set_bratu needed ------ */
+/* x = V[:, :k] @ c                                                    ref:krylow.py:41-42 */
+int gnk_flat_gemv(gnk_ctx* ctx, const double* V, int64_t ldv, int k, const double* c, double* x, int64_t n);
+/* h = V[:, :k]^T g (deterministic)                                   ref:krylow.py:64 (inner) */
+int gnk_flat_gemv_t(gnk_ctx* ctx, const double* V, int64_t ldv, int k, const double* g, int64_t n, double* h_out);
+/* g -= V[:, :k] @ h ; stats_out = {sum g^2, max|g|}            ref:krylow.py:64, :66, :71 */
+int gnk_flat_cgs_update(gnk_ctx* ctx, const double* V, int64_t ldv, int k, const double* h, double* g, int64_t n,
+                        double* stats_out);
+/* {sum x^2, max |x|}; a . b; dst = src / denom; out = x + (alpha * d) */
+int gnk_flat_stats(gnk_ctx* ctx, const double* x, int64_t n, double* stats_out);
+int gnk_flat_dot(gnk_ctx* ctx, const double* a, const double* b, int64_t n, double* out);
+int gnk_flat_div(gnk_ctx* ctx, const double* src, double denom, double* dst, int64_t n);
+int gnk_flat_axpy(gnk_ctx* ctx, const double* x, double alpha, const double* d, double* out, int64_t n);
+/* CG vector updates on flat vectors (as gnk_cg_update_xr / gnk_cg_update_p) */
+int gnk_flat_cg_update_xr(gnk_ctx* ctx, double alpha, const double* p, const double* q, double* x, double* r,
+                          const double* dinv, double* z, int64_t n, double* out);
+int gnk_flat_cg_update_p(gnk_ctx* ctx, double beta, int first, const double* z, double* p, int64_t n);
+/* y = A x (negate != 0: y = -(A x)), CSR with 32-bit indices, scipy csr_matvec summation order:
+ * the J @ v / J.T @ w of a user Jacobian (J.T as the CSR of the transpose)
+ *                                                  ref:krylow.py:62, gauss_newton_krylow.py:86 */
+int gnk_csr_spmv(gnk_ctx* ctx, int64_t nrows, const int* indptr, const int* indices, const double* data,
+                 const double* x, double* y, int negate);
+/* Gram of [W @ RinvAug | r] for a materialised W (k <= 63 columns of length m, stride ldw),
+ * G_out kp x kp (kp = gnk_gram_padded_dim(k, r != NULL)); rinv NULL = identity
+ *                                                       ref:gauss_newton_krylow.py:16-36, 86-89 */
+int gnk_flat_gram(gnk_ctx* ctx, const double* W, int64_t ldw, int k, const double* rinv, int64_t ldr,
+                  const double* r, int64_t m, double* G_out);
+
 /* ---- tooling (not on the solver path) ----------------------------------- */
 /* Per-launch HIP-event timer for one kernel class (bench roofline): after
  * gnk_timer_start, the next `capacity` launches of that kernel are bracketed by

@@ -432,6 +432,20 @@ def gauss_newton(res, x0, jac, args=(), tol=1e-8, max_iter=100, step_length_cont
     return RegressionResult("gauss newton", x, success, nfev, njev, it)
 
 
+def rosenbrock(p):
+    """ref:rosenbrock_problem.py:8-19 -- the sparse Rosenbrock chain with parameter_count = p
+    (m = 2(p - 1) residuals); returns (res, jac) as the reference module's functions."""
+    def res(x):
+        return 2 ** 0.5 * np.concatenate([10 * (x[1:] - x[:-1] ** 2), 1 - x[:-1]])
+
+    def jac(x):
+        b1 = 10 * scipy.sparse.eye(p - 1, p, k=1) - 20 * scipy.sparse.diags(x[:-1], shape=(p - 1, p))
+        b2 = -scipy.sparse.eye(p - 1, p, k=0)
+        return 2 ** 0.5 * scipy.sparse.block_array([[b1], [b2]])
+
+    return res, jac
+
+
 def bratu_workload(N, alpha=5.0, lam=10.0, seed=42, grid_resolution=None, linear_u0=False):
     """Synthetic Bratu inputs of ref:bratu_pde_test.py:22-36 (and :196-219 when linear_u0)."""
     prob = BratuPdeProblem(N + 1, alpha, lam, grid_resolution=grid_resolution)

@@ -9,6 +9,7 @@ imports it; tests inject it through the private ``_backend`` argument.
 from __future__ import annotations
 
 import numpy as np
+import scipy.sparse
 import torch
 
 GHOST = 2
@@ -149,6 +150,63 @@ class NumpyBackend:
     def gemv(self, V, k, c, x):
         Vn = V.numpy()[:k]
         x.numpy()[:] = np.asarray(c.numpy()[:k]) @ Vn
+
+    # -- flat vectors (generic problems) --------------------------------------------------
+    def flat_gemv(self, V, k, c, x):
+        x.numpy()[:] = np.asarray(c.numpy()[:k]) @ V.numpy()[:k]
+
+    def flat_gemv_t(self, V, k, g, h):
+        h.numpy()[:k] = V.numpy()[:k] @ g.numpy()
+
+    def flat_cgs_update(self, V, k, h, g, stats):
+        G = g.numpy()
+        G -= h.numpy()[:k] @ V.numpy()[:k]
+        stats[0] = float(np.sum(G * G))
+        stats[1] = float(np.max(np.abs(G)))
+
+    def flat_stats(self, x, stats):
+        o = x.numpy()
+        stats[0] = float(np.sum(o * o))
+        stats[1] = float(np.max(np.abs(o)))
+
+    def flat_dot(self, a, b, out):
+        out[0] = float(np.dot(a.numpy(), b.numpy()))
+
+    def flat_div(self, src, denom, dst):
+        dst.numpy()[:] = src.numpy() / denom
+
+    def flat_axpy(self, x, alpha, d, out):
+        out.numpy()[:] = x.numpy() + alpha * d.numpy()
+
+    def flat_cg_update_xr(self, alpha, p, q, x, r, dinv, z, out):
+        X, R = x.numpy(), r.numpy()
+        X[:] = X + alpha * p.numpy()
+        R[:] = R - alpha * q.numpy()
+        Z = R if dinv is None else 0.0 + dinv.numpy() * R
+        if dinv is not None:
+            z.numpy()[:] = Z
+        out[0] = float(np.dot(R, R))
+        out[1] = float(np.dot(R, Z))
+
+    def flat_cg_update_p(self, beta, first, z, p):
+        P = p.numpy()
+        P[:] = z.numpy() if first else P * beta + z.numpy()
+
+    def csr_spmv(self, nrows, indptr, indices, data, x, y, negate=False):
+        A = scipy.sparse.csr_array((data.numpy(), indices.numpy(), indptr.numpy()),
+                                   shape=(int(nrows), x.numel()))
+        v = A @ x.numpy()
+        y.numpy()[:] = -v if negate else v
+
+    def flat_gram(self, W, k, rinv, r, m, G):
+        kp = self.gram_dim(k, r is not None)
+        Wa = np.zeros((int(m), kp))
+        Wa[:, :k] = W.numpy()[:k].T
+        if r is not None:
+            Wa[:, k] = r.numpy()
+        if rinv is not None:
+            Wa = Wa @ rinv.numpy().reshape(kp, kp)
+        G.numpy()[:] = (Wa.T @ Wa).reshape(-1)
 
     def gemv_vjp_gemv_t(self, V, k, c, r, x, g, h):
         self.gemv(V, k, c, x)

@@ -1,0 +1,138 @@
+"""Generic problems on the GPU: the flat-vector kernels, the CSR SpMV and the
+flat Gram against NumPy, then gauss_newton_krylow with the reference's Rosenbrock callables
+against the golden runs (stdout / bookkeeping exact; ||x_k|| within 1e-10 for p = 2, 1e-9 for
+p = 1000 -- the reductions sum in a different order than NumPy)."""
+import numpy as np
+import pytest
+import scipy.sparse
+import torch
+
+pytestmark = pytest.mark.gpu
+
+import gauss_newton_via_generalized_krylov_subspaces_amd as gnk  # noqa: E402
+from gauss_newton_via_generalized_krylov_subspaces_amd._device import make_backend  # noqa: E402
+from gauss_newton_via_generalized_krylov_subspaces_amd.generic import DeviceCSR  # noqa: E402
+from oracle import gnk_oracle as O  # noqa: E402
+from tests.test_generic_host import rosen_x0  # noqa: E402
+from tests.test_oracle_golden import _check, _run  # noqa: E402
+
+
+@pytest.fixture(scope="module")
+def be():
+    return make_backend()
+
+
+@pytest.mark.parametrize("n,k", [(1, 1), (2, 2), (999, 7), (1000, 48), (100003, 20)])
+def test_flat_basis_ops(be, n, k):
+    rng = np.random.default_rng(n + k)
+    Vh = rng.standard_normal((k, n))
+    V = be.to_device(Vh)
+    c = rng.standard_normal(k)
+    x = be.zeros(n)
+    be.flat_gemv(V, k, be.to_device(c), x)
+    np.testing.assert_allclose(x.cpu().numpy(), c @ Vh, rtol=1e-13, atol=1e-13 * np.abs(Vh).sum(0).max())
+    g = rng.standard_normal(n)
+    h = be.zeros(k)
+    be.flat_gemv_t(V, k, be.to_device(g), h)
+    np.testing.assert_allclose(h.cpu().numpy(), Vh @ g, rtol=1e-12, atol=1e-12 * np.abs(g).sum())
+    gd = be.to_device(g)
+    st = be.zeros(2)
+    be.flat_cgs_update(V, k, h, gd, st)
+    g2 = g - h.cpu().numpy() @ Vh
+    np.testing.assert_allclose(gd.cpu().numpy(), g2, rtol=1e-12, atol=1e-12 * np.abs(Vh).max() * np.abs(h.cpu().numpy()).sum())
+    np.testing.assert_allclose(st[0].item(), np.sum(gd.cpu().numpy() ** 2), rtol=1e-12)
+    assert st[1].item() == np.abs(gd.cpu().numpy()).max()
+    out = be.zeros(1)
+    be.flat_dot(gd, gd, out)
+    np.testing.assert_allclose(out.item(), st[0].item(), rtol=1e-12)
+    d = be.zeros(n)
+    be.flat_div(gd, 3.0, d)
+    np.testing.assert_array_equal(d.cpu().numpy(), gd.cpu().numpy() / 3.0)
+    be.flat_axpy(gd, 0.25, d, d)
+    np.testing.assert_array_equal(d.cpu().numpy(), gd.cpu().numpy() + 0.25 * (gd.cpu().numpy() / 3.0))
+
+
+@pytest.mark.parametrize("p", [2, 1000])
+def test_csr_spmv_matches_scipy_bitwise(be, p):
+    """J @ v and J.T @ w (CSR of the transpose) in scipy's summation order, bit for bit."""
+    res, jac = O.rosenbrock(p)
+    rng = np.random.default_rng(p)
+    x = rng.standard_normal(p)
+    J = jac(x)
+    v, w = rng.standard_normal(p), rng.standard_normal(J.shape[0])
+    A = DeviceCSR(be, J)
+    y, z = be.zeros(J.shape[0]), be.zeros(p)
+    A.matvec(be.to_device(v), y)
+    A.rmatvec(be.to_device(w), z, negate=True)
+    np.testing.assert_array_equal(y.cpu().numpy(), J @ v)
+    np.testing.assert_array_equal(z.cpu().numpy(), -(J.T @ w))
+
+
+@pytest.mark.parametrize("m,k,with_r,with_rinv", [(2, 1, True, False), (1998, 48, True, True), (1998, 15, False, True),
+                                                  (5000, 33, True, False), (17, 63, False, False)])
+def test_flat_gram(be, m, k, with_r, with_rinv):
+    rng = np.random.default_rng(m + k)
+    W = rng.standard_normal((k, m))
+    r = rng.standard_normal(m)
+    kp = be.gram_dim(k, with_r)
+    Wa = np.zeros((m, kp))
+    Wa[:, :k] = W.T
+    if with_r:
+        Wa[:, k] = r
+    rinv = None
+    if with_rinv:
+        K1 = k + (1 if with_r else 0)
+        A = np.zeros((kp, kp))
+        A[:K1, :K1] = np.triu(rng.standard_normal((K1, K1))) + 3 * np.eye(K1)
+        if with_r:
+            A[k, :] = 0
+            A[:, k] = 0
+            A[k, k] = 1.0
+        rinv = A
+        Wa = Wa @ A
+    Gref = Wa.T @ Wa
+    G = be.zeros(kp * kp)
+    be.flat_gram(be.to_device(W), k, None if rinv is None else be.to_device(rinv.reshape(-1)),
+                 be.to_device(r) if with_r else None, m, G)
+    Gd = G.cpu().numpy().reshape(kp, kp)
+    scale = np.sqrt(np.outer(np.diag(Gref), np.diag(Gref))) + 1e-300
+    assert np.max(np.abs(Gd - Gref) / scale) < 1e-13
+    np.testing.assert_array_equal(Gd, Gd.T)
+
+
+@pytest.mark.parametrize("p,x0name", [(2, "m1_1"), (2, "2_2"), (1000, "i"), (1000, "ii"), (1000, "iii")])
+@pytest.mark.parametrize("version", ["res_old", "res_new"])
+def test_gpu_generic_gnk_rosenbrock(golden, p, x0name, version):
+    meta, arr = golden
+    res, jac = O.rosenbrock(p)
+    x0 = rosen_x0(arr, p, x0name)
+    out, rec, so, exc = _run(gnk.gauss_newton_krylow, res, x0, jac, version=version)
+    name = f"rosen{p}_{x0name}_{version}"
+    _check(meta["cases"][name], out, rec, so, exc, rtol=1e-10 if p == 2 else 1e-9)
+    if p == 2:
+        np.testing.assert_allclose(out.x, arr[name + "__x"], rtol=1e-10, atol=1e-14)
+
+
+def test_gpu_generic_bratu_csr_matches_matrix_free():
+    """The generic path on reference-style CSR Bratu closures (J assembled as
+    -(L + ALPHA D_x + LAMBDA diag e^u), ref:bratu_pde_problem.py:88-96) reproduces the matrix-free
+    Bratu path: bookkeeping exact, ||x_k|| within 1e-10 (N = 24, 30 iterations)."""
+    prob, y, u0 = O.bratu_workload(24)
+    p2 = gnk.BratuPdeProblem(25, 5, 10)
+    lin = (p2.laplace2d + p2.ALPHA * p2.partial_diff_x).tocsr()
+
+    def csr_jac(u):
+        return -1 * (lin + p2.LAMBDA * scipy.sparse.diags(np.exp(u)))
+
+    traj = {}
+    for kind in ("generic", "bratu"):
+        xs = []
+        if kind == "generic":
+            res, jac = prob.make_res(y), csr_jac
+        else:
+            res, jac = p2.make_res(y), p2.make_jac()
+        r = gnk.gauss_newton_krylow(res, u0, jac, max_iter=30, krylow_restart=None,
+                                    callback=lambda x, nfev, cg_iter: xs.append(np.linalg.norm(x)))
+        traj[kind] = (r.nit, r.nrev, r.njev, np.array(xs))
+    assert traj["generic"][:3] == traj["bratu"][:3]
+    np.testing.assert_allclose(traj["generic"][3], traj["bratu"][3], rtol=1e-10)

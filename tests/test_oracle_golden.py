@@ -16,16 +16,7 @@ from oracle import gnk_oracle as O
 RTOL = 1e-10
 
 
-def _rosen(p):
-    def res(x):
-        return 2 ** 0.5 * np.concatenate([10 * (x[1:] - x[:-1] ** 2), 1 - x[:-1]])
-
-    def jac(x):
-        b1 = 10 * scipy.sparse.eye(p - 1, p, k=1) - 20 * scipy.sparse.diags(x[:-1], shape=(p - 1, p))
-        b2 = -scipy.sparse.eye(p - 1, p, k=0)
-        return 2 ** 0.5 * scipy.sparse.block_array([[b1], [b2]])
-
-    return res, jac
+_rosen = O.rosenbrock
 
 
 def _run(method, res, x0, jac, **kw):
