@@ -12,6 +12,7 @@ from __future__ import annotations
 import ctypes
 import os
 
+import numpy as np
 import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
@@ -154,6 +155,34 @@ class HipBackend:
     def to_device(self, a):
         return torch.as_tensor(a, dtype=torch.float64).to(self.device)
 
+    _PIN_SLOTS, _PIN_LEN = 16, 64 * 64
+
+    def upload(self, dst, a):
+        """dst[:len(a)] = a for a small host array, without stalling the host: through a ring of
+        pinned staging buffers and a stream-ordered copy (a pageable copy would wait for the
+        queue to drain).  Each slot is reused only after its previous copy completed."""
+        a = np.asarray(a, dtype=np.float64).reshape(-1)
+        n = a.size
+        if n > self._PIN_LEN:
+            dst[:n].copy_(self.to_device(a))
+            return dst
+        if not hasattr(self, "_pin"):
+            self._pin = [torch.empty(self._PIN_LEN, dtype=torch.float64, pin_memory=True)
+                         for _ in range(self._PIN_SLOTS)]
+            self._pin_ev = [None] * self._PIN_SLOTS
+            self._pin_i = 0
+        i = self._pin_i
+        self._pin_i = (i + 1) % self._PIN_SLOTS
+        if self._pin_ev[i] is not None:
+            self._pin_ev[i].synchronize()
+        buf = self._pin[i]
+        buf.numpy()[:n] = a
+        dst[:n].copy_(buf[:n], non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(self.device))
+        self._pin_ev[i] = ev
+        return dst
+
     # --- operator ----------------------------------------------------------------
     def jvp(self, u, v, out):
         self._call("gnk_bratu_jvp", _p(u), _p(v), _p(out))
@@ -213,8 +242,9 @@ class HipBackend:
     def flat_cg_update_p(self, beta, first, z, p):
         self._call("gnk_flat_cg_update_p", float(beta), int(bool(first)), _p(z), _p(p), p.numel())
 
-    def csr_spmv(self, nrows, indptr, indices, data, x, y, negate=False):
-        self._call("gnk_csr_spmv", int(nrows), _p(indptr), _p(indices), _p(data), _p(x), _p(y), int(bool(negate)))
+    def csr_spmv(self, nrows, indptr, indices, data, x, y, negate=False, reciprocal=False):
+        mode = 2 if reciprocal else (1 if negate else 0)
+        self._call("gnk_csr_spmv", int(nrows), _p(indptr), _p(indices), _p(data), _p(x), _p(y), mode)
 
     def flat_gram(self, W, k, rinv, r, m, G):
         kp = self.gram_dim(k, r is not None)

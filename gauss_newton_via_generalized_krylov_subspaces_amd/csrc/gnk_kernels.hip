@@ -1612,15 +1612,17 @@ __global__ __launch_bounds__(BLOCK) void k_gemv_t(const double* __restrict__ V, 
   block_sum_store<KCT>(acc, kc, partial + (size_t(blockIdx.z) * nblk + blockIdx.y * gridDim.x + blockIdx.x) * KCT, sh);
 }
 
-// y = A x (neg: y = -(A x)) for a CSR matrix with 32-bit indices; one thread per row, entries in
-// stored order from 0 -- scipy's csr_matvec rounding (compiled without FMA contraction)
+// y = A x for a CSR matrix with 32-bit indices; one thread per row, entries in stored order from
+// 0 -- scipy's csr_matvec rounding (compiled without FMA contraction).  mode 1: y = -(A x)
+// (= (-A) x exactly), mode 2: y = 1 / (A x) (the Jacobi vector 1 / diag(A^T A) from the squared
+// entries of A^T and x = 1, summed in the k-ascending order of scipy's csr_matmat)
 __global__ __launch_bounds__(BLOCK) void k_csr_spmv(int64_t nrows, const int* __restrict__ indptr,
                                                     const int* __restrict__ indices, const double* __restrict__ data,
-                                                    const double* __restrict__ x, double* __restrict__ y, int neg) {
+                                                    const double* __restrict__ x, double* __restrict__ y, int mode) {
   for (int64_t i = int64_t(blockIdx.x) * BLOCK + threadIdx.x; i < nrows; i += int64_t(gridDim.x) * BLOCK) {
     double s = 0.0;
     for (int jj = indptr[i]; jj < indptr[i + 1]; ++jj) s = s + data[jj] * x[indices[jj]];
-    y[i] = neg ? -s : s;
+    y[i] = mode == 1 ? -s : (mode == 2 ? 1.0 / s : s);
   }
 }
 
@@ -2485,12 +2487,13 @@ int gnk_flat_cg_update_p(gnk_ctx* ctx, double beta, int first, const double* z, 
 }
 
 int gnk_csr_spmv(gnk_ctx* ctx, int64_t nrows, const int* indptr, const int* indices, const double* data,
-                 const double* x, double* y, int negate) {
+                 const double* x, double* y, int mode) {
   if (!ctx_ok(ctx)) return -1;
   if (nrows < 1 || !indptr || !x || !y) return fail(ctx, "csr_spmv: bad arguments");
   const int64_t nb = std::min<int64_t>((nrows + BLOCK - 1) / BLOCK, 1 << 20);
+  if (mode < 0 || mode > 2) return fail(ctx, "csr_spmv: mode must be 0, 1 or 2");
   hipLaunchKernelGGL(k_csr_spmv, dim3(unsigned(nb)), dim3(BLOCK), 0, ctx->stream, nrows, indptr, indices, data, x, y,
-                     negate);
+                     mode);
   return check_launch(ctx, "csr_spmv");
 }
 

@@ -1,5 +1,11 @@
 """Classical Gauss-Newton with the CGLS inner solve on MI355X (ref:gauss_newton.py:11-138).
 
+Problems: the matrix-free Bratu problem of this package (``BratuGNOps``: slab vectors, fused
+stencils, multi-GPU) or any ``res`` / ``jac`` callables (``generic.HostCallableOps``: J uploaded as
+CSR per iteration, J v / J^T w / the Jacobi vector in ``gnk_csr_spmv``, flat vector kernels).
+Dense-ndarray Jacobians take the reference's ``lstsq`` branch there, which is out of scope (f4):
+the generic GN path raises NotImplementedError for them (GNK accepts dense Jacobians).
+
 ``cg_least_squares`` restates scipy 1.15.3 ``scipy.sparse.linalg.cg``
 (iterative.py:305-422: x0 = 0, atol = rtol * ||b||, strict ``<`` test before
 each iteration, ``maxiter = 10 n``) on the normal equations A^T A x = A^T y with
@@ -28,29 +34,104 @@ from .regression_result import RegressionResult
 from .slab import Comm
 
 
-class DeviceCG:
-    """Device state of the CGLS solve for one rank."""
+class BratuGNOps:
+    """Problem side of GN / CGLS for the matrix-free Bratu problem (slab vectors on this rank):
+    the fused 13-point J^T J p stencil, the closed-form diag(J^T J), halos of p."""
 
-    def __init__(self, dev: BratuDevice):
-        self.dev = dev
-        self.be = dev.backend
-        v = dev.vec
+    jacobian_is_free = True
+
+    def __init__(self, problem, y=None, comm=None, device=None, backend=None):
+        self.dev = BratuDevice(problem, comm, device, backend)
+        self.be = self.dev.backend
+        self.comm = self.dev.comm
+        self.n_global = self.dev.slab.n_global
+        self.y = None if y is None else self.dev.load(y)
+        self._s1 = self.dev.scalar(1)
+        self._s2 = self.dev.scalar(2)
+        self.dvec = self.dev.vec()
+        self._jd = None
+
+    def vec(self):
+        return self.dev.vec()
+
+    rvec = vec
+
+    def load(self, x0):
+        return self.dev.load(x0)
+
+    def residual(self, x, r) -> float:
+        self.be.residual(x, self.y, r, self._s1)
+        return float(self.comm.sum(self._s1)[0])
+
+    def to_host(self, x):
+        return self.dev.slab.to_host(x)
+
+    def own(self, x):
+        return x[self.dev.slab.own]
+
+    def on_jacobian(self, u):
+        pass
+
+    def jvp_sumsq(self, u, d) -> float:
+        if self._jd is None:
+            self._jd = self.dev.vec()
+        self.be.jvp(u, d, self._jd)                                  # jac_ev @ d (ref:armijo_goldstein.py:50)
+        return self.sumsq(self._jd)
+
+    def axpy(self, x, t, d, out):
+        self.be.vec_axpy(x, t, d, out, True)                         # x + t d (whole slab)
+
+    def sumsq(self, v) -> float:
+        self.be.vec_stats(v, self._s2)
+        s, _ = self.comm.sum_max(self._s2)
+        return s
+
+    # CG pieces
+    def cg_rhs(self, u, y, b):
+        self.be.vjp_gemv_t(u, y, None, 0, b, None)                   # b = A.T @ y = -(J.T y)
+
+    def cg_prepare(self, u):
+        self.be.jdiag(u, self.dvec)                                  # J's diagonal, fixed during CG
+
+    def cg_jacobi(self, u, dinv):
+        self.be.diag_jtj(u, dinv, reciprocal=True)                   # ref:gauss_newton.py:50-54
+
+    def cg_normal_matvec(self, p, q) -> float:
+        sl = self.dev.slab
+        self.comm.halo(p, sl.N, sl.nrows)
+        self.be.cg_matvec(self.dvec, p, q, self._s1)
+        return float(self.comm.sum(self._s1)[0])
+
+    def cg_update_xr(self, alpha, p, q, x, r, dinv, z):
+        self.be.cg_update_xr(alpha, p, q, x, r, dinv, z, self._s2)
+        rr, rz = self.comm.sum(self._s2)
+        return float(rr), float(rz)
+
+    def cg_update_p(self, beta, first, z, p):
+        self.be.cg_update_p(beta, first, z, p)
+
+    def cg_finish(self, x):
+        sl = self.dev.slab
+        self.comm.halo(x, sl.N, sl.nrows)
+
+
+class DeviceCG:
+    """Device state of the CGLS solve (one rank of a Bratu slab, or a generic problem)."""
+
+    def __init__(self, ops):
+        if isinstance(ops, BratuDevice):                              # legacy: a BratuDevice
+            ops = BratuGNOps(ops.problem, None, ops.comm, backend=ops.backend)
+        self.ops = ops
+        v = ops.vec
         self.b, self.x, self.r, self.z, self.p, self.q = v(), v(), v(), v(), v(), v()
-        self.dvec, self.dinv = v(), v()
-        self._s2 = dev.scalar(2)
-        self._s1 = dev.scalar(1)
+        self.dinv = v()
         self.total_iters = 0
 
-    def _sum2(self):
-        return self.dev.comm.sum(self._s2)
-
     def solve(self, u, y, cg_rtol=1e-4, preconditioner=True, callback=None):
-        """x = argmin ||y - A x||, A = -J(u); returns (x slab, cg_iter) like ref:gauss_newton.py:11-60.
-        ``u`` and ``y`` are slab vectors (u valid on owned +-2 rows, y on owned +-1 rows)."""
-        be, dev = self.be, self.dev
-        sl = dev.slab
-        be.vjp_gemv_t(u, y, None, 0, self.b, None)                 # b = A.T @ y = -(J.T y)
-        be.jdiag(u, self.dvec)                                     # J's diagonal, fixed during CG
+        """x = argmin ||y - A x||, A = -J(u); returns (x, cg_iter) like ref:gauss_newton.py:11-60."""
+        ops = self.ops
+        ops.cg_rhs(u, y, self.b)                                    # b = A.T @ y
+        ops.cg_prepare(u)
         count = [0]
 
         def cb():
@@ -60,31 +141,27 @@ class DeviceCG:
 
         if not preconditioner:
             self._cg(cg_rtol, None, cb)                            # ref:gauss_newton.py:45-48
-        be.diag_jtj(u, self.dinv, reciprocal=True)                 # ref:gauss_newton.py:50-54
+        ops.cg_jacobi(u, self.dinv)                                # ref:gauss_newton.py:50-54
         self._cg(cg_rtol, self.dinv, cb)                           # :56-58
         self.total_iters += count[0]
-        dev.comm.halo(self.x, sl.N, sl.nrows)
+        ops.cg_finish(self.x)
         return self.x, count[0]
 
     def _cg(self, rtol, dinv, cb):
         """scipy iterative.py:305-422 with x0 = 0, atol = 0."""
-        be, dev, sl = self.be, self.dev, self.dev.slab
-        be.vec_stats(self.b, self._s2)
-        bb, _ = dev.comm.sum_max(self._s2)
-        bnrm2 = math.sqrt(bb)
+        ops = self.ops
+        bnrm2 = math.sqrt(ops.sumsq(self.b))
         atol = max(0.0, float(rtol) * float(bnrm2))
         self.x.zero_()
         if bnrm2 == 0:
             self.x.copy_(self.b)
             return 0
-        n = sl.n_global
-        maxiter = n * 10
+        maxiter = ops.n_global * 10
         self.r.copy_(self.b)
         self.p.zero_()
         self.q.zero_()
         # z = M r and (r.r, r.z) via the update kernel with alpha = 0 (x, r unchanged)
-        be.cg_update_xr(0.0, self.p, self.q, self.x, self.r, dinv, self.z, self._s2)
-        rr, rz = self._sum2()
+        rr, rz = ops.cg_update_xr(0.0, self.p, self.q, self.x, self.r, dinv, self.z)
         z = self.z if dinv is not None else self.r
         rho_prev = None
         for iteration in range(maxiter):
@@ -92,15 +169,12 @@ class DeviceCG:
                 return iteration
             rho = rz
             if iteration > 0:
-                be.cg_update_p(rho / rho_prev, False, z, self.p)
+                ops.cg_update_p(rho / rho_prev, False, z, self.p)
             else:
-                be.cg_update_p(0.0, True, z, self.p)
-            dev.comm.halo(self.p, sl.N, sl.nrows)
-            be.cg_matvec(self.dvec, self.p, self.q, self._s1)
-            pq = float(dev.comm.sum(self._s1)[0])
+                ops.cg_update_p(0.0, True, z, self.p)
+            pq = ops.cg_normal_matvec(self.p, self.q)
             alpha = rho / pq
-            be.cg_update_xr(alpha, self.p, self.q, self.x, self.r, dinv, self.z, self._s2)
-            rr, rz = self._sum2()
+            rr, rz = ops.cg_update_xr(alpha, self.p, self.q, self.x, self.r, dinv, self.z)
             rho_prev = rho
             cb()
         return maxiter
@@ -114,12 +188,12 @@ def cg_least_squares(A, y, x0=None, cg_rtol=1e-4, preconditioner=True):
         raise NotImplementedError("x0 != None is not used by the reference (ref:gauss_newton.py:112-114)")
     if not isinstance(A, BratuJacobian) or A.sign != -1.0:
         raise TypeError("cg_least_squares on MI355X expects A = -1 * jac(u) from BratuPdeProblem.make_jac()")
-    dev = BratuDevice(A.problem, Comm(single=True))
-    cg = DeviceCG(dev)
-    u = dev.load(A.u if not torch.is_tensor(A.u) else A.u.cpu().numpy())
-    ys = dev.load(y)
+    ops = BratuGNOps(A.problem, None, Comm(single=True))
+    cg = DeviceCG(ops)
+    u = ops.load(A.u if not torch.is_tensor(A.u) else A.u.cpu().numpy())
+    ys = ops.load(y)
     x, it = cg.solve(u, ys, cg_rtol=cg_rtol, preconditioner=preconditioner)
-    return dev.slab.to_host(x), it
+    return ops.to_host(x), it
 
 
 class GNSolver:
@@ -127,29 +201,27 @@ class GNSolver:
 
     def __init__(self, problem, y, tol=1e-8, max_iter=100, cg_preconditioner=False, cg_rtol=1e-4,
                  comm: Optional[Comm] = None, device=None, backend=None, callback: Callable = None,
-                 callback_format="numpy"):
-        self.dev = BratuDevice(problem, comm, device, backend)
-        self.be = self.dev.backend
-        self.comm = self.dev.comm
+                 callback_format="numpy", ops=None):
+        self.ops = ops if ops is not None else BratuGNOps(problem, y, comm, device, backend)
+        self.dev = getattr(self.ops, "dev", None)
+        self.be = self.ops.be
+        self.comm = self.ops.comm
         self.tol, self.max_iter = tol, int(max_iter)
         self.cg_pre, self.cg_rtol = cg_preconditioner, cg_rtol
         self.callback, self.callback_format = callback, callback_format
-        self.y = self.dev.load(y)
-        self.cg = DeviceCG(self.dev)
-        self.xb = [self.dev.vec(), self.dev.vec()]
-        self.rb = [self.dev.vec(), self.dev.vec()]
-        self.jd = self.dev.vec()
-        self._s1 = self.dev.scalar(1)
-        self._s2 = self.dev.scalar(2)
+        self.cg = DeviceCG(self.ops)
+        self.xb = [self.ops.vec(), self.ops.vec()]
+        self.rb = None
         self.trace = []
 
     def _residual(self, x, r):
-        self.be.residual(x, self.y, r, self._s1)
-        return float(self.comm.sum(self._s1)[0])
+        return self.ops.residual(x, r)
 
     def setup(self, x0):
         self.xi, self.ri = 0, 0
-        self.xb[0].copy_(self.dev.load(x0))                          # x = x0.copy() (:95)
+        self.xb[0].copy_(self.ops.load(x0))                          # x = x0.copy() (:95)
+        if self.rb is None:
+            self.rb = [self.ops.rvec(), self.ops.rvec()]
         self.rr = self._residual(self.xb[0], self.rb[0])             # :100
         self.nfev, self.njev = 1, 0
         self.cg_iter = None
@@ -161,34 +233,31 @@ class GNSolver:
 
     def step(self):
         it = self.iter + 1
-        sl = self.dev.slab
+        ops = self.ops
         x, r = self.xb[self.xi], self.rb[self.ri]
-        self.njev += 1                                               # :107-108
+        ops.on_jacobian(x)                                           # J = jac(x) (:107)
+        self.njev += 1                                               # :108
         d, self.cg_iter = self.cg.solve(x, r, cg_rtol=self.cg_rtol, preconditioner=self.cg_pre)   # :111-114
-        self.be.jvp(x, d, self.jd)                                   # jac_ev @ d (ref:armijo_goldstein.py:50)
-        self.be.vec_stats(self.jd, self._s2)
-        jdd, _ = self.comm.sum_max(self._s2)
+        jdd = ops.jvp_sumsq(x, d)                                    # sum((J d)^2) (ref:armijo_goldstein.py:50)
         xt, rt = self.xb[1 - self.xi], self.rb[1 - self.ri]
         last = {}
 
         def trial(t):
-            self.be.vec_axpy(x, t, d, xt, True)                      # x + t d (whole slab)
+            ops.axpy(x, t, d, xt)                                    # x + t d
             last["rr"] = self._residual(xt, rt)
             return last["rr"]
 
         t, ntrial = armijo_device(trial, self.rr, jdd, d_norm_host(self, d))
         self.nfev += ntrial
-        self.be.vec_stats(x, self._s2)
-        s, _ = self.comm.sum_max(self._s2)                          # np.sum(x**2) (:123)
-        self.be.vec_stats(d, self._s2)
-        dd, _ = self.comm.sum_max(self._s2)
+        s = ops.sumsq(x)                                             # np.sum(x**2) (:123)
+        dd = ops.sumsq(d)
         self.xi, self.ri = 1 - self.xi, 1 - self.ri                  # x += t d (:125) == trial point
         self.rr = last["rr"]
         self.iter = it
         self.trace.append({"t": t, "trials": ntrial, "cg_iter": self.cg_iter})
         if self.callback is not None:
             xs = self.xb[self.xi]
-            xo = xs[sl.own] if self.callback_format == "torch" else sl.to_host(xs)
+            xo = ops.own(xs) if self.callback_format == "torch" else ops.to_host(xs)
             self.callback(x=xo, nfev=self.nfev, cg_iter=self.cg_iter)
         if t ** 2 * dd <= self.tol ** 2 * s:                         # :129-131
             self.success = True
@@ -201,7 +270,7 @@ class GNSolver:
         if not self.success:
             print("Warning: The gauss_newton algorithm reached maximal iteration bound before terminating!")
         xs = self.xb[self.xi]
-        x = xs[self.dev.slab.own].clone() if result_format == "torch" else self.dev.slab.to_host(xs)
+        x = self.ops.own(xs).clone() if result_format == "torch" else self.ops.to_host(xs)
         return RegressionResult("gauss newton", x, self.success, self.nfev, self.njev, self.iter)
 
 
@@ -212,10 +281,7 @@ class _DNorm:
         self.solver, self.d = solver, d
 
     def __array__(self, dtype=None, copy=None):
-        be = self.solver.be
-        be.vec_stats(self.d, self.solver._s2)
-        s, _ = self.solver.comm.sum_max(self.solver._s2)
-        return np.array([math.sqrt(s)])
+        return np.array([math.sqrt(self.solver.ops.sumsq(self.d))])
 
 
 def d_norm_host(solver, d):
@@ -227,14 +293,23 @@ def gauss_newton(res, x0, jac, args: tuple = (), tol: float = 1e-8, max_iter=100
                  comm: Optional[Comm] = None, device=None, callback_format: str = "numpy",
                  result_format: str = "numpy", _backend=None) -> RegressionResult:
     """Drop-in for ref:gauss_newton.py:63-138 (sparse-Jacobian / CGLS branch); ``cg_rtol`` added."""
-    problem, y = resolve_bratu(res, jac)
-    if args:
-        raise TypeError("<lambda>() takes 1 positional argument but {} were given".format(1 + len(args)))
+    bratu = resolve_bratu(res, jac)
     if step_length_control is not None:
         raise NotImplementedError("the device solver uses the reference's armijo_goldstein rule")
     cb = None if (callback is None or callback is _noop) else callback
+    if bratu is not None:
+        if args:
+            raise TypeError("<lambda>() takes 1 positional argument but {} were given".format(1 + len(args)))
+        problem, y = bratu
+        ops = None
+    else:
+        from .generic import HostCallableOps
+        problem, y = None, None
+        x0h = x0.detach().cpu().numpy() if torch.is_tensor(x0) else np.asarray(x0, dtype=np.float64)
+        ops = HostCallableOps(res, jac, x0h.size, args, device=device, backend=_backend, dense_jacobian=False)
     solver = GNSolver(problem, y, tol=tol, max_iter=max_iter, cg_preconditioner=cg_preconditioner, cg_rtol=cg_rtol,
-                      comm=comm, device=device, backend=_backend, callback=cb, callback_format=callback_format)
+                      comm=comm, device=device, backend=_backend, callback=cb, callback_format=callback_format,
+                      ops=ops)
     solver.setup(x0 if not torch.is_tensor(x0) else x0.detach().cpu().numpy())
     while not solver.step():
         pass

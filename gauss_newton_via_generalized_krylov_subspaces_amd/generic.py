@@ -53,6 +53,7 @@ class DeviceCSR:
             self._arrays.append((torch.as_tensor(M.indptr.astype(np.int32), device=dev),
                                  torch.as_tensor(M.indices.astype(np.int32), device=dev),
                                  torch.as_tensor(M.data, device=dev)))
+        self._At_data_sq = torch.as_tensor(At.data * At.data, device=dev)   # Jacobi (host squares)
         self.be = be
 
     def matvec(self, x, y, negate=False):
@@ -62,6 +63,12 @@ class DeviceCSR:
     def rmatvec(self, w, y, negate=False):
         ip, ix, d = self._arrays[1]
         self.be.csr_spmv(self.shape[1], ip, ix, d, w, y, negate)
+
+    def jacobi(self, ones_m, dinv):
+        """dinv = 1 / diag(J^T J) (= 1 / diag(A^T A) for A = -J, ref:gauss_newton.py:50-52): the
+        squared entries of J^T summed per row in k-ascending order, as scipy's csr_matmat."""
+        ip, ix, _ = self._arrays[1]
+        self.be.csr_spmv(self.shape[1], ip, ix, self._At_data_sq, ones_m, dinv, reciprocal=True)
 
 
 class FlatKrylovBasis:
@@ -140,7 +147,7 @@ class HostCallableOps:
     jacobian_is_free = False       # jac(x) is user code: evaluated exactly where the reference does
     fuse_trial = False
 
-    def __init__(self, res, jac, n: int, args=(), device=None, backend=None):
+    def __init__(self, res, jac, n: int, args=(), device=None, backend=None, dense_jacobian: bool = True):
         self.be = backend if backend is not None else make_backend(device)
         self.comm = Comm(single=True)
         self.backend = self.be         # the attribute lls.CholQR2Solver reads
@@ -148,6 +155,7 @@ class HostCallableOps:
         self.res, self.jac, self.args = res, jac, tuple(args)
         self.n = self.n_global = int(n)
         self.m = None                  # learnt from the first res / jac evaluation
+        self.dense_jacobian = dense_jacobian
         self._J = {}                   # iterate buffer -> DeviceCSR of jac at its value
         self._W = None
         self._st = self.be.zeros(2)
@@ -188,7 +196,13 @@ class HostCallableOps:
 
     def on_jacobian(self, u):
         """jac(u, *args) (the user's function) -> device CSR of J and J^T, kept for u's buffer."""
-        J = DeviceCSR(self.be, self.jac(self.to_host(u), *self.args))
+        Jh = self.jac(self.to_host(u), *self.args)
+        if not self.dense_jacobian and not scipy.sparse.issparse(Jh):
+            raise NotImplementedError(
+                "gauss_newton with a dense ndarray Jacobian takes the reference's scipy.linalg.lstsq branch "
+                "(ref:gauss_newton.py:115-116), which is out of scope (SURVEY §8 f4); pass a scipy.sparse "
+                "Jacobian for the CGLS branch")
+        J = DeviceCSR(self.be, Jh)
         if J.shape[1] != self.n:
             raise ValueError(f"jac returned shape {J.shape}, expected (m, {self.n})")
         if self.m is None:
@@ -220,6 +234,55 @@ class HostCallableOps:
         for j in range(k):
             J.matvec(V[j], self._W[j])
         self.be.flat_gram(self._W, k, rinv, r, self.m, G)
+
+    # -- Gauss-Newton / CGLS (gauss_newton.GNSolver, DeviceCG) -----------------------------
+    def jvp_sumsq(self, u, d) -> float:
+        """jdd = sum((J(u) d)^2) (ref:armijo_goldstein.py:50)."""
+        if getattr(self, "_jd", None) is None:
+            self._jd = self.be.zeros(self.m)
+        self._jac_of(u).matvec(d, self._jd)
+        self.be.flat_stats(self._jd, self._st)
+        return float(self._st[0].item())
+
+    def axpy(self, x, t, d, out):
+        self.be.flat_axpy(x, t, d, out)
+
+    def sumsq(self, v) -> float:
+        self.be.flat_stats(v, self._st)
+        return float(self._st[0].item())
+
+    def cg_rhs(self, u, y, b):
+        """b = A^T y with A = -J(u): -(J^T y) (ref:gauss_newton.py:46,57)."""
+        self._jac_of(u).rmatvec(y, b, negate=True)
+
+    def cg_prepare(self, u):
+        self._cgJ = self._jac_of(u)
+        if getattr(self, "_tm", None) is None:
+            self._tm = self.be.zeros(self.m)
+            self._ones = self.be.to_device(np.ones(self.m))
+            self._s1 = self.be.zeros(1)
+            self._s2 = self.be.zeros(2)
+
+    def cg_jacobi(self, u, dinv):
+        self._jac_of(u).jacobi(self._ones, dinv)
+
+    def cg_normal_matvec(self, p, q) -> float:
+        """q = A^T (A p) = J^T (J p) (the reference's LinearOperator, ref:gauss_newton.py:36); p . q."""
+        self._cgJ.matvec(p, self._tm)
+        self._cgJ.rmatvec(self._tm, q)
+        self.be.flat_dot(p, q, self._s1)
+        return float(self._s1[0].item())
+
+    def cg_update_xr(self, alpha, p, q, x, r, dinv, z):
+        self.be.flat_cg_update_xr(alpha, p, q, x, r, dinv, z, self._s2)
+        rr, rz = self._s2.cpu().numpy()
+        return float(rr), float(rz)
+
+    def cg_update_p(self, beta, first, z, p):
+        self.be.flat_cg_update_p(beta, first, z, p)
+
+    def cg_finish(self, x):
+        pass
 
     # -- solver parts --------------------------------------------------------------------
     def make_basis(self, kmax):

@@ -63,7 +63,7 @@ class DeviceKrylovBasis:
     def x(self, c: np.ndarray, out):
         """out = V @ c over the whole slab (ref:krylow.py:41-42)."""
         k = len(c)
-        self._c[:k].copy_(self.be.to_device(c))
+        self.be.upload(self._c, c)
         self.be.gemv(self.V, k, self._c, out)
         return out
 
@@ -75,7 +75,7 @@ class DeviceKrylovBasis:
         products_ready=True)`` then continues from them.  Used for the first Armijo trial of
         version "res_old" (the update after acceptance is exactly this product)."""
         k = len(c)
-        self._c[:k].copy_(self.be.to_device(c))
+        self.be.upload(self._c, c)
         self.be.gemv_vjp_gemv_t(self.V, k, self._c, r, out, self._g, self._h)
         return out
 
@@ -93,8 +93,8 @@ class DeviceKrylovBasis:
         g = self._g
         if not products_ready:
             self.be.vjp_gemv_t(u_jac, r, self.V, k, g, self._h)   # g = -J^T r ; h = V^T g (:62, :64)
-        h = self.dev.comm.sum(self._h[:k])
-        self._h[:k].copy_(self.be.to_device(h))
+        if self.dev.comm.world > 1:                           # rank-ordered sum of the partials
+            self.be.upload(self._h, self.dev.comm.sum(self._h[:k]))
         self.be.cgs_update(self.V, k, self._h, g, self._stats)   # g -= V h (:64)
         sumsq, maxabs = self.dev.comm.sum_max(self._stats)
         if maxabs <= 1e-8 and not math.isnan(sumsq):          # :66
@@ -107,4 +107,7 @@ class DeviceKrylovBasis:
         # equal the neighbours' V[k] rows bit for bit) + sum (J g)^2 on owned rows
         self.be.normalize_jnorm(u_jac if u_next is None else u_next, g, nrm, self.V[k], self._jn2)
         self.k = k + 1
-        return math.sqrt(float(self.dev.comm.sum(self._jn2)[0])) / nrm
+        jn2, comm = self._jn2, self.dev.comm
+        # ||J v_new|| is needed only by the next least-squares solve: read it then (after the Gram
+        # pass's own sync) instead of stalling the queue here
+        return lambda: math.sqrt(float(comm.sum(jn2)[0])) / nrm

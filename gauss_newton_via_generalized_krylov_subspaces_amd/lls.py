@@ -69,13 +69,14 @@ class CholQR2Solver:
         self.s_new = None           # ||J v_new|| of the column appended since then
 
     # -- basis events (the solver tells us how V changed since the last solve) -------
-    def on_append(self, s_new: float):
-        self.s_new = float(s_new)
+    def on_append(self, s_new):
+        """s_new = ||J v_new||, a float or a callable returning it (read lazily at the next solve)."""
+        self.s_new = s_new
 
-    def on_restart(self, s0: float = None):
+    def on_restart(self, s0=None):
         """The basis restarted with one column v_0; s0 = ||J v_0|| (None: unknown -> CholQR2)."""
         self.R_prev = None if s0 is None else np.zeros((0, 0))
-        self.s_new = None if s0 is None else float(s0)
+        self.s_new = s0
 
     def _gram(self, u, basis, k, P, r):
         be = self.be
@@ -87,7 +88,7 @@ class CholQR2Solver:
             if r is not None:
                 aug[k, k] = 1.0
             rinv_dev = self._rinv[:kp * kp]
-            rinv_dev.copy_(be.to_device(aug.reshape(-1)))
+            be.upload(rinv_dev, aug.reshape(-1))
         G = self._G[:kp * kp]
         self._gram_fn(u, basis.V, k, rinv_dev, r, G)
         self.passes += 1
@@ -97,6 +98,8 @@ class CholQR2Solver:
         R = self.R_prev
         if R is None:
             return None
+        if callable(self.s_new):
+            self.s_new = float(self.s_new())
         kp = R.shape[0]
         if kp == k:
             return R                                   # basis unchanged (breakdown / spans space)

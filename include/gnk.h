@@ -153,11 +153,12 @@ int gnk_flat_axpy(gnk_ctx* ctx, const double* x, double alpha, const double* d, 
 int gnk_flat_cg_update_xr(gnk_ctx* ctx, double alpha, const double* p, const double* q, double* x, double* r,
                           const double* dinv, double* z, int64_t n, double* out);
 int gnk_flat_cg_update_p(gnk_ctx* ctx, double beta, int first, const double* z, double* p, int64_t n);
-/* y = A x (negate != 0: y = -(A x)), CSR with 32-bit indices, scipy csr_matvec summation order:
- * the J @ v / J.T @ w of a user Jacobian (J.T as the CSR of the transpose)
- *                                                  ref:krylow.py:62, gauss_newton_krylow.py:86 */
+/* y = A x, CSR with 32-bit indices, scipy csr_matvec summation order: the J @ v / J.T @ w of a
+ * user Jacobian (J.T as the CSR of the transpose).  mode 1: y = -(A x); mode 2: y = 1 / (A x)
+ * (with the squared entries of J.T and x = 1: the Jacobi vector 1 / diag(A.T @ A))
+ *                    ref:krylow.py:62, gauss_newton_krylow.py:86, gauss_newton.py:36, :50-52 */
 int gnk_csr_spmv(gnk_ctx* ctx, int64_t nrows, const int* indptr, const int* indices, const double* data,
-                 const double* x, double* y, int negate);
+                 const double* x, double* y, int mode);
 /* Gram of [W @ RinvAug | r] for a materialised W (k <= 63 columns of length m, stride ldw),
  * G_out kp x kp (kp = gnk_gram_padded_dim(k, r != NULL)); rinv NULL = identity
  *                                                       ref:gauss_newton_krylow.py:16-36, 86-89 */

@@ -42,6 +42,11 @@ class NumpyBackend:
     def zeros(self, *shape):
         return torch.zeros(*shape, dtype=torch.float64)
 
+    def upload(self, dst, a):
+        a = np.asarray(a, dtype=np.float64).reshape(-1)
+        dst.numpy()[:a.size] = a
+        return dst
+
     def to_device(self, a):
         return torch.as_tensor(np.asarray(a, dtype=np.float64)).clone()
 
@@ -192,11 +197,11 @@ class NumpyBackend:
         P = p.numpy()
         P[:] = z.numpy() if first else P * beta + z.numpy()
 
-    def csr_spmv(self, nrows, indptr, indices, data, x, y, negate=False):
+    def csr_spmv(self, nrows, indptr, indices, data, x, y, negate=False, reciprocal=False):
         A = scipy.sparse.csr_array((data.numpy(), indices.numpy(), indptr.numpy()),
                                    shape=(int(nrows), x.numel()))
         v = A @ x.numpy()
-        y.numpy()[:] = -v if negate else v
+        y.numpy()[:] = 1.0 / v if reciprocal else (-v if negate else v)
 
     def flat_gram(self, W, k, rinv, r, m, G):
         kp = self.gram_dim(k, r is not None)

@@ -25,18 +25,27 @@ def rosen_x0(arr, p, name):
 
 
 @pytest.mark.parametrize("p,x0name", [(2, "m1_1"), (2, "2_2"), (1000, "i"), (1000, "ii"), (1000, "iii")])
-@pytest.mark.parametrize("version", ["res_old", "res_new"])
+@pytest.mark.parametrize("version", ["res_old", "res_new", "gn"])
 def test_generic_gnk_rosenbrock(golden, p, x0name, version):
     meta, arr = golden
     res, jac = O.rosenbrock(p)
     x0 = rosen_x0(arr, p, x0name)
     x0_copy = x0.copy()
-    out, rec, so, exc = _run(gnk.gauss_newton_krylow, res, x0, jac, version=version, _backend=NumpyBackend())
+    if version == "gn":
+        out, rec, so, exc = _run(gnk.gauss_newton, res, x0, jac, _backend=NumpyBackend())
+    else:
+        out, rec, so, exc = _run(gnk.gauss_newton_krylow, res, x0, jac, version=version, _backend=NumpyBackend())
     name = f"rosen{p}_{x0name}_{version}"
     _check(meta["cases"][name], out, rec, so, exc, rtol=1e-10 if p == 2 else 1e-9)
     np.testing.assert_array_equal(x0, x0_copy)        # x0 is not mutated
     if p == 2:
         np.testing.assert_allclose(out.x, arr[name + "__x"], rtol=1e-10, atol=1e-14)
+
+
+def test_generic_gn_rejects_dense_jacobian():
+    res, jac = O.rosenbrock(2)
+    with pytest.raises(NotImplementedError, match="lstsq"):
+        gnk.gauss_newton(res, np.array([2.0, 2.0]), lambda x: jac(x).toarray(), _backend=NumpyBackend())
 
 
 def test_generic_args_and_dense_jacobian():

@@ -101,14 +101,27 @@ def test_flat_gram(be, m, k, with_r, with_rinv):
 
 
 @pytest.mark.parametrize("p,x0name", [(2, "m1_1"), (2, "2_2"), (1000, "i"), (1000, "ii"), (1000, "iii")])
-@pytest.mark.parametrize("version", ["res_old", "res_new"])
+@pytest.mark.parametrize("version", ["res_old", "res_new", "gn"])
 def test_gpu_generic_gnk_rosenbrock(golden, p, x0name, version):
     meta, arr = golden
     res, jac = O.rosenbrock(p)
     x0 = rosen_x0(arr, p, x0name)
-    out, rec, so, exc = _run(gnk.gauss_newton_krylow, res, x0, jac, version=version)
+    if version == "gn":
+        out, rec, so, exc = _run(gnk.gauss_newton, res, x0, jac)
+    else:
+        out, rec, so, exc = _run(gnk.gauss_newton_krylow, res, x0, jac, version=version)
     name = f"rosen{p}_{x0name}_{version}"
-    _check(meta["cases"][name], out, rec, so, exc, rtol=1e-10 if p == 2 else 1e-9)
+    case = meta["cases"][name]
+    if version == "gn":
+        # scipy's cg stops on ||r|| < rtol ||b|| (strict): near convergence that is a rounding tie,
+        # and the GPU reductions round differently from OpenBLAS ddot / dnrm2 -- a CG solve may take
+        # one iteration more or less (as for the long Bratu CG solves); the outer
+        # bookkeeping and trajectory stay exact
+        ref_cg = case["per_iter"]["cg_iter"]
+        assert len(rec["cg_iter"]) == len(ref_cg)
+        assert all(abs(a - b) <= 1 for a, b in zip(rec["cg_iter"], ref_cg))
+        rec = dict(rec, cg_iter=ref_cg)
+    _check(case, out, rec, so, exc, rtol=1e-10 if p == 2 else 1e-9)
     if p == 2:
         np.testing.assert_allclose(out.x, arr[name + "__x"], rtol=1e-10, atol=1e-14)
 
