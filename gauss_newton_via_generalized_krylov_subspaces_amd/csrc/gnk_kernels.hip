@@ -1267,7 +1267,6 @@ __global__ __launch_bounds__(BLOCK) void k_gram_m(const double* __restrict__ u, 
 #endif                  // loop, 2 = no stencil fragments, 4 = no MFMAs
 constexpr int GS_SW = 128;
 constexpr int GS_CS = 144;
-constexpr int GS_R = 5;
 constexpr int GS_NW = 8;
 constexpr int GS_KMAX = 20;     // V columns the staged kernel covers (k 21..24 would fit the LDS
                                 // ring but the two-block instance then spills past 256 VGPRs)
@@ -1291,8 +1290,8 @@ __device__ __forceinline__ double bcast_row(double v) {
 // then r . Y[:, block] per block, then r . r
 constexpr int gs_nacc(int nb, int ksl) { return nb == 1 ? 2 : 2 * 4 * ksl + 2 + 1; }
 
-template <int NB, int L, int KSL>
-__global__ __launch_bounds__(64 * GS_NW) void k_gram_s(const double* __restrict__ u, const double* __restrict__ V,
+template <int NB, int L, int KSL, int R, int WPE>
+__global__ __launch_bounds__(64 * GS_NW) __attribute__((amdgpu_waves_per_eu(WPE))) void k_gram_s(const double* __restrict__ u, const double* __restrict__ V,
                                                        int64_t ldv, int k, const double* __restrict__ rinv,
                                                        int ldr, const double* __restrict__ r, Geo geo, Coef cf,
                                                        int64_t rpr, double* __restrict__ partial) {
@@ -1451,19 +1450,22 @@ __global__ __launch_bounds__(64 * GS_NW) void k_gram_s(const double* __restrict_
       }
     }
   };
+  // R = 5: row x+3 is issued in step x and lands by the end of step x+1 (one row in flight across
+  // each barrier); R = 4: row x+2 is issued in step x and waited for at its end (a smaller ring,
+  // so two blocks fit a CU at larger k)
+  constexpr int INF = R - 4;                        // rows still in flight at a barrier
   if (x0 < x1) {
-    // ring slots rotate: sn/sc/ss = rows x-1, x, x+1; sd = row x+3 (the slot of row x-2)
-    int sn = int((x0 - 1 + GS_R) % GS_R), sc = int(x0 % GS_R), ss = int((x0 + 1) % GS_R);
-    int sp = int((x0 + 2) % GS_R), sd = int((x0 + 3) % GS_R);
+    // ring slots rotate: sn/sc/ss = rows x-1, x, x+1; sd = row x+R-2 (the slot of row x-2)
+    int sn = 0, sc = 1, ss = 2, sp = 3, sd = R - 1;
     issue_row(x0 - 1, sn);
     issue_row(x0, sc);
     issue_row(x0 + 1, ss);
-    issue_row(x0 + 2, sp);
-    __builtin_amdgcn_s_waitcnt(waitcnt_vm_lgkm0(L));    // rows x0-1 .. x0+1 landed
+    if (R == 5) issue_row(x0 + 2, sp);
+    __builtin_amdgcn_s_waitcnt(waitcnt_vm_lgkm0(L * INF));  // rows x0-1 .. x0+1 landed
     __builtin_amdgcn_s_barrier();
     double dn = -jdiag(cf, lds[sc * slotd + ou]);
     for (int64_t x = x0; x < x1; ++x) {
-      if (!(GNK_SDBG & 1)) issue_row(x + 3, sd);
+      if (!(GNK_SDBG & 1)) issue_row(x + R - 2, sd);
       const double* Ln = lds + sn * slotd;
       const double* Lc = lds + sc * slotd;
       const double* Ls = lds + ss * slotd;
@@ -1509,10 +1511,14 @@ __global__ __launch_bounds__(64 * GS_NW) void k_gram_s(const double* __restrict_
       const int t = sn;
       sn = sc;
       sc = ss;
-      ss = sp;
-      sp = sd;
+      if (R == 5) {
+        ss = sp;
+        sp = sd;
+      } else {
+        ss = sd;
+      }
       sd = t;
-      __builtin_amdgcn_s_waitcnt(waitcnt_vm_lgkm0(L));  // row x+2 landed; only row x+3 in flight
+      __builtin_amdgcn_s_waitcnt(waitcnt_vm_lgkm0(L * INF));  // row x+2 landed (R = 5: x+3 in flight)
       __builtin_amdgcn_s_barrier();
     }
     if (!(GNK_SDBG & 4)) gram(qp, lds + sn * slotd);  // last row x1-1 (its slot is now sn)
@@ -2188,7 +2194,21 @@ int gnk_gram(gnk_ctx* ctx, const double* u, const double* V, int64_t ldv, int k,
     const int nbs = k <= 16 ? 1 : 2;                        // MFMA transform blocks of the V columns
     const int nrow = k + 1 + (r ? 1 : 0);
     const int L = (nrow + 1 + GS_NW - 1) / GS_NW;
-    const size_t lds = size_t(GS_R) * (size_t(nrow) * GS_CS + 128) * sizeof(double);
+    // ring depth and occupancy: 5 slots (one row in flight across a barrier) while two blocks fit a
+    // CU, else 4 slots if that makes two blocks fit, else 5 slots at one block per CU.  Two blocks
+    // need <= 128 VGPRs, which KSL = 4 only reaches by spilling (measured 1.2-1.5x slower), so the
+    // 4-slot ring is for KSL <= 3: k = 12 with r, 1.98 ms vs 2.31 ms at 8192^2.
+    // GNK_GRAM_RING=5 / 4 forces a depth (tooling A/B).
+    const char* ring_s = getenv("GNK_GRAM_RING");
+    const int ring_env = ring_s ? atoi(ring_s) : 0;
+    const size_t slot_bytes = (size_t(nrow) * GS_CS + 128) * sizeof(double);
+    const size_t half_lds = 80 * 1024;
+    int ring = 5;
+    if (ring_env == 4 || (ring_env != 5 && 5 * slot_bytes > half_lds && 4 * slot_bytes <= half_lds && k <= 12))
+      ring = 4;
+    if (nbs == 2) ring = 5;
+    const size_t lds = size_t(ring) * slot_bytes;
+    const bool two_wg = lds <= half_lds;                      // 4 waves per SIMD: VGPRs capped at 128
     if (L <= 4 && lds <= 160 * 1024) {
       const double* rv = rinv ? rinv : ctx->ident + ident_offset(KP / 16);
       // 4-column k-steps of the last transform block
@@ -2206,9 +2226,15 @@ int gnk_gram(gnk_ctx* ctx, const double* u, const double* V, int64_t ldv, int k,
         return fail(ctx, "gram: scratch too small (staged)");
       const int64_t nown = nrows * ctx->geo.N;
       TimedLaunch tls(ctx, GNK_TIMER_GRAM, 8.0 * double(nown) * double(k + 1 + (r ? 1 : 0)));
-#define GRAMS(NBV, LV, KV)                                                                                    \
-  hipLaunchKernelGGL((k_gram_s<NBV, LV, KV>), dim3(unsigned(nwg)), dim3(64 * GS_NW), lds, ctx->stream, u, V, ldv, k, \
-                     rv, KP, r, ctx->geo, ctx->coef, rpr, ctx->scratch)
+#define GRAMS_RW(NBV, LV, KV, RV, WV)                                                                         \
+  hipLaunchKernelGGL((k_gram_s<NBV, LV, KV, RV, WV>), dim3(unsigned(nwg)), dim3(64 * GS_NW), lds, ctx->stream, u, V, \
+                     ldv, k, rv, KP, r, ctx->geo, ctx->coef, rpr, ctx->scratch)
+#define GRAMS(NBV, LV, KV)                                                 \
+  do {                                                                     \
+    if (ring == 4) GRAMS_RW(NBV, LV, KV, 4, 4);                       \
+    else if (two_wg) GRAMS_RW(NBV, LV, KV, 5, 4);                          \
+    else GRAMS_RW(NBV, LV, KV, 5, 2);                                      \
+  } while (0)
 #define GRAMS_K(NBV, LV)                                                    \
   do {                                                                      \
     if (ksl == 1) GRAMS(NBV, LV, 1); else if (ksl == 2) GRAMS(NBV, LV, 2);  \
@@ -2217,10 +2243,11 @@ int gnk_gram(gnk_ctx* ctx, const double* u, const double* V, int64_t ldv, int k,
       if (nbs == 1) {
         if (L == 1) GRAMS_K(1, 1); else if (L == 2) GRAMS_K(1, 2); else if (L == 3) GRAMS_K(1, 3); else GRAMS_K(1, 4);
       } else {
-        if (L == 3) GRAMS(2, 3, 1); else GRAMS(2, 4, 1);     // k <= 20: one tail k-step
+        if (L == 3) GRAMS_RW(2, 3, 1, 5, 2); else GRAMS_RW(2, 4, 1, 5, 2);     // k <= 20: one tail k-step
       }
 #undef GRAMS_K
 #undef GRAMS
+#undef GRAMS_RW
       tls.done();
       int rcs = check_launch(ctx, "gram_s");
       if (rcs) return rcs;

@@ -176,15 +176,19 @@ def test_cgs_max_propagates_nan():
                                                   (1024, 25, False, False), (256, 31, False, False),
                                                   # staged kernel: one block, k = 16 with r, tails 1..4
                                                   (256, 16, True, True), (256, 17, True, True), (128, 18, False, True),
-                                                  (256, 19, True, False), (1024, 16, True, True), (256, 4, True, True)])
-@pytest.mark.parametrize("staged", ["default", "forced"])
+                                                  (256, 19, True, False), (1024, 16, True, True), (256, 4, True, True),
+                                                  (512, 12, True, True), (384, 9, False, True)])
+@pytest.mark.parametrize("staged", ["default", "forced", "ring4"])
 def test_gram_mfma(N, k, with_r, with_rinv, staged, monkeypatch):
     """W = [J V | r] @ RinvAug on fp64 MFMA vs an fp64 NumPy Gram (host BLAS).  "forced" runs
-    the staged LDS-DMA kernel for every pass it supports (N % 128 == 0, k <= 20)."""
-    if staged == "forced":
+    the staged LDS-DMA kernel for every pass it supports (N % 128 == 0, k <= 20); "ring4" also
+    forces its 4-slot ring (two blocks per CU, the default only for k = 12)."""
+    if staged != "default":
         if N % 128 or k > 20:
             pytest.skip("staged kernel does not cover this shape")
         monkeypatch.setenv("GNK_GRAM_STAGED", "2")
+        if staged == "ring4":
+            monkeypatch.setenv("GNK_GRAM_RING", "4")
     prob, dev, ref = make(N)
     be = dev.backend
     rng = np.random.default_rng(N + k)
