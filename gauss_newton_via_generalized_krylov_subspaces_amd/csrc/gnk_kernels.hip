@@ -629,6 +629,101 @@ __global__ __launch_bounds__(BLOCK) void k_cg_matvec(const double* __restrict__ 
   block_sum_store<1>(acc, 1, partial + (blockIdx.y * gridDim.x + blockIdx.x), sh);
 }
 
+// q = J^T (J p) by row marching, and the partial p.q.  One wave walks a 128-point strip (two points
+// per lane) down a range of rows, four strips per block.  t = J p of rows x-1, x, x+1 stays in
+// registers, so every p and d value is loaded once per range (+2 warm-up rows) instead of up to 13
+// times.  The in-row neighbours of p and t come from the adjacent lanes.  At the strip edges:
+//   * lanes 0 and 63 load one extra 16-B pair of p and d per row;
+//   * they evaluate the one t point outside the strip.
+// Each point is computed as in k_cg_matvec (jvp_pt then vjp_pt, same operands, same order), so q
+// is bit-identical; only the p.q partial sums are grouped differently.  Requires N even (16-B pairs).
+constexpr int CGM_SW = 128;
+
+__global__ __launch_bounds__(BLOCK) void k_cg_matvec_m(const double* __restrict__ d, const double* __restrict__ p,
+                                                       double* __restrict__ q, Geo geo, Coef c, int64_t rpr,
+                                                       double* __restrict__ partial) {
+  __shared__ double sh[BLOCK / 64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int64_t N = geo.N;
+  const int nbc = int((N + 4 * CGM_SW - 1) / (4 * CGM_SW));
+  const int nwg = gridDim.x, b = blockIdx.x;
+  // XCD-aware: consecutive tiles of one XCD (blockIdx % 8) are neighbouring strips of a row range
+  const int idx = (nwg % 8 == 0) ? (b % 8) * (nwg / 8) + b / 8 : b;
+  const int64_t x0 = int64_t(idx / nbc) * rpr;            // owned-row index range [x0, x1)
+  const int64_t x1 = min(geo.nrows, x0 + rpr);
+  const int64_t col0 = int64_t(idx % nbc) * (4 * CGM_SW) + wave * CGM_SW;
+  const int64_t y0 = col0 + 2 * lane;                     // this lane's points y0, y0 + 1
+  const bool valid = y0 < N;
+  const bool hw0 = y0 > 0, he1 = y0 + 2 < N;
+  // edge pairs: lane 0 -> columns col0-2, col0-1; lane 63 -> col0+128, col0+129
+  const bool ex = (lane == 0 && col0 > 0) || (lane == 63 && col0 + CGM_SW < N);
+  const int64_t exo = lane == 0 ? -2 : 2;
+  double acc[1] = {0.0};
+  auto ld = [&](const double* base, int64_t x) -> d2 {    // x: owned-row index (may be -2 .. nrows+1)
+    return valid ? *reinterpret_cast<const d2*>(base + (G + x) * N + y0) : d2{0.0, 0.0};
+  };
+  auto ldx = [&](const double* base, int64_t x) -> d2 {
+    return ex ? *reinterpret_cast<const d2*>(base + (G + x) * N + y0 + exo) : d2{0.0, 0.0};
+  };
+  // t = J p at this lane's two points of row x (0 outside the domain)
+  auto trow = [&](int64_t x, d2 pn, d2 pc, d2 ps, d2 xc, d2 dc) -> d2 {
+    double pw = __shfl_up(pc.y, 1);
+    double pe = __shfl_down(pc.x, 1);
+    if (lane == 0) pw = xc.y;
+    if (lane == 63) pe = xc.x;
+    const int64_t gx = geo.row0 + x;
+    if (gx < 0 || gx >= N || !valid) return d2{0.0, 0.0};
+    d2 t;
+    t.x = jvp_pt(c, dc.x, pn.x, pw, hw0, pc.x, pc.y, true, ps.x);
+    t.y = jvp_pt(c, dc.y, pn.y, pc.x, true, pc.y, pe, he1, ps.y);
+    return t;
+  };
+  if (x0 < x1) {
+    // rows x-1 .. x+2 of p (and edge pairs), rows x, x+1 of d, t rows x-1, x
+    d2 pA = ld(p, x0 - 2), pB = ld(p, x0 - 1), pC = ld(p, x0), pD = ld(p, x0 + 1), pE = ld(p, x0 + 2);
+    d2 xA = ldx(p, x0 - 1), xB = ldx(p, x0), xC = ldx(p, x0 + 1), xD = ldx(p, x0 + 2);
+    d2 dA = ld(d, x0 - 1), dB = ld(d, x0), dC = ld(d, x0 + 1);
+    d2 eB = ldx(d, x0), eC = ldx(d, x0 + 1);
+    d2 tn = trow(x0 - 1, pA, pB, pC, xA, dA);
+    d2 tc = trow(x0, pB, pC, pD, xB, dB);
+    // loop invariants: pB, pC, pD, pE = p rows x-1 .. x+2; xA, xB, xC = edge pairs x-1 .. x+1,
+    // xD = x+2; dB, dC = d rows x, x+1; eB, eC = their edge pairs
+    for (int64_t x = x0; x < x1; ++x) {
+      // prefetch row x+3 of p and row x+2 of d for the next step
+      const bool more = x + 1 < x1;
+      const d2 pF = more ? ld(p, x + 3) : d2{0.0, 0.0};
+      const d2 xE = more ? ldx(p, x + 3) : d2{0.0, 0.0};
+      const d2 dD = more ? ld(d, x + 2) : d2{0.0, 0.0};
+      const d2 eD = more ? ldx(d, x + 2) : d2{0.0, 0.0};
+      const d2 ts = trow(x + 1, pC, pD, pE, xC, dC);
+      // the t point just outside the strip, row x (lane 0: col0-1; lane 63: col0+128)
+      const bool l0 = lane == 0;
+      const double te = jvp_pt(c, l0 ? eB.y : eB.x, l0 ? xA.y : xA.x, l0 ? xB.x : pC.y, l0 ? col0 - 1 > 0 : true,
+                               l0 ? xB.y : xB.x, l0 ? pC.x : xB.y, l0 ? true : col0 + CGM_SW < N - 1,
+                               l0 ? xC.y : xC.x);
+      double tw = __shfl_up(tc.y, 1);
+      double tE = __shfl_down(tc.x, 1);
+      if (lane == 0) tw = te;
+      if (lane == 63) tE = te;
+      if (valid) {
+        d2 qo;
+        qo.x = vjp_pt(c, dB.x, tn.x, tw, hw0, tc.x, tc.y, true, ts.x);
+        qo.y = vjp_pt(c, dB.y, tn.y, tc.x, true, tc.y, tE, he1, ts.y);
+        *reinterpret_cast<d2*>(q + (G + x) * N + y0) = qo;
+        acc[0] += pC.x * qo.x;
+        acc[0] += pC.y * qo.y;
+      }
+      tn = tc;
+      tc = ts;
+      pB = pC; pC = pD; pD = pE; pE = pF;
+      xA = xB; xB = xC; xC = xD; xD = xE;
+      dB = dC; dC = dD;
+      eB = eC; eC = eD;
+    }
+  }
+  block_sum_store<1>(acc, 1, partial + blockIdx.x, sh);
+}
+
 template <int VEC>
 __global__ __launch_bounds__(BLOCK) void k_cg_xr(double alpha, const double* __restrict__ p,
                                                  const double* __restrict__ q, double* __restrict__ x,
@@ -2556,9 +2651,25 @@ int gnk_flat_gram(gnk_ctx* ctx, const double* W, int64_t ldw, int k, const doubl
 
 int gnk_cg_normal_matvec(gnk_ctx* ctx, const double* d, const double* p, double* q, double* pq_out) {
   if (!ready(ctx)) return -1;
-  RowLaunch L = rows(ctx, G, ctx->geo.nrows, vec_of(ctx));
-  const int nblk = L.grid.x * L.grid.y;
-  DISPATCH_VEC(ctx, k_cg_matvec, L, 0, d, p, q, ctx->geo, ctx->coef, L.lr0, L.nlr, ctx->scratch);
+  const char* cgm_s = getenv("GNK_CG_MATVEC");            // tooling A/B: 0 = the point-wise kernel
+  int nblk;
+  if (ctx->geo.N % 2 == 0 && !(cgm_s && atoi(cgm_s) == 0)) {
+    const int64_t nbc = (ctx->geo.N + 4 * CGM_SW - 1) / (4 * CGM_SW);
+    const int64_t nrows = ctx->geo.nrows;
+    int64_t nranges = std::max<int64_t>(1, std::min<int64_t>(nrows, int64_t(ctx->num_cus) * 8 / nbc));
+    const int64_t rpr = (nrows + nranges - 1) / nranges;
+    nranges = (nrows + rpr - 1) / rpr;
+    if (nbc * nranges > MAX_RED_BLOCKS) return fail(ctx, "cg_normal_matvec: grid too large");
+    nblk = int(nbc * nranges);
+    TimedLaunch tl(ctx, GNK_TIMER_CG_MATVEC, 24.0 * double(nrows) * double(ctx->geo.N));
+    hipLaunchKernelGGL(k_cg_matvec_m, dim3(unsigned(nblk)), dim3(BLOCK), 0, ctx->stream, d, p, q, ctx->geo, ctx->coef,
+                       rpr, ctx->scratch);
+    tl.done();
+  } else {
+    RowLaunch L = rows(ctx, G, ctx->geo.nrows, vec_of(ctx));
+    nblk = L.grid.x * L.grid.y;
+    DISPATCH_VEC(ctx, k_cg_matvec, L, 0, d, p, q, ctx->geo, ctx->coef, L.lr0, L.nlr, ctx->scratch);
+  }
   int rc = check_launch(ctx, "cg_normal_matvec");
   if (rc) return rc;
   return reduce(ctx, ctx->scratch, nblk, 1, 1, nullptr, pq_out);

@@ -172,6 +172,7 @@ int gnk_flat_gram(gnk_ctx* ctx, const double* W, int64_t ldw, int k, const doubl
  * returns the count, the milliseconds and the algorithmic bytes of each launch. */
 #define GNK_TIMER_GRAM 1
 #define GNK_TIMER_JVP 2
+#define GNK_TIMER_CG_MATVEC 3
 int gnk_timer_start(gnk_ctx* ctx, int kernel_id, int capacity);
 int gnk_timer_collect(gnk_ctx* ctx, double* ms_out, double* bytes_out, int capacity);
 /* back-to-back v_mfma_f64_16x16x4_f64 issue-rate probe: blocks x 256 threads,

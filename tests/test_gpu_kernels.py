@@ -250,8 +250,10 @@ def test_gram_deterministic(staged, monkeypatch):
         np.testing.assert_array_equal(outs[i % 2], outs[i])
 
 
-@pytest.mark.parametrize("N", [24, 101, 512])
-def test_cg_matvec_matches_two_pass(N):
+@pytest.mark.parametrize("N", [24, 100, 101, 512, 640, 1030])
+def test_cg_matvec_matches_two_pass(N, monkeypatch):
+    """q = J^T J p (13-point fused) vs the oracle's two passes; even N runs the row-marching kernel,
+    whose q must equal the point-wise kernel's bit for bit (same per-point arithmetic)."""
     prob, dev, ref = make(N)
     be = dev.backend
     rng = np.random.default_rng(N)
@@ -267,6 +269,14 @@ def test_cg_matvec_matches_two_pass(N):
     q_ref = ref.vjp(u, ref.jvp(u, p))
     close(own(dev, q), q_ref, rtol=1e-12)
     np.testing.assert_allclose(pq.item(), p @ q_ref, rtol=1e-12)
+    pq_again = dev.scalar(1)
+    be.cg_matvec(d, ps, q, pq_again)
+    assert pq_again.item() == pq.item()                            # deterministic reduction
+    monkeypatch.setenv("GNK_CG_MATVEC", "0")
+    q0, pq0 = dev.vec(), dev.scalar(1)
+    be.cg_matvec(d, ps, q0, pq0)
+    np.testing.assert_array_equal(own(dev, q), own(dev, q0))
+    np.testing.assert_allclose(pq0.item(), pq.item(), rtol=1e-13)
 
 
 def test_cg_updates():
