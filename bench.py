@@ -49,6 +49,7 @@ def parse():
     ap.add_argument("--version", default="res_old")
     ap.add_argument("--cpu-seconds", type=float, default=20.0, help="CPU oracle sample budget (0 = skip)")
     ap.add_argument("--jvp-reps", type=int, default=20)
+    ap.add_argument("--cg-iters", type=int, default=200, help="CGLS iterations of the C3 line (0 = skip)")
     return ap.parse_args()
 
 
@@ -109,6 +110,55 @@ def cpu_baseline(N, seconds, version, restart):
     return {"value": it / total, "unit": "outer_iters/s", "cores": threads, "kind": "port",
             "sample": f"oracle/gnk_oracle.py GNK on the same {N}^2 workload, first {it} outer iterations "
                       f"(basis k=1..{it}; {total:.1f} s, setup excluded), OPENBLAS threads={threads}"}
+
+
+CG_BYTES_PER_ITER = 112     # SURVEY §8d model, bytes per unknown: p update 24, J^T J p 24, x/r/z update 64
+                            # (the fused iteration moves 96: step matvec 56 + r/z update 40)
+
+
+def gn_cg_line(args, prob, u_true, u0, comm, device, world):
+    """CGLS of the first Gauss-Newton step at cg_rtol = 1e-8 (Jacobi preconditioner,
+    ref:gauss_newton.py:50-58), capped at --cg-iters iterations (a full solve at 8192^2 takes far
+    more).  Reports CG iterations/s of the whole job and the fused J^T J p kernel's per-launch rate."""
+    from gauss_newton_via_generalized_krylov_subspaces_amd import _native
+    from gauss_newton_via_generalized_krylov_subspaces_amd._device import SingleRankOperator
+    from gauss_newton_via_generalized_krylov_subspaces_amd.gauss_newton import BratuGNOps, DeviceCG
+    N = args.grid
+    n = N * N
+    y = SingleRankOperator(prob, device).forward(u_true)
+    ops = BratuGNOps(prob, y, comm, device)
+    del y
+    cg = DeviceCG(ops)
+    u = ops.load(u0)
+    be = ops.be
+    cg.solve(u, ops.y, cg_rtol=1e-8, preconditioner=True, maxiter=5)          # warm-up
+    cap = args.cg_iters + 8
+    be.timer_start(_native.TIMER_CG_MATVEC, cap)
+    comm.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    _, iters = cg.solve(u, ops.y, cg_rtol=1e-8, preconditioner=True, maxiter=args.cg_iters)
+    torch.cuda.synchronize()
+    comm.barrier()
+    elapsed = time.perf_counter() - t0
+    ml = be.timer_collect(cap)
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = t.item()
+    m_ms = float(np.mean([m for m, _ in ml])) if ml else float("nan")
+    m_by = float(np.mean([b for _, b in ml])) if ml else float("nan")
+    m_gbs = m_by / (m_ms * 1e-3) / 1e9 if ml else float("nan")
+    return {"workload": f"bratu_{N}x{N}_gn_cgls_rtol1e-8_first_step", "cg_iters": iters,
+            "value": iters / elapsed, "unit": "cg_iters/s", "ms_per_iter": 1e3 * elapsed / max(iters, 1),
+            "algorithmic_GBs": CG_BYTES_PER_ITER * n * iters / elapsed / 1e9,
+            "bytes_per_iter": CG_BYTES_PER_ITER * n,
+            "note": "timed: one CGLS solve capped at cg_iters (b = A^T y, Jacobi diag and the initial update "
+                    "included); scipy's 10 n cap would need millions of iterations at rtol 1e-8",
+            "matvec": {"kernel": "k_cg_matvec_m (p = z + beta p, lagged x += alpha p, q = J^T J p, 13-point, "
+                                 "row marching)", "avg_launch_ms": m_ms,
+                       "GBs": m_gbs, "frac_of_peak": m_gbs / HBM_PEAK_GBS,
+                       "algorithmic_bytes_per_launch": m_by}}
 
 
 def pmc_traffic(config_key):
@@ -207,6 +257,8 @@ def main():
     j_ms = float(np.median([m for m, _ in jl]))
     j_gbs = jl[0][1] / (j_ms * 1e-3) / 1e9
 
+    cg_line = gn_cg_line(args, prob, u_true, u0, comm, device, world) if args.cg_iters > 0 else None
+
     config_key = f"bratu{N}_gnk_restart{args.restart}_{args.version}_ranks{world}"
     traffic, traffic_src = pmc_traffic(config_key)
     result = {
@@ -237,6 +289,8 @@ def main():
         "step_algorithmic_GBs": total_bytes / elapsed / 1e9,
         "gram_passes_per_step": ppi,
     }
+    if cg_line is not None:
+        result["gn_cg"] = cg_line
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
         try:
             result["cpu_baseline"] = cpu_baseline(N, args.cpu_seconds, args.version, args.restart)

@@ -18,7 +18,7 @@ import torch
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("GNK_LIB", os.path.join(_HERE, "libgnk.so"))
 GHOST = 2  # GNK_GHOST_ROWS
-TIMER_GRAM, TIMER_JVP = 1, 2  # GNK_TIMER_*
+TIMER_GRAM, TIMER_JVP, TIMER_CG_MATVEC = 1, 2, 3  # GNK_TIMER_*
 
 _c_int, _c_i64, _c_dbl, _c_vp = ctypes.c_int, ctypes.c_int64, ctypes.c_double, ctypes.c_void_p
 
@@ -60,6 +60,8 @@ SIGNATURES = {
     "gnk_gram": (_c_int, [_c_vp, _c_vp, _c_vp, _c_i64, _c_int, _c_vp, _c_i64, _c_vp, _c_vp]),
     "gnk_cg_normal_matvec": (_c_int, [_c_vp, _c_vp, _c_vp, _c_vp, _c_vp]),
     "gnk_cg_update_xr": (_c_int, [_c_vp, _c_dbl, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp]),
+    "gnk_cg_step_matvec": (_c_int, [_c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_dbl, _c_int, _c_vp, _c_dbl,
+                                    _c_vp]),
     "gnk_cg_update_p": (_c_int, [_c_vp, _c_dbl, _c_int, _c_vp, _c_vp]),
     "gnk_probe_mfma_f64": (_c_int, [_c_vp, _c_vp, _c_int, _c_int]),
     "gnk_timer_start": (_c_int, [_c_vp, _c_int, _c_int]),
@@ -275,6 +277,10 @@ class HipBackend:
     # --- CG ------------------------------------------------------------------------
     def cg_matvec(self, d, p, q, pq):
         self._call("gnk_cg_normal_matvec", _p(d), _p(p), _p(q), _p(pq))
+
+    def cg_step_matvec(self, d, z, p_in, p_out, q, beta, first, x, xalpha, pq):
+        self._call("gnk_cg_step_matvec", _p(d), _p(z), _p(p_in), _p(p_out), _p(q), float(beta), int(bool(first)),
+                   _p(x), float(xalpha), _p(pq))
 
     def cg_update_xr(self, alpha, p, q, x, r, dinv, z, out):
         self._call("gnk_cg_update_xr", float(alpha), _p(p), _p(q), _p(x), _p(r), _p(dinv), _p(z), _p(out))

@@ -637,11 +637,21 @@ __global__ __launch_bounds__(BLOCK) void k_cg_matvec(const double* __restrict__ 
 //   * they evaluate the one t point outside the strip.
 // Each point is computed as in k_cg_matvec (jvp_pt then vjp_pt, same operands, same order), so q
 // is bit-identical; only the p.q partial sums are grouped differently.  Requires N even (16-B pairs).
+//
+// FUSED: the CG direction update of the same iteration rides on the loads (scipy iterative.py:
+// 401-415 order kept): p = first ? z : p_in * beta + z is formed as each row of z / p_in streams in
+// and stored to p (never p_in: neighbouring ranges read the overlap rows); the ranges at the slab
+// ends also store the ghost rows, so with z's halo exchanged every rank holds its neighbours' p
+// bit for bit.  x (optional) takes the previous iteration's x += xalpha * p_in on owned rows at the
+// same point (one iteration late; the caller applies the last one).
 constexpr int CGM_SW = 128;
 
-__global__ __launch_bounds__(BLOCK) void k_cg_matvec_m(const double* __restrict__ d, const double* __restrict__ p,
+template <bool FUSED>
+__global__ __launch_bounds__(BLOCK) void k_cg_matvec_m(const double* __restrict__ d, const double* __restrict__ pin,
                                                        double* __restrict__ q, Geo geo, Coef c, int64_t rpr,
-                                                       double* __restrict__ partial) {
+                                                       double* __restrict__ partial, const double* __restrict__ z,
+                                                       double* __restrict__ p, double beta, int first,
+                                                       double* __restrict__ x, double xalpha) {
   __shared__ double sh[BLOCK / 64];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int64_t N = geo.N;
@@ -659,19 +669,41 @@ __global__ __launch_bounds__(BLOCK) void k_cg_matvec_m(const double* __restrict_
   const bool ex = (lane == 0 && col0 > 0) || (lane == 63 && col0 + CGM_SW < N);
   const int64_t exo = lane == 0 ? -2 : 2;
   double acc[1] = {0.0};
-  auto ld = [&](const double* base, int64_t x) -> d2 {    // x: owned-row index (may be -2 .. nrows+1)
-    return valid ? *reinterpret_cast<const d2*>(base + (G + x) * N + y0) : d2{0.0, 0.0};
+  auto ld = [&](const double* base, int64_t xr) -> d2 {   // xr: owned-row index (may be -2 .. nrows+1)
+    return valid ? *reinterpret_cast<const d2*>(base + (G + xr) * N + y0) : d2{0.0, 0.0};
   };
-  auto ldx = [&](const double* base, int64_t x) -> d2 {
-    return ex ? *reinterpret_cast<const d2*>(base + (G + x) * N + y0 + exo) : d2{0.0, 0.0};
+  auto ldx = [&](const double* base, int64_t xr) -> d2 {
+    return ex ? *reinterpret_cast<const d2*>(base + (G + xr) * N + y0 + exo) : d2{0.0, 0.0};
+  };
+  auto pnew = [&](d2 zz, d2 pp) -> d2 {                  // k_cg_p's arithmetic
+    return first ? zz : d2{pp.x * beta + zz.x, pp.y * beta + zz.y};
+  };
+  // row xr of the direction: loaded (plain) or formed and stored (FUSED, + the lagged x update)
+  auto ldp = [&](int64_t xr) -> d2 {
+    if (!FUSED) return ld(pin, xr);
+    const d2 pi = ld(pin, xr);
+    const d2 pv = pnew(ld(z, xr), pi);
+    const bool own = xr >= x0 && xr < x1;
+    const bool ghost = (x0 == 0 && xr < 0) || (x1 == geo.nrows && xr >= geo.nrows);
+    if (valid && (own || ghost)) *reinterpret_cast<d2*>(p + (G + xr) * N + y0) = pv;
+    if (x && valid && own) {
+      d2* xp = reinterpret_cast<d2*>(x + (G + xr) * N + y0);
+      const d2 xv = *xp;
+      *xp = d2{xv.x + xalpha * pi.x, xv.y + xalpha * pi.y};
+    }
+    return pv;
+  };
+  auto ldpx = [&](int64_t xr) -> d2 {
+    if (!FUSED) return ldx(pin, xr);
+    return ex ? pnew(ldx(z, xr), ldx(pin, xr)) : d2{0.0, 0.0};
   };
   // t = J p at this lane's two points of row x (0 outside the domain)
-  auto trow = [&](int64_t x, d2 pn, d2 pc, d2 ps, d2 xc, d2 dc) -> d2 {
+  auto trow = [&](int64_t xr, d2 pn, d2 pc, d2 ps, d2 xc, d2 dc) -> d2 {
     double pw = __shfl_up(pc.y, 1);
     double pe = __shfl_down(pc.x, 1);
     if (lane == 0) pw = xc.y;
     if (lane == 63) pe = xc.x;
-    const int64_t gx = geo.row0 + x;
+    const int64_t gx = geo.row0 + xr;
     if (gx < 0 || gx >= N || !valid) return d2{0.0, 0.0};
     d2 t;
     t.x = jvp_pt(c, dc.x, pn.x, pw, hw0, pc.x, pc.y, true, ps.x);
@@ -680,22 +712,22 @@ __global__ __launch_bounds__(BLOCK) void k_cg_matvec_m(const double* __restrict_
   };
   if (x0 < x1) {
     // rows x-1 .. x+2 of p (and edge pairs), rows x, x+1 of d, t rows x-1, x
-    d2 pA = ld(p, x0 - 2), pB = ld(p, x0 - 1), pC = ld(p, x0), pD = ld(p, x0 + 1), pE = ld(p, x0 + 2);
-    d2 xA = ldx(p, x0 - 1), xB = ldx(p, x0), xC = ldx(p, x0 + 1), xD = ldx(p, x0 + 2);
+    d2 pA = ldp(x0 - 2), pB = ldp(x0 - 1), pC = ldp(x0), pD = ldp(x0 + 1), pE = ldp(x0 + 2);
+    d2 xA = ldpx(x0 - 1), xB = ldpx(x0), xC = ldpx(x0 + 1), xD = ldpx(x0 + 2);
     d2 dA = ld(d, x0 - 1), dB = ld(d, x0), dC = ld(d, x0 + 1);
     d2 eB = ldx(d, x0), eC = ldx(d, x0 + 1);
     d2 tn = trow(x0 - 1, pA, pB, pC, xA, dA);
     d2 tc = trow(x0, pB, pC, pD, xB, dB);
     // loop invariants: pB, pC, pD, pE = p rows x-1 .. x+2; xA, xB, xC = edge pairs x-1 .. x+1,
     // xD = x+2; dB, dC = d rows x, x+1; eB, eC = their edge pairs
-    for (int64_t x = x0; x < x1; ++x) {
+    for (int64_t xs = x0; xs < x1; ++xs) {
       // prefetch row x+3 of p and row x+2 of d for the next step
-      const bool more = x + 1 < x1;
-      const d2 pF = more ? ld(p, x + 3) : d2{0.0, 0.0};
-      const d2 xE = more ? ldx(p, x + 3) : d2{0.0, 0.0};
-      const d2 dD = more ? ld(d, x + 2) : d2{0.0, 0.0};
-      const d2 eD = more ? ldx(d, x + 2) : d2{0.0, 0.0};
-      const d2 ts = trow(x + 1, pC, pD, pE, xC, dC);
+      const bool more = xs + 1 < x1;
+      const d2 pF = more ? ldp(xs + 3) : d2{0.0, 0.0};
+      const d2 xE = more ? ldpx(xs + 3) : d2{0.0, 0.0};
+      const d2 dD = more ? ld(d, xs + 2) : d2{0.0, 0.0};
+      const d2 eD = more ? ldx(d, xs + 2) : d2{0.0, 0.0};
+      const d2 ts = trow(xs + 1, pC, pD, pE, xC, dC);
       // the t point just outside the strip, row x (lane 0: col0-1; lane 63: col0+128)
       const bool l0 = lane == 0;
       const double te = jvp_pt(c, l0 ? eB.y : eB.x, l0 ? xA.y : xA.x, l0 ? xB.x : pC.y, l0 ? col0 - 1 > 0 : true,
@@ -709,7 +741,7 @@ __global__ __launch_bounds__(BLOCK) void k_cg_matvec_m(const double* __restrict_
         d2 qo;
         qo.x = vjp_pt(c, dB.x, tn.x, tw, hw0, tc.x, tc.y, true, ts.x);
         qo.y = vjp_pt(c, dB.y, tn.y, tc.x, true, tc.y, tE, he1, ts.y);
-        *reinterpret_cast<d2*>(q + (G + x) * N + y0) = qo;
+        *reinterpret_cast<d2*>(q + (G + xs) * N + y0) = qo;
         acc[0] += pC.x * qo.x;
         acc[0] += pC.y * qo.y;
       }
@@ -735,7 +767,7 @@ __global__ __launch_bounds__(BLOCK) void k_cg_xr(double alpha, const double* __r
   ROW_LOOP_BEGIN(VEC)
   for (int qq = 0; qq < VEC && iy + qq < N; ++qq) {
     const int64_t i = li + qq;
-    x[i] = x[i] + alpha * p[i];
+    if (x) x[i] = x[i] + alpha * p[i];                 // NULL x: done by the fused matvec (lagged)
     const double ri = r[i] - alpha * q[i];
     r[i] = ri;
     const double zi = dinv ? 0.0 + dinv[i] * ri : ri;
@@ -2662,8 +2694,8 @@ int gnk_cg_normal_matvec(gnk_ctx* ctx, const double* d, const double* p, double*
     if (nbc * nranges > MAX_RED_BLOCKS) return fail(ctx, "cg_normal_matvec: grid too large");
     nblk = int(nbc * nranges);
     TimedLaunch tl(ctx, GNK_TIMER_CG_MATVEC, 24.0 * double(nrows) * double(ctx->geo.N));
-    hipLaunchKernelGGL(k_cg_matvec_m, dim3(unsigned(nblk)), dim3(BLOCK), 0, ctx->stream, d, p, q, ctx->geo, ctx->coef,
-                       rpr, ctx->scratch);
+    hipLaunchKernelGGL(k_cg_matvec_m<false>, dim3(unsigned(nblk)), dim3(BLOCK), 0, ctx->stream, d, p, q, ctx->geo,
+                       ctx->coef, rpr, ctx->scratch, nullptr, nullptr, 0.0, 0, nullptr, 0.0);
     tl.done();
   } else {
     RowLaunch L = rows(ctx, G, ctx->geo.nrows, vec_of(ctx));
@@ -2671,6 +2703,27 @@ int gnk_cg_normal_matvec(gnk_ctx* ctx, const double* d, const double* p, double*
     DISPATCH_VEC(ctx, k_cg_matvec, L, 0, d, p, q, ctx->geo, ctx->coef, L.lr0, L.nlr, ctx->scratch);
   }
   int rc = check_launch(ctx, "cg_normal_matvec");
+  if (rc) return rc;
+  return reduce(ctx, ctx->scratch, nblk, 1, 1, nullptr, pq_out);
+}
+
+int gnk_cg_step_matvec(gnk_ctx* ctx, const double* d, const double* z, const double* p_in, double* p_out, double* q,
+                       double beta, int first, double* x, double xalpha, double* pq_out) {
+  if (!ready(ctx)) return -1;
+  if (ctx->geo.N % 2) return fail(ctx, "cg_step_matvec: N must be even (use cg_update_p + cg_normal_matvec)");
+  if (!d || !z || !p_in || !p_out || !q || p_in == p_out) return fail(ctx, "cg_step_matvec: bad buffers");
+  const int64_t nbc = (ctx->geo.N + 4 * CGM_SW - 1) / (4 * CGM_SW);
+  const int64_t nrows = ctx->geo.nrows;
+  int64_t nranges = std::max<int64_t>(1, std::min<int64_t>(nrows, int64_t(ctx->num_cus) * 8 / nbc));
+  const int64_t rpr = (nrows + nranges - 1) / nranges;
+  nranges = (nrows + rpr - 1) / rpr;
+  if (nbc * nranges > MAX_RED_BLOCKS) return fail(ctx, "cg_step_matvec: grid too large");
+  const int nblk = int(nbc * nranges);
+  TimedLaunch tl(ctx, GNK_TIMER_CG_MATVEC, (x ? 56.0 : 40.0) * double(nrows) * double(ctx->geo.N));
+  hipLaunchKernelGGL(k_cg_matvec_m<true>, dim3(unsigned(nblk)), dim3(BLOCK), 0, ctx->stream, d, p_in, q, ctx->geo,
+                     ctx->coef, rpr, ctx->scratch, z, p_out, beta, first, x, xalpha);
+  tl.done();
+  int rc = check_launch(ctx, "cg_step_matvec");
   if (rc) return rc;
   return reduce(ctx, ctx->scratch, nblk, 1, 1, nullptr, pq_out);
 }

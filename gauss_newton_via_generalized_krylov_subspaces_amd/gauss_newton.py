@@ -21,6 +21,7 @@ one p update -- 112 n bytes of algorithmic traffic -- and two scalar syncs.
 from __future__ import annotations
 
 import math
+import os
 from collections.abc import Callable
 from typing import Optional
 
@@ -114,6 +115,28 @@ class BratuGNOps:
         sl = self.dev.slab
         self.comm.halo(x, sl.N, sl.nrows)
 
+    # fused iteration (N even): direction update + x update (one iteration late) ride on the
+    # normal matvec's loads; the halo moves to z (or r), from which every rank forms p itself
+    @property
+    def cg_fused(self) -> bool:
+        return self.dev.slab.N % 2 == 0 and os.environ.get("GNK_CG_FUSED", "1") != "0"
+
+    def cg_halo(self, z):
+        sl = self.dev.slab
+        self.comm.halo(z, sl.N, sl.nrows)
+
+    def cg_step_matvec(self, z, p_in, p_out, q, beta, first, x, xalpha) -> float:
+        self.be.cg_step_matvec(self.dvec, z, p_in, p_out, q, beta, first, x, xalpha, self._s1)
+        return float(self.comm.sum(self._s1)[0])
+
+    def cg_update_rz(self, alpha, q, r, dinv, z):
+        self.be.cg_update_xr(alpha, None, q, None, r, dinv, z, self._s2)
+        rr, rz = self.comm.sum(self._s2)
+        return float(rr), float(rz)
+
+    def cg_axpy(self, x, alpha, p):
+        self.be.vec_axpy(x, alpha, p, x, False)                     # x + alpha p (owned rows)
+
 
 class DeviceCG:
     """Device state of the CGLS solve (one rank of a Bratu slab, or a generic problem)."""
@@ -124,11 +147,13 @@ class DeviceCG:
         self.ops = ops
         v = ops.vec
         self.b, self.x, self.r, self.z, self.p, self.q = v(), v(), v(), v(), v(), v()
+        self.p2 = v() if getattr(ops, "cg_fused", False) else None   # double-buffered direction
         self.dinv = v()
         self.total_iters = 0
 
-    def solve(self, u, y, cg_rtol=1e-4, preconditioner=True, callback=None):
-        """x = argmin ||y - A x||, A = -J(u); returns (x, cg_iter) like ref:gauss_newton.py:11-60."""
+    def solve(self, u, y, cg_rtol=1e-4, preconditioner=True, callback=None, maxiter=None):
+        """x = argmin ||y - A x||, A = -J(u); returns (x, cg_iter) like ref:gauss_newton.py:11-60.
+        ``maxiter`` (tooling, bench.py) caps each CG run below scipy's 10 n."""
         ops = self.ops
         ops.cg_rhs(u, y, self.b)                                    # b = A.T @ y
         ops.cg_prepare(u)
@@ -140,15 +165,17 @@ class DeviceCG:
                 callback(self.x)
 
         if not preconditioner:
-            self._cg(cg_rtol, None, cb)                            # ref:gauss_newton.py:45-48
+            self._cg(cg_rtol, None, cb, maxiter)                   # ref:gauss_newton.py:45-48
         ops.cg_jacobi(u, self.dinv)                                # ref:gauss_newton.py:50-54
-        self._cg(cg_rtol, self.dinv, cb)                           # :56-58
+        self._cg(cg_rtol, self.dinv, cb, maxiter)                  # :56-58
         self.total_iters += count[0]
         ops.cg_finish(self.x)
         return self.x, count[0]
 
-    def _cg(self, rtol, dinv, cb):
+    def _cg(self, rtol, dinv, cb, maxiter=None):
         """scipy iterative.py:305-422 with x0 = 0, atol = 0."""
+        if self.p2 is not None:
+            return self._cg_fused(rtol, dinv, cb, maxiter)
         ops = self.ops
         bnrm2 = math.sqrt(ops.sumsq(self.b))
         atol = max(0.0, float(rtol) * float(bnrm2))
@@ -156,7 +183,7 @@ class DeviceCG:
         if bnrm2 == 0:
             self.x.copy_(self.b)
             return 0
-        maxiter = ops.n_global * 10
+        maxiter = ops.n_global * 10 if maxiter is None else min(int(maxiter), ops.n_global * 10)
         self.r.copy_(self.b)
         self.p.zero_()
         self.q.zero_()
@@ -178,6 +205,47 @@ class DeviceCG:
             rho_prev = rho
             cb()
         return maxiter
+
+    def _cg_fused(self, rtol, dinv, cb, maxiter):
+        """The same iteration (same roundings, same scalars) in two kernels: p = z + beta p, x += alpha'
+        p' (previous iteration's) and q = A^T A p with p.q; then r -= alpha q, z = M r, r.r, r.z.
+        The last x update is applied after the loop."""
+        ops = self.ops
+        bnrm2 = math.sqrt(ops.sumsq(self.b))
+        atol = max(0.0, float(rtol) * float(bnrm2))
+        self.x.zero_()
+        if bnrm2 == 0:
+            self.x.copy_(self.b)
+            return 0
+        maxiter = ops.n_global * 10 if maxiter is None else min(int(maxiter), ops.n_global * 10)
+        self.r.copy_(self.b)
+        self.p.zero_()
+        self.p2.zero_()
+        self.q.zero_()
+        rr, rz = ops.cg_update_rz(0.0, self.q, self.r, dinv, self.z)
+        z = self.z if dinv is not None else self.r
+        ops.cg_halo(z)
+        p_in, p_out = self.p, self.p2
+        rho_prev = alpha_prev = None
+        done = maxiter
+        for iteration in range(maxiter):
+            if math.sqrt(rr) < atol:
+                done = iteration
+                break
+            rho = rz
+            if iteration > 0:
+                pq = ops.cg_step_matvec(z, p_in, p_out, self.q, rho / rho_prev, False, self.x, alpha_prev)
+            else:
+                pq = ops.cg_step_matvec(z, p_in, p_out, self.q, 0.0, True, None, 0.0)
+            alpha = rho / pq
+            rr, rz = ops.cg_update_rz(alpha, self.q, self.r, dinv, self.z)
+            ops.cg_halo(z)
+            rho_prev, alpha_prev = rho, alpha
+            p_in, p_out = p_out, p_in
+            cb()
+        if alpha_prev is not None:
+            ops.cg_axpy(self.x, alpha_prev, p_in)                       # the last x += alpha p
+        return done
 
 
 def cg_least_squares(A, y, x0=None, cg_rtol=1e-4, preconditioner=True):

@@ -129,7 +129,15 @@ int gnk_gram(gnk_ctx* ctx, const double* u, const double* V, int64_t ldv, int k,
  * pq_out[0] = p . q over owned rows        ref:gauss_newton.py:36, scipy iterative.py:411-412 */
 int gnk_cg_normal_matvec(gnk_ctx* ctx, const double* d, const double* p, double* q,
                          double* pq_out);
-/* x += alpha p ; r -= alpha q ; z = dinv * r (or r if dinv NULL);
+/* One CG iteration's direction update + normal matvec in one pass (N even):
+ * p_out = z (first) or p_in * beta + z on owned and slab ghost rows (z's ghost rows
+ * exchanged), q = J.T (J p_out), pq_out[0] = p_out . q (owned); if x != NULL also
+ * x += xalpha * p_in on owned rows (the previous iteration's update, applied one
+ * iteration late).  p_out must not alias p_in.   scipy iterative.py:401-415 */
+int gnk_cg_step_matvec(gnk_ctx* ctx, const double* d, const double* z, const double* p_in,
+                       double* p_out, double* q, double beta, int first, double* x,
+                       double xalpha, double* pq_out);
+/* x += alpha p (skipped when x is NULL) ; r -= alpha q ; z = dinv * r (or r if dinv NULL);
  * out = {r . r, r . z} (owned)              scipy iterative.py:401-415 */
 int gnk_cg_update_xr(gnk_ctx* ctx, double alpha, const double* p, const double* q,
                      double* x, double* r, const double* dinv, double* z, double* out);

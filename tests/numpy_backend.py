@@ -286,10 +286,21 @@ class NumpyBackend:
         own = slice(GHOST * self.N, (GHOST + self.nrows) * self.N)
         pq[0] = float(np.dot(p.numpy()[own], q.numpy()[own]))
 
+    def cg_step_matvec(self, d, z, p_in, p_out, q, beta, first, x, xalpha, pq):
+        # p_out on every slab row (owned + ghost, as the kernel's boundary ranges), lagged x update
+        own = slice(GHOST * self.N, (GHOST + self.nrows) * self.N)
+        pi, pv, zv = p_in.numpy(), p_out.numpy(), z.numpy()
+        pv[:] = zv if first else pi * beta + zv
+        if x is not None:
+            xv = x.numpy()
+            xv[own] = xv[own] + xalpha * pi[own]
+        self.cg_matvec(d, p_out, q, pq)
+
     def cg_update_xr(self, alpha, p, q, x, r, dinv, z, out):
         own = slice(GHOST * self.N, (GHOST + self.nrows) * self.N)
-        xv, rv = x.numpy(), r.numpy()
-        xv[own] = xv[own] + alpha * p.numpy()[own]
+        xv, rv = (x.numpy() if x is not None else None), r.numpy()
+        if xv is not None:
+            xv[own] = xv[own] + alpha * p.numpy()[own]
         rv[own] = rv[own] - alpha * q.numpy()[own]
         if dinv is not None:
             z.numpy()[own] = 0.0 + dinv.numpy()[own] * rv[own]

@@ -279,6 +279,39 @@ def test_cg_matvec_matches_two_pass(N, monkeypatch):
     np.testing.assert_allclose(pq0.item(), pq.item(), rtol=1e-13)
 
 
+@pytest.mark.parametrize("N", [24, 100, 640])
+@pytest.mark.parametrize("first", [True, False])
+def test_cg_step_matvec_fused(N, first):
+    """p_out = z + beta p_in (or z), x += alpha' p_in, q = J^T J p_out in one kernel: bit-identical to
+    cg_update_p + cg_normal_matvec + the x update of cg_update_xr, ghost rows of p_out included."""
+    prob, dev, ref = make(N)
+    be = dev.backend
+    rng = np.random.default_rng(N + first)
+    n = N * N
+    u = 0.3 * rng.standard_normal(n)
+    us = dev.load(u)
+    d = dev.vec()
+    be.jdiag(us, d)
+    z, p_in, x = (dev.load(rng.standard_normal(n)) for _ in range(3))
+    beta, xalpha = 0.37, -1.3
+    p_out, q, pq = dev.vec(), dev.vec(), dev.scalar(1)
+    x_f = x.clone()
+    be.cg_step_matvec(d, z, p_in, p_out, q, beta, first, None if first else x_f, xalpha, pq)
+    # unfused reference sequence on the GPU
+    p_ref = p_in.clone()
+    be.cg_update_p(beta, first, z, p_ref)
+    q_ref, pq_ref = dev.vec(), dev.scalar(1)
+    be.cg_matvec(d, p_ref, q_ref, pq_ref)
+    np.testing.assert_array_equal(p_out.cpu().numpy(), p_ref.cpu().numpy())    # whole slab (ghosts = 0)
+    np.testing.assert_array_equal(own(dev, q), own(dev, q_ref))
+    assert pq.item() == pq_ref.item()
+    if not first:
+        x_ref = x.clone()
+        zero = dev.vec()
+        be.cg_update_xr(xalpha, p_in, zero, x_ref, dev.vec(), None, dev.vec(), dev.scalar(2))
+        np.testing.assert_array_equal(own(dev, x_f), own(dev, x_ref))
+
+
 def test_cg_updates():
     prob, dev, ref = make(64)
     be = dev.backend
