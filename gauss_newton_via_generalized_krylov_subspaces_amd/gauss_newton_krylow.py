@@ -86,6 +86,13 @@ class BratuOps:
         self.be.residual(x, self.y, r, self._n2)
         return float(self.comm.sum(self._n2)[0])
 
+    def residual_with_stats(self, x, r, pack):
+        """residual partial into pack[0] next to the speculative CGS stats pack[1:3]: one
+        collective / host read for (sum r^2, (sum g^2, max |g|))."""
+        self.be.residual(x, self.y, r, pack[0:1])
+        sums, mx = self.comm.sum_and_max(pack, 2)
+        return float(sums[0]), (float(sums[1]), mx)
+
     def to_host(self, x):
         return self.dev.slab.to_host(x)
 
@@ -182,10 +189,16 @@ class GNKSolver:
         # computed from the same read of V as the trial point itself (speculative; a rejected
         # first trial falls back to the separate update products)
         fuse = self.ops.fuse_trial and self.version == "res_old" and 1 <= basis.k <= basis.FUSE_KMAX
+        # ... and its CGS step too, read with the trial's residual (one sync instead of two)
+        spec_cgs = fuse and hasattr(self.ops, "residual_with_stats") and basis.k < basis.kmax
 
         def trial(t):
             if fuse and not last:
                 basis.x_with_update_products(self.c + t * d, r_old, x_t)  # res_krylow(x + t d)
+                if spec_cgs:
+                    pack = basis.cgs_speculative()
+                    last["rr"], last["stats"] = self.ops.residual_with_stats(x_t, r_t, pack)
+                    return last["rr"]
             else:
                 basis.x(self.c + t * d, x_t)
             last["rr"] = self._residual(x_t, r_t)
@@ -210,7 +223,8 @@ class GNKSolver:
         u_new = self.xb[self.uJ]      # the next LS solve's J; s = ||J(u_new) v_new|| (lls.py)
         try:
             if self.version == "res_old":
-                s_new = basis.update(u_new, r_old, u_new, products_ready=products_ready)
+                spec = {"stats": last["stats"]} if products_ready and "stats" in last else {}
+                s_new = basis.update(u_new, r_old, u_new, products_ready=products_ready, **spec)
             elif self.version == "res_new":
                 s_new = basis.update(u_new, r_t, u_new)
             elif self.version == "jac_old_res_old":

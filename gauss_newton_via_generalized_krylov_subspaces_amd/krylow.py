@@ -35,6 +35,7 @@ class DeviceKrylovBasis:
         self._c = self.be.zeros(self.kmax)
         self._h = self.be.zeros(self.kmax)
         self._stats = self.be.zeros(2)
+        self._pack = self.be.zeros(3)          # [residual partial, sum g^2, max |g|] of a speculative step
         self._g = dev.vec()              # new column before normalisation (stencil source)
         self._jn2 = self.be.zeros(1)
 
@@ -79,24 +80,39 @@ class DeviceKrylovBasis:
         self.be.gemv_vjp_gemv_t(self.V, k, self._c, r, out, self._g, self._h)
         return out
 
-    def update(self, u_jac, r, u_next=None, products_ready=False):
+    def cgs_speculative(self):
+        """Right after ``x_with_update_products``: enqueue the CGS step g -= V h (+ its stats into
+        pack[1:3]) before the Armijo test has read the trial's residual, so that one host read serves
+        both (pack[0] is the caller's residual slot).  ``update(..., stats=...)`` continues from it;
+        a rejected trial recomputes g."""
+        k = self.k
+        if self.dev.comm.world > 1:
+            self._h[:k].copy_(self.dev.comm.sum_device(self._h[:k]))
+        self.be.cgs_update(self.V, k, self._h, self._g, self._pack[1:3])
+        return self._pack
+
+    def update(self, u_jac, r, u_next=None, products_ready=False, stats=None):
         """ref:krylow.py:55-73 with jac_ev = J(u_jac), res_ev = r (slab vectors).
 
         Returns ||J(u_next) v_new|| (u_next defaults to u_jac), computed in the same
         pass that normalises the new column (the next least-squares preconditioner).
-        ``products_ready``: g and h were produced by ``x_with_update_products`` at u_jac."""
+        ``products_ready``: g and h were produced by ``x_with_update_products`` at u_jac;
+        ``stats`` = (sum g^2, max |g|) when ``cgs_speculative`` has also done the CGS step."""
         k = self.k
         if k == self.dev.slab.n_global:                       # :59-60
             raise GeneralizedKrylowSubspaceSpansEntireSpace
         if k >= self.kmax:
             raise RuntimeError("Krylov basis storage exhausted")
         g = self._g
-        if not products_ready:
-            self.be.vjp_gemv_t(u_jac, r, self.V, k, g, self._h)   # g = -J^T r ; h = V^T g (:62, :64)
-        if self.dev.comm.world > 1:                           # rank-ordered sum of the partials
-            self.be.upload(self._h, self.dev.comm.sum(self._h[:k]))
-        self.be.cgs_update(self.V, k, self._h, g, self._stats)   # g -= V h (:64)
-        sumsq, maxabs = self.dev.comm.sum_max(self._stats)
+        if stats is not None and products_ready:
+            sumsq, maxabs = stats
+        else:
+            if not products_ready:
+                self.be.vjp_gemv_t(u_jac, r, self.V, k, g, self._h)   # g = -J^T r ; h = V^T g (:62, :64)
+            if self.dev.comm.world > 1:                           # rank-ordered sum of the partials
+                self._h[:k].copy_(self.dev.comm.sum_device(self._h[:k]))
+            self.be.cgs_update(self.V, k, self._h, g, self._stats)   # g -= V h (:64)
+            sumsq, maxabs = self.dev.comm.sum_max(self._stats)
         if maxabs <= 1e-8 and not math.isnan(sumsq):          # :66
             raise GeneralizedKrylowSubspaceBreakdown(
                 "Normal residual is allready inside generalized Krylow Subspcae, there for gauss newton "

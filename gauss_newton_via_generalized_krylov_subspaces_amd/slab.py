@@ -74,14 +74,37 @@ class Comm:
 
     def sum_max(self, t: torch.Tensor) -> tuple[float, float]:
         """t = [sum, max] per rank -> (sum over ranks, NaN-propagating max over ranks)."""
+        sums, m = self.sum_and_max(t, 1)
+        return float(sums[0]), m
+
+    def sum_and_max(self, t: torch.Tensor, nsum: int) -> tuple[np.ndarray, float]:
+        """t = [s_0 .. s_{nsum-1}, m] per rank -> (rank-ordered sums, NaN-propagating max): several
+        control scalars of one step in one collective and one host read."""
         parts = self._gather(t)
-        s, m = float(parts[0][0]), float(parts[0][1])
+        s = parts[0][:nsum].copy()
+        m = float(parts[0][nsum])
         for p in range(1, parts.shape[0]):
-            s = s + float(parts[p][0])
-            v = float(parts[p][1])
+            s = s + parts[p][:nsum]
+            v = float(parts[p][nsum])
             if v > m or math.isnan(v):
                 m = v
         return s, m
+
+    def sum_device(self, t: torch.Tensor) -> torch.Tensor:
+        """Rank-ordered sum of a small per-rank device tensor, left on the device (no host round
+        trip on RCCL): the same IEEE additions in the same order as ``sum``."""
+        if self.world == 1:
+            return t
+        if self.stage:
+            return torch.from_numpy(self.sum(t)).to(t.device)
+        t = t.contiguous().reshape(-1)
+        buf = torch.empty(self.world * t.numel(), dtype=t.dtype, device=t.device)
+        dist.all_gather_into_tensor(buf, t, group=self.group)
+        parts = buf.view(self.world, -1)
+        s = parts[0].clone()
+        for p in range(1, self.world):
+            s.add_(parts[p])
+        return s
 
     def barrier(self):
         if self.world > 1:
