@@ -63,18 +63,19 @@ def bratu_inputs(N, seed=42):
     return prob, u_true, u0
 
 
-def step_bytes(n, k, a, passes=1.0, fused=False):
+def step_bytes(n, k, a, passes=1.0, fused=False, pending=True):
     """Algorithmic HBM bytes of one outer iteration as implemented, in units of
-    8 n bytes (one grid vector):
-      Gram passes            passes * (k + 2)      V, u, r
-      first trial, fused     (k + 1) + 2           V -> x, plus r read / g written  (res_old)
-      other trials           a' * (k + 1)          basis GEMV
-      residual per trial     a * 3                 x, y -> r
-      update products        k + 4 unless fused    u, r, V -> g, h
-      CGS update             k + 2                 V, g -> g
-      normalise + ||J v||    3                     g, u -> v"""
-    trials = a * 3 + (a - 1) * (k + 1) + ((k + 3) if fused else (k + 1))
-    update = (0 if fused else k + 4) + (k + 2) + 3
+    8 n bytes (one grid vector); k = Gram columns (settled + the pending one), a = Armijo trials:
+      Gram passes              passes * (k + 2)          V (incl. the pending raw g), u, r
+      first trial, fused       (k + 3) + [pending]       V -> x; r_old -> g_new; + the w write-back
+      first trial, plain       (k + 1) + [pending]       V -> x (+ w write-back)
+      other trials             (a - 1) * (k + 1)         basis GEMV
+      residual per trial       a * 3                     x, y -> r
+      update products          k + 3 unless fused and a = 1   u, r, V -> g (h = V^T g)
+    (deferred Gram-Schmidt: no separate CGS or normalisation pass)"""
+    first = (k + 3 if fused else k + 1) + (1 if pending else 0)
+    trials = first + (a - 1) * (k + 1) + 3 * a
+    update = 0 if (fused and a == 1) else k + 3
     return 8.0 * n * (passes * (k + 2) + trials + update)
 
 
@@ -231,7 +232,7 @@ def main():
     passes = solver.lls.passes - passes0
     ppi = passes / max(len(tr), 1)
     fuse_ok = args.version == "res_old"
-    total_bytes = sum(step_bytes(n, s["k"], s["trials"], ppi, fused=fuse_ok and s["trials"] == 1 and s["k"] <= 24)
+    total_bytes = sum(step_bytes(n, s["k"], s["trials"], ppi, fused=fuse_ok and s["k"] <= 24, pending=s["k"] > 1)
                       for s in tr)
     # dominant kernel: Gram pass (per-launch events; bytes are this rank's slab)
     g_ms = [m for m, _ in launches]

@@ -54,6 +54,9 @@ SIGNATURES = {
     "gnk_csr_spmv": (_c_int, [_c_vp, _c_i64, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_int]),
     "gnk_flat_gram": (_c_int, [_c_vp, _c_vp, _c_i64, _c_int, _c_vp, _c_i64, _c_vp, _c_i64, _c_vp]),
     "gnk_basis_gemv_vjp_gemv_t": (_c_int, [_c_vp, _c_vp, _c_i64, _c_int, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp]),
+    "gnk_basis_gemv_pending": (_c_int, [_c_vp, _c_vp, _c_i64, _c_int, _c_vp, _c_vp, _c_vp, _c_vp]),
+    "gnk_basis_gemv_vjp_gemv_t_pending": (_c_int, [_c_vp, _c_vp, _c_i64, _c_int, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp,
+                                                   _c_vp, _c_vp]),
     "gnk_normalize_jnorm": (_c_int, [_c_vp, _c_vp, _c_vp, _c_dbl, _c_vp, _c_vp]),
     "gnk_vec_axpy": (_c_int, [_c_vp, _c_vp, _c_dbl, _c_vp, _c_vp, _c_int]),
     "gnk_gram_padded_dim": (_c_int, [_c_int, _c_int]),
@@ -214,6 +217,14 @@ class HipBackend:
 
     def gemv_vjp_gemv_t(self, V, k, c, r, x, g, h):
         self._call("gnk_basis_gemv_vjp_gemv_t", _p(V), V.stride(0), int(k), _p(c), _p(r), _p(x), _p(g), _p(h))
+
+    def gemv_pending(self, V, k, c, hh, x, stats):
+        """column k of V is the pending raw column: materialised in place (see gnk.h)"""
+        self._call("gnk_basis_gemv_pending", _p(V), V.stride(0), int(k), _p(c), _p(hh), _p(x), _p(stats))
+
+    def gemv_vjp_gemv_t_pending(self, V, k, c, hh, r, x, g, h, stats):
+        self._call("gnk_basis_gemv_vjp_gemv_t_pending", _p(V), V.stride(0), int(k), _p(c), _p(hh), _p(r), _p(x),
+                   _p(g), _p(h), _p(stats))
 
     # -- flat vectors (generic problems) --------------------------------------------------
     def flat_gemv(self, V, k, c, x):

@@ -299,6 +299,81 @@ __global__ __launch_bounds__(BLOCK) void k_gemv(const double* __restrict__ V, in
   ROW_LOOP_END
 }
 
+// block-wide {sum, NaN-propagating max} -> partial[2 blk], partial[2 blk + 1]
+__device__ __forceinline__ void block_sum_max_store(double ss, double mx, double* __restrict__ partial) {
+  __shared__ double shm[BLOCK / 64][2];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  ss = wave_sum(ss);
+  mx = wave_max(mx);
+  if (lane == 0) { shm[wave][0] = ss; shm[wave][1] = mx; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double a = shm[0][0], b = shm[0][1];
+    for (int w = 1; w < BLOCK / 64; ++w) { a += shm[w][0]; b = nan_max(b, shm[w][1]); }
+    const size_t blk = blockIdx.y * gridDim.x + blockIdx.x;
+    partial[2 * blk] = a;
+    partial[2 * blk + 1] = b;
+  }
+}
+
+// Trial point with the pending basis column materialised (deferred CGS of krylow.py:64):
+//   w = g - V[:, :k] @ hh        in place over column k (= g), whole slab, the rounding of k_cgs;
+//   x = V[:, :k] @ c[:k] + w c[k]   the rounding of k_gemv over k + 1 columns;
+//   partial {sum w^2, max |w|} over owned rows (the norm and breakdown test of krylow.py:66, 71).
+// Column k is read and written only through `w` (never through V).
+template <int VEC>
+__global__ __launch_bounds__(BLOCK) void k_gemv_p(const double* __restrict__ V, int64_t ldv, int k,
+                                                  const double* __restrict__ cvec, const double* __restrict__ hh,
+                                                  double* __restrict__ w, double* __restrict__ x, Geo geo,
+                                                  int64_t lr0, int64_t nlr, double* __restrict__ partial) {
+  double ss = 0.0, mx = 0.0;
+  const double ck = cvec[k];
+  ROW_LOOP_BEGIN(VEC)
+  const bool owned = lr >= G && lr < G + geo.nrows;       // block-uniform
+  if (VEC == 2 && iy + 1 < N) {
+    d2 acc = {0.0, 0.0}, s = {0.0, 0.0};
+    for (int j = 0; j < k; ++j) {
+      const d2 vv = *reinterpret_cast<const d2*>(V + j * ldv + li);
+      const double cj = cvec[j], hj = hh[j];
+      acc.x = acc.x + vv.x * cj;
+      acc.y = acc.y + vv.y * cj;
+      s.x = s.x + vv.x * hj;
+      s.y = s.y + vv.y * hj;
+    }
+    d2 ww = *reinterpret_cast<const d2*>(w + li);
+    ww.x = ww.x - s.x;
+    ww.y = ww.y - s.y;
+    *reinterpret_cast<d2*>(w + li) = ww;
+    acc.x = acc.x + ww.x * ck;
+    acc.y = acc.y + ww.y * ck;
+    *reinterpret_cast<d2*>(x + li) = acc;
+    if (owned) {
+      ss += ww.x * ww.x;
+      ss += ww.y * ww.y;
+      mx = nan_max(mx, fabs(ww.x));
+      mx = nan_max(mx, fabs(ww.y));
+    }
+  } else {
+    for (int q = 0; q < VEC && iy + q < N; ++q) {
+      double acc = 0.0, s = 0.0;
+      for (int j = 0; j < k; ++j) {
+        const double vv = V[j * ldv + li + q];
+        acc = acc + vv * cvec[j];
+        s = s + vv * hh[j];
+      }
+      const double wi = w[li + q] - s;
+      w[li + q] = wi;
+      x[li + q] = acc + wi * ck;
+      if (owned) {
+        ss += wi * wi;
+        mx = nan_max(mx, fabs(wi));
+      }
+    }
+  }
+  ROW_LOOP_END
+  block_sum_max_store(ss, mx, partial);
+}
+
 // g = -(J^T r) on owned rows (chunk 0 stores it), h[j0 + j] partial = V_j . g.
 // KCT columns per chunk (compile time): every V load is unconditional (clamped column),
 // surplus accumulators are discarded by the block reduction (no loads under a branch).
@@ -364,26 +439,58 @@ __global__ __launch_bounds__(BLOCK) void k_vjp_gemv_t(const double* __restrict__
 // from ONE read of V (k_gemv + k_vjp_gemv_t read it twice and read u = x back).
 // One chunk of KCT >= k columns; surplus columns are clamped loads with c = 0 and discarded
 // partials (no loads under a branch).
-template <int VEC, int KCT>
+// PEND: column k is the pending (raw) basis column g_k of the deferred CGS; it is materialised
+// in place first, w = g_k - V[:, :k] @ hh (the rounding of k_cgs: hh_j = 0 past k adds zeros),
+// and then enters x and h as column k (k + 1 columns, h partials for all of them); spart gets
+// {sum w^2, max |w|} over owned rows.
+template <int VEC, int KCT, bool PEND>
 __global__ __launch_bounds__(BLOCK) void k_gemv_vjpg(const double* __restrict__ V, int64_t ldv, int k,
-                                                     const double* __restrict__ cvec, const double* __restrict__ r,
+                                                     const double* __restrict__ cvec, const double* __restrict__ hh,
+                                                     double* __restrict__ wcol, const double* __restrict__ r,
                                                      double* __restrict__ x, double* __restrict__ g, Geo geo, Coef c,
-                                                     int64_t lr0, int64_t nlr, double* __restrict__ partial) {
+                                                     int64_t lr0, int64_t nlr, double* __restrict__ partial,
+                                                     double* __restrict__ spart) {
   __shared__ double sh[(BLOCK / 64) * KCT];
   const int lane = threadIdx.x & 63;
-  const int jmax = k - 1;
-  double cj[KCT];
+  const int kk = PEND ? k + 1 : k;                  // columns entering x and h
+  const int jmax = PEND ? k - 1 : kk - 1;           // last column read through V (>= 0: k >= 1)
+  double cj[KCT], hj[KCT];
 #pragma unroll
-  for (int j = 0; j < KCT; ++j) cj[j] = j < k ? cvec[j] : 0.0;
+  for (int j = 0; j < KCT; ++j) {
+    cj[j] = j < kk ? cvec[j] : 0.0;
+    hj[j] = (PEND && j < k) ? hh[j] : 0.0;
+  }
   double acc[KCT];
 #pragma unroll
   for (int j = 0; j < KCT; ++j) acc[j] = 0.0;
+  double ss = 0.0, mx = 0.0;
   ROW_LOOP_BEGIN(VEC)
   const bool owned = lr >= G && lr < G + geo.nrows;       // block-uniform
   if (VEC == 2 && iy + 1 < N) {
     d2 vv[KCT];
 #pragma unroll
     for (int j = 0; j < KCT; ++j) vv[j] = *reinterpret_cast<const d2*>(V + min(j, jmax) * ldv + li);
+    if (PEND) {
+      d2 s = {0.0, 0.0};
+#pragma unroll
+      for (int j = 0; j < KCT; ++j) {
+        s.x = s.x + vv[j].x * hj[j];
+        s.y = s.y + vv[j].y * hj[j];
+      }
+      d2 ww = *reinterpret_cast<const d2*>(wcol + li);
+      ww.x = ww.x - s.x;
+      ww.y = ww.y - s.y;
+      *reinterpret_cast<d2*>(wcol + li) = ww;
+#pragma unroll
+      for (int j = 0; j < KCT; ++j)
+        if (j == k) vv[j] = ww;
+      if (owned) {
+        ss += ww.x * ww.x;
+        ss += ww.y * ww.y;
+        mx = nan_max(mx, fabs(ww.x));
+        mx = nan_max(mx, fabs(ww.y));
+      }
+    }
     d2 xs = {0.0, 0.0};
 #pragma unroll
     for (int j = 0; j < KCT; ++j) {
@@ -416,12 +523,25 @@ __global__ __launch_bounds__(BLOCK) void k_gemv_vjpg(const double* __restrict__ 
       const int64_t yy = iy + q;
       if (yy >= N) break;
       double vv[KCT];
+#pragma unroll
+      for (int j = 0; j < KCT; ++j) vv[j] = V[min(j, jmax) * ldv + i];
+      if (PEND) {
+        double s = 0.0;
+#pragma unroll
+        for (int j = 0; j < KCT; ++j) s = s + vv[j] * hj[j];
+        const double wi = wcol[i] - s;
+        wcol[i] = wi;
+#pragma unroll
+        for (int j = 0; j < KCT; ++j)
+          if (j == k) vv[j] = wi;
+        if (owned) {
+          ss += wi * wi;
+          mx = nan_max(mx, fabs(wi));
+        }
+      }
       double xs = 0.0;
 #pragma unroll
-      for (int j = 0; j < KCT; ++j) {
-        vv[j] = V[min(j, jmax) * ldv + i];
-        xs = xs + vv[j] * cj[j];
-      }
+      for (int j = 0; j < KCT; ++j) xs = xs + vv[j] * cj[j];
       x[i] = xs;
       if (owned) {
         const bool hw = yy > 0, he = yy < N - 1;
@@ -434,7 +554,8 @@ __global__ __launch_bounds__(BLOCK) void k_gemv_vjpg(const double* __restrict__ 
     }
   }
   ROW_LOOP_END
-  block_sum_store<KCT>(acc, k, partial + size_t(blockIdx.y * gridDim.x + blockIdx.x) * KCT, sh);
+  block_sum_store<KCT>(acc, kk, partial + size_t(blockIdx.y * gridDim.x + blockIdx.x) * KCT, sh);
+  if (PEND) block_sum_max_store(ss, mx, spart);
 }
 
 // g -= V[:, :k] @ h ; partial {sum g^2, max|g|}
@@ -2215,19 +2336,31 @@ int gnk_vjp_gemv_t(gnk_ctx* ctx, const double* u, const double* r, const double*
   return wreduce(ctx, ctx->scratch, nblk, k, kct, kct, int64_t(nblk) * kct, nullptr, h_out);
 }
 
-int gnk_basis_gemv_vjp_gemv_t(gnk_ctx* ctx, const double* V, int64_t ldv, int k, const double* c, const double* r,
-                              double* x, double* g, double* h_out) {
-  if (!ready(ctx)) return -1;
-  if (k < 1 || k > 24) return fail(ctx, "basis_gemv_vjp_gemv_t: k must be in [1, 24]");
-  if (!V || !c || !r || !x || !g || !h_out) return fail(ctx, "basis_gemv_vjp_gemv_t: NULL argument");
-  if (vec_of(ctx) == 2 && (ldv % 2 != 0)) return fail(ctx, "basis_gemv_vjp_gemv_t: ldv must be even");
-  const int kct = std::max(4, (k + 3) / 4 * 4);
+// shared body of gnk_basis_gemv_vjp_gemv_t (hh == nullptr) and its pending-column form
+static int gemv_vjpg_launch(gnk_ctx* ctx, const char* what, const double* V, int64_t ldv, int k, const double* c,
+                     const double* hh, const double* r, double* x, double* g, double* h_out, double* stats_out) {
+  const bool pend = hh != nullptr;
+  const int kk = k + (pend ? 1 : 0);
+  if (k < 1 || kk > 24) return fail(ctx, std::string(what) + ": columns must be in [1, 24]");
+  if (!V || !c || !r || !x || !g || !h_out || (pend && !stats_out)) return fail(ctx, std::string(what) + ": NULL argument");
+  if (vec_of(ctx) == 2 && (ldv % 2 != 0)) return fail(ctx, std::string(what) + ": ldv must be even");
+  double* wcol = pend ? const_cast<double*>(V) + int64_t(k) * ldv : nullptr;
+  if (pend && (g == wcol || x == wcol)) return fail(ctx, std::string(what) + ": g / x alias the pending column");
+  const int kct = std::max(4, (kk + 3) / 4 * 4);
   RowLaunch L = rows(ctx, 0, ctx->geo.nrows + 2 * G, vec_of(ctx), 2048);
   const int nblk = L.grid.x * L.grid.y;
-  if (size_t(nblk) * kct > SCRATCH_DOUBLES) return fail(ctx, "basis_gemv_vjp_gemv_t: scratch too small");
-#define GVJ_LAUNCH(V_, K_)                                                                                    \
-  hipLaunchKernelGGL((k_gemv_vjpg<V_, K_>), L.grid, dim3(BLOCK), 0, ctx->stream, V, ldv, k, c, r, x, g, ctx->geo, \
-                     ctx->coef, L.lr0, L.nlr, ctx->scratch)
+  const size_t soff = (size_t(nblk) * kct + 1) & ~size_t(1);     // stats partials after the h partials
+  if (soff + 2 * size_t(nblk) > SCRATCH_DOUBLES / 2) return fail(ctx, std::string(what) + ": scratch too small");
+  double* spart = ctx->scratch + soff;
+#define GVJ_LAUNCH(V_, K_)                                                                                     \
+  do {                                                                                                         \
+    if (pend)                                                                                                  \
+      hipLaunchKernelGGL((k_gemv_vjpg<V_, K_, true>), L.grid, dim3(BLOCK), 0, ctx->stream, V, ldv, k, c, hh,   \
+                         wcol, r, x, g, ctx->geo, ctx->coef, L.lr0, L.nlr, ctx->scratch, spart);               \
+    else                                                                                                       \
+      hipLaunchKernelGGL((k_gemv_vjpg<V_, K_, false>), L.grid, dim3(BLOCK), 0, ctx->stream, V, ldv, k, c, hh,  \
+                         wcol, r, x, g, ctx->geo, ctx->coef, L.lr0, L.nlr, ctx->scratch, spart);               \
+  } while (0)
 #define GVJ_SWITCH(V_)                  \
   switch (kct) {                        \
     case 4: GVJ_LAUNCH(V_, 4); break;   \
@@ -2244,9 +2377,41 @@ int gnk_basis_gemv_vjp_gemv_t(gnk_ctx* ctx, const double* V, int64_t ldv, int k,
   }
 #undef GVJ_SWITCH
 #undef GVJ_LAUNCH
-  int rc = check_launch(ctx, "basis_gemv_vjp_gemv_t");
+  int rc = check_launch(ctx, what);
   if (rc) return rc;
-  return wreduce(ctx, ctx->scratch, nblk, k, kct, kct, int64_t(nblk) * kct, nullptr, h_out);
+  rc = wreduce(ctx, ctx->scratch, nblk, kk, kct, kct, int64_t(nblk) * kct, nullptr, h_out);
+  if (rc || !pend) return rc;
+  return reduce(ctx, spart, nblk, 2, 2, sum_max_flags(), stats_out);
+}
+
+int gnk_basis_gemv_vjp_gemv_t(gnk_ctx* ctx, const double* V, int64_t ldv, int k, const double* c, const double* r,
+                              double* x, double* g, double* h_out) {
+  if (!ready(ctx)) return -1;
+  return gemv_vjpg_launch(ctx, "basis_gemv_vjp_gemv_t", V, ldv, k, c, nullptr, r, x, g, h_out, nullptr);
+}
+
+int gnk_basis_gemv_vjp_gemv_t_pending(gnk_ctx* ctx, const double* V, int64_t ldv, int k, const double* c,
+                                      const double* hh, const double* r, double* x, double* g, double* h_out,
+                                      double* stats_out) {
+  if (!ready(ctx)) return -1;
+  if (!hh) return fail(ctx, "basis_gemv_vjp_gemv_t_pending: hh is NULL");
+  return gemv_vjpg_launch(ctx, "basis_gemv_vjp_gemv_t_pending", V, ldv, k, c, hh, r, x, g, h_out, stats_out);
+}
+
+int gnk_basis_gemv_pending(gnk_ctx* ctx, const double* V, int64_t ldv, int k, const double* c, const double* hh,
+                           double* x, double* stats_out) {
+  if (!ready(ctx)) return -1;
+  if (k < 1) return fail(ctx, "basis_gemv_pending: k < 1");
+  if (!V || !c || !hh || !x || !stats_out) return fail(ctx, "basis_gemv_pending: NULL argument");
+  if (vec_of(ctx) == 2 && (ldv % 2 != 0)) return fail(ctx, "basis_gemv_pending: ldv must be even");
+  double* w = const_cast<double*>(V) + int64_t(k) * ldv;
+  if (x == w) return fail(ctx, "basis_gemv_pending: x aliases the pending column");
+  RowLaunch L = rows(ctx, 0, ctx->geo.nrows + 2 * G, vec_of(ctx), 2048);
+  const int nblk = L.grid.x * L.grid.y;
+  DISPATCH_VEC(ctx, k_gemv_p, L, 0, V, ldv, k, c, hh, w, x, ctx->geo, L.lr0, L.nlr, ctx->scratch);
+  int rc = check_launch(ctx, "basis_gemv_pending");
+  if (rc) return rc;
+  return reduce(ctx, ctx->scratch, nblk, 2, 2, sum_max_flags(), stats_out);
 }
 
 int gnk_cgs_update(gnk_ctx* ctx, const double* V, int64_t ldv, int k, const double* h, double* g,

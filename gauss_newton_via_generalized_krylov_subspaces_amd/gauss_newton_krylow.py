@@ -86,12 +86,11 @@ class BratuOps:
         self.be.residual(x, self.y, r, self._n2)
         return float(self.comm.sum(self._n2)[0])
 
-    def residual_with_stats(self, x, r, pack):
-        """residual partial into pack[0] next to the speculative CGS stats pack[1:3]: one
-        collective / host read for (sum r^2, (sum g^2, max |g|))."""
+    def residual_pack(self, x, r, pack):
+        """residual partial into pack[0] beside a first trial's device stats (pack[1] = sum w^2,
+        pack[2] = max |w|, pack[3:] = V^T g partials): one collective and one host read for all."""
         self.be.residual(x, self.y, r, pack[0:1])
-        sums, mx = self.comm.sum_and_max(pack, 2)
-        return float(sums[0]), (float(sums[1]), mx)
+        return self.comm.sum_except_max(pack, 2)
 
     def to_host(self, x):
         return self.dev.slab.to_host(x)
@@ -157,14 +156,11 @@ class GNKSolver:
         self.done = False
         self.uJ = 0                                        # J is evaluated at x0 (:78)
         self.xb[0].copy_(self.ops.load(x0))
-        if self.ops.jacobian_is_free:
-            self.c, s0 = self.basis.start(self.xb[0], self.xb[self.uJ])   # :71 (+ ||J(x0) v_0||)
-            self.lls.on_restart(s0)
-        else:
-            self.c = self.basis.start(self.xb[0])                         # :71
-            self.lls.on_restart(None)
+        self.c = self.basis.start(self.xb[0])              # :71
+        self.e = self.c.copy()                             # stored-unit coordinates (krylow.py)
+        self.lls.on_restart()
         xi = self._free_x(self.uJ)
-        self.basis.x(self.c, self.xb[xi])
+        self.basis.x(self.e, self.xb[xi])
         if self.rb is None:
             self.rb = [self.ops.rvec() for _ in range(2)]
         self.ri = 0
@@ -175,6 +171,52 @@ class GNKSolver:
         if self.max_iter < 2:
             raise UnboundLocalError("local variable 'iter' referenced before assignment")
 
+    def _breakdown_message(self, it):
+        print(f"Generalized krylow subspace breakdown at iteration = {it}, basis.shape = {self.basis.shape}")
+
+    def _append_coordinate(self):
+        self.c = np.append(self.c, 0)                                     # :124
+        self.e = np.append(self.e, 0)
+
+    def _settle_explicit(self):
+        """A pending column that no trial will settle (restart, end of the loop): its breakdown test
+        and message belong to the iteration that appended it (ref:krylow.py:66, gnk:126-129)."""
+        basis = self.basis
+        it = basis.pend["it"]
+        if basis.resolve_explicit():
+            self._breakdown_message(it)
+        else:
+            self._append_coordinate()
+
+    def _first_trial(self, d, jdd, x_t, r_t, r_old, fuse):
+        """Armijo trial t = 1 (ref:armijo_goldstein.py:56).  Settles a pending basis column first --
+        on its breakdown the least-squares solve is redone without it -- and, for the fused res_old
+        path, computes the basis-update products at the trial point.
+        Returns (d, jdd, ds, sum r_t^2, raw h or None); ds = d in stored units."""
+        basis = self.basis
+        while True:
+            kk = basis.gram_k()
+            ds = basis.stored_step(d)
+            e_try = np.append(self.e, np.zeros(kk - len(self.e))) + 1.0 * ds
+            prod = fuse and kk <= basis.FUSE_KMAX
+            pend = basis.pending
+            if not (prod or pend):
+                basis.x(e_try, x_t)
+                return d, jdd, ds, self._residual(x_t, r_t), None
+            pack = basis.trial_first(e_try, x_t, r_old if prod else None)
+            host = self.ops.residual_pack(x_t, r_t, pack[:3 + kk])
+            if pend:
+                it = basis.pend["it"]
+                if basis.resolve(float(host[1]), float(host[2])):
+                    # ref:krylow.py:66-69 raised in iteration `it`: the basis was not enlarged
+                    self._breakdown_message(it)
+                    self.lls.discard_pending()
+                    d, jdd, _ = self.lls.solve(self.xb[self.uJ], basis, r_old)
+                    continue
+                self._append_coordinate()                                 # :124 of iteration `it`
+                d = self.lls.resolve_pending(basis.last_norm)
+            return d, jdd, ds, float(host[0]), (host[3:3 + basis.k].copy() if prod else None)
+
     def step(self) -> bool:
         """One pass of ref:gauss_newton_krylow.py:84-136; returns True when the loop has ended."""
         it = self.iter + 1
@@ -184,31 +226,25 @@ class GNKSolver:
         xi = self._free_x(self.uJ)
         rti = 1 - self.ri
         x_t, r_t = self.xb[xi], self.rb[rti]
-        last = {}
         # res_old: the update after an accepted first trial is g = -J(x_t)^T r_old, h = V^T g --
-        # computed from the same read of V as the trial point itself (speculative; a rejected
-        # first trial falls back to the separate update products)
-        fuse = self.ops.fuse_trial and self.version == "res_old" and 1 <= basis.k <= basis.FUSE_KMAX
-        # ... and its CGS step too, read with the trial's residual (one sync instead of two)
-        spec_cgs = fuse and hasattr(self.ops, "residual_with_stats") and basis.k < basis.kmax
+        # computed from the same read of V as the trial point itself (speculative)
+        fuse = self.ops.fuse_trial and self.version == "res_old"
+        d, jdd, ds, rr1, h1 = self._first_trial(d, jdd, x_t, r_t, r_old, fuse)
+        last = {"rr": rr1}
 
-        def trial(t):
-            if fuse and not last:
-                basis.x_with_update_products(self.c + t * d, r_old, x_t)  # res_krylow(x + t d)
-                if spec_cgs:
-                    pack = basis.cgs_speculative()
-                    last["rr"], last["stats"] = self.ops.residual_with_stats(x_t, r_t, pack)
-                    return last["rr"]
-            else:
-                basis.x(self.c + t * d, x_t)
+        def trial(t):                                                     # res_krylow(c + t d)
+            if t == 1.0 and "first" not in last:
+                last["first"] = True
+                return rr1
+            basis.x(self.e + t * ds, x_t)
             last["rr"] = self._residual(x_t, r_t)
             return last["rr"]
 
         t, ntrial = armijo_device(trial, self.rr, jdd, d)                 # :91-93
-        products_ready = fuse and ntrial == 1
         self.nfev += ntrial                                               # :94
         s = np.sum(self.c ** 2)                                           # :96
         self.c += t * d                                                   # :98
+        self.e = self.e + t * ds              # the coefficients of the accepted trial point, bit for bit
         self.trace.append({"t": t, "k": basis.k, "trials": ntrial})
         self._emit(x_t)                                                   # :100
         self.iter = it
@@ -220,36 +256,41 @@ class GNKSolver:
         uJ_old, self.uJ = self.uJ, xi                                     # :106-108
         self.ops.on_jacobian(self.xb[self.uJ])
         self.njev += 1
-        u_new = self.xb[self.uJ]      # the next LS solve's J; s = ||J(u_new) v_new|| (lls.py)
+        u_new = self.xb[self.uJ]
+        products = h1 if (h1 is not None and ntrial == 1) else None
         try:
             if self.version == "res_old":
-                spec = {"stats": last["stats"]} if products_ready and "stats" in last else {}
-                s_new = basis.update(u_new, r_old, u_new, products_ready=products_ready, **spec)
+                basis.update(u_new, r_old, it=it, products=products)
             elif self.version == "res_new":
-                s_new = basis.update(u_new, r_t, u_new)
+                basis.update(u_new, r_t, it=it)
             elif self.version == "jac_old_res_old":
-                s_new = basis.update(self.xb[uJ_old], r_old, u_new)
+                basis.update(self.xb[uJ_old], r_old, it=it)
             elif self.version == "jac_old_res_new":
-                s_new = basis.update(self.xb[uJ_old], r_t, u_new)
+                basis.update(self.xb[uJ_old], r_t, it=it)
             else:
                 raise ValueError(
                     "Variable version must be in ['res_old','res_new','jac_old_res_old','jac_old_res_new']")
-            self.c = np.append(self.c, 0)                                 # :124
-            self.lls.on_append(s_new)
+            if not basis.deferred:
+                self._append_coordinate()                                 # :124
+                self.lls.on_append()
         except GeneralizedKrylowSubspaceBreakdown:
-            print(f"Generalized krylow subspace breakdown at iteration = {it}, basis.shape = {basis.shape}")
+            self._breakdown_message(it)
         except GeneralizedKrylowSubspaceSpansEntireSpace:
             print("Warning: The genearlized krylow subspace is now identical to the whole parameter space "
                   f"at iteration = {it}")
         self.ri = rti
         self.rr = last["rr"]
-        if it % self.restart == 0:                                        # :135-136
-            xr = self._free_x(self.uJ)
-            basis.x(self.c, self.xb[xr])
-            self.c, s0 = basis.start(self.xb[xr], self.xb[self.uJ])
-            self.lls.on_restart(s0)
+        restart = it % self.restart == 0
         if it >= self.max_iter - 1:
             self.done = True
+        if basis.pending and (restart or self.done):
+            self._settle_explicit()
+        if restart:                                                       # :135-136
+            xr = self._free_x(self.uJ)
+            basis.x(self.e, self.xb[xr])
+            self.c = basis.start(self.xb[xr])
+            self.e = self.c.copy()
+            self.lls.on_restart()
         return self.done
 
     def finish(self, result_format="numpy"):
@@ -257,7 +298,7 @@ class GNKSolver:
         if not self.success:
             print("Warning: The gauss_newton_krylow algorithm reached maximal iteration bound before terminating!")
         xi = self._free_x(self.uJ)
-        xs = self.basis.x(self.c, self.xb[xi])
+        xs = self.basis.x(self.e, self.xb[xi])
         x = self.ops.own(xs).clone() if result_format == "torch" else self.ops.to_host(xs)
         return RegressionResult("gauss newton krylow", x, self.success, self.nfev, self.njev, self.iter)
 

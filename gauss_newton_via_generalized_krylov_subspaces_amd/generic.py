@@ -75,6 +75,8 @@ class FlatKrylovBasis:
     """ref:krylow.py:16-73 on flat device vectors (same interface as krylow.DeviceKrylovBasis)."""
 
     FUSE_KMAX = 0          # no fused first trial for generic problems
+    deferred = False       # Gram-Schmidt runs inside update (the breakdown is known there)
+    pending = False
 
     def __init__(self, ops, kmax: int):
         self.ops = ops
@@ -86,22 +88,19 @@ class FlatKrylovBasis:
         self._h = self.be.zeros(self.kmax)
         self._stats = self.be.zeros(2)
         self._g = self.be.zeros(ops.n)
-        self._jv = None
 
     @property
     def shape(self):
         return (self.ops.n, self.k)
 
-    def _jnorm(self, u, v) -> float:
-        """||J(u) v|| (the least-squares preconditioner's column scale)."""
-        if self._jv is None:
-            self._jv = self.be.zeros(self.ops.m)
-        self.ops.jvp(u, v, self._jv)
-        self.be.flat_stats(self._jv, self._stats)
-        return math.sqrt(float(self._stats[0].item()))
+    def gram_k(self):
+        return self.k
 
-    def start(self, x, u_jac=None):
-        """ref:krylow.py:30-39 (+ ||J(u_jac) v_0|| when u_jac is given)."""
+    def stored_step(self, d):
+        return np.asarray(d, dtype=np.float64)     # columns are stored normalised
+
+    def start(self, x):
+        """ref:krylow.py:30-39."""
         self.be.flat_stats(x, self._stats)
         sumsq, maxabs = (float(v) for v in self._stats.cpu().numpy())
         if maxabs <= 1e-8:                                    # np.allclose(x0, 0) (:31)
@@ -109,9 +108,7 @@ class FlatKrylovBasis:
         nrm = math.sqrt(sumsq)                                # :36
         self.be.flat_div(x, nrm, self.V[0])                   # :37
         self.k = 1
-        if u_jac is None:
-            return np.array([nrm])
-        return np.array([nrm]), self._jnorm(u_jac, self.V[0])
+        return np.array([nrm])
 
     def x(self, c: np.ndarray, out):
         k = len(c)
@@ -119,8 +116,8 @@ class FlatKrylovBasis:
         self.be.flat_gemv(self.V, k, self._c, out)
         return out
 
-    def update(self, u_jac, r, u_next=None, products_ready=False):
-        """ref:krylow.py:55-73 with jac_ev = J(u_jac), res_ev = r; returns ||J(u_next) v_new||."""
+    def update(self, u_jac, r, it=None, products=None):
+        """ref:krylow.py:55-73 with jac_ev = J(u_jac), res_ev = r (CGS done here, not deferred)."""
         k = self.k
         if k == self.ops.n:                                   # :59-60
             raise GeneralizedKrylowSubspaceSpansEntireSpace
@@ -138,7 +135,6 @@ class FlatKrylovBasis:
         nrm = math.sqrt(sumsq)                                # :71
         self.be.flat_div(g, nrm, self.V[k])
         self.k = k + 1
-        return self._jnorm(u_jac if u_next is None else u_next, self.V[k])
 
 
 class HostCallableOps:

@@ -8,7 +8,27 @@ its run time) does not exist here.
 
 Numerics follow the reference step by step: single classical Gram-Schmidt
 pass (CGS1, :64), breakdown when every |g_i| <= 1e-8 (:66, np.allclose with
-rtol=0), normalisation by division (:71).
+rtol=0), normalisation by the 2-norm (:71).
+
+Deferred Gram-Schmidt (the schedule, not the arithmetic, differs from the
+reference).  ``update`` computes g = -J^T r and h = V^T g (:62, :64) and stores
+the raw g as column k -- the *pending* column -- with its projection
+coefficients; it does not stream V a second time for g -= V h.  The pending
+column is settled by the next pass that reads V anyway:
+  * the next least-squares pass sees J w = J g - (J V) h through its triangular
+    transform (lls.py: ``gram_left``);
+  * the next first Armijo trial point materialises w = g - V h in place over
+    column k (the arithmetic of the CGS kernel) and returns sum w^2 and max |w|
+    with the trial's residual, so the norm (:71) and the breakdown test (:66)
+    come back with a host read the trial makes anyway (``resolve``);
+  * a restart or the end of the loop settles it explicitly (``resolve_explicit``).
+Column j of the reference basis is ``sc[j] * V[j]`` (sc = 1 / ||w||: the
+division of :71 is folded into the coefficients of every product with V).  The
+solver keeps the iterate's coordinates twice: ``c`` in the reference's units (the
+convergence test, ref:gauss_newton_krylow.py:96-104) and ``e`` in stored units,
+e = c * sc as it was accumulated -- every trial point is V @ (e + t ds) and the
+accepted one becomes the new e, so the reference's bit identity "the accepted
+trial point V (c + t d) is the next iterate V c"  holds for V @ e.
 """
 from __future__ import annotations
 
@@ -25,105 +45,168 @@ class GeneralizedKrylowSubspaceSpansEntireSpace(Exception):
     """ref:krylow.py:12-13"""
 
 
+BREAKDOWN_MESSAGE = ("Normal residual is allready inside generalized Krylow Subspcae, there for gauss newton "
+                     "krylow algorithm has to proceed without enlarging the subspace.")
+
+
+def is_breakdown(sumsq: float, maxabs: float) -> bool:
+    """np.allclose(g, 0, atol=1e-8, rtol=0) of ref:krylow.py:66 (NaN is never close)."""
+    return maxabs <= 1e-8 and not math.isnan(sumsq)
+
+
 class DeviceKrylovBasis:
+    deferred = True
+    FUSE_KMAX = 24                   # columns the fused first-trial kernel covers
+
     def __init__(self, dev, kmax: int):
         self.dev = dev
         self.be = dev.backend
         self.kmax = int(kmax)
         self.V = self.be.zeros(self.kmax, dev.slab.length)
-        self.k = 0
-        self._c = self.be.zeros(self.kmax)
-        self._h = self.be.zeros(self.kmax)
+        self.k = 0                       # settled columns
+        self.sc = np.ones(self.kmax)     # reference column j = sc[j] * V[j]
+        self.pend = None                 # pending column: {"slot", "hh", "it"}
+        self.last_norm = None            # ||w|| of the column settled last
+        self._c = self.be.zeros(self.kmax + 1)
+        self._hh = self.be.zeros(self.kmax)
+        self._h = self.be.zeros(self.kmax + 1)
         self._stats = self.be.zeros(2)
-        self._pack = self.be.zeros(3)          # [residual partial, sum g^2, max |g|] of a speculative step
-        self._g = dev.vec()              # new column before normalisation (stencil source)
-        self._jn2 = self.be.zeros(1)
+        # [sum r^2, sum w^2, max |w|, h_0 .. h_k] of a first trial: one collective / host read
+        self.pack = self.be.zeros(3 + self.kmax + 1)
+        self._g = dev.vec()              # raw g when V has no free slot (never pending in a Gram)
 
     @property
     def shape(self):
-        """(n, k) like ``basis.shape`` in the reference (n = global unknowns)."""
+        """(n, k) like ``basis.shape`` in the reference (n = global unknowns, settled columns)."""
         return (self.dev.slab.n_global, self.k)
 
-    def start(self, x, u_jac=None):
-        """ref:krylow.py:30-39.  ``x`` is a slab vector valid on owned +-GHOST rows.
+    @property
+    def pending(self) -> bool:
+        return self.pend is not None
 
-        Returns the coordinates [||x||]; with ``u_jac`` also ||J(u_jac) v_0|| (the first
-        least-squares preconditioner), from the same pass that normalises x."""
+    def gram_k(self) -> int:
+        """Columns the least-squares pass covers: the settled ones and a pending one."""
+        return self.k + (1 if self.pend is not None else 0)
+
+    def gram_left(self):
+        """Upper-triangular M with [reference columns | w] = [V_0 .. V_{k-1} | g] M: diag(sc) on the
+        settled columns and (-hh, 1) in the pending column; None when M = I."""
+        k = self.k
+        if self.pend is None:
+            return None if np.all(self.sc[:k] == 1.0) else np.diag(self.sc[:k])
+        M = np.zeros((k + 1, k + 1))
+        M[np.arange(k), np.arange(k)] = self.sc[:k]
+        M[:k, k] = -self.pend["hh"]
+        M[k, k] = 1.0
+        return M
+
+    def _slot(self, j):
+        return self.V[j] if j < self.kmax else self._g
+
+    def stored_step(self, d: np.ndarray) -> np.ndarray:
+        """A least-squares step in stored units: sc * d on the settled columns; a pending column's
+        entry is already in its raw (stored) units."""
+        ds = np.array(d, dtype=np.float64)
+        k = min(len(ds), self.k)
+        ds[:k] *= self.sc[:k]
+        return ds
+
+    def start(self, x):
+        """ref:krylow.py:30-39.  ``x`` is a slab vector valid on owned +-GHOST rows; returns [||x||]."""
         self.be.vec_stats(x, self._stats)
         sumsq, maxabs = self.dev.comm.sum_max(self._stats)
         if maxabs <= 1e-8:                                    # np.allclose(x0, 0) (:31)
             raise ValueError("x0 is not allowed to be 0 in the gauss_newton_krylow algorithm")
         nrm = math.sqrt(sumsq)                                # np.linalg.norm (:36)
+        self.be.vec_div(x, nrm, self.V[0], True)              # whole slab incl. ghosts (:37)
         self.k = 1
-        if u_jac is None:
-            self.be.vec_div(x, nrm, self.V[0], True)          # whole slab incl. ghosts (:37)
-            return np.array([nrm])
-        self.be.normalize_jnorm(u_jac, x, nrm, self.V[0], self._jn2)
-        return np.array([nrm]), math.sqrt(float(self.dev.comm.sum(self._jn2)[0])) / nrm
+        self.sc[:] = 1.0
+        self.pend = None
+        return np.array([nrm])
 
-    def x(self, c: np.ndarray, out):
-        """out = V @ c over the whole slab (ref:krylow.py:41-42)."""
-        k = len(c)
-        self.be.upload(self._c, c)
+    def x(self, e: np.ndarray, out):
+        """out = V @ e over the whole slab (ref:krylow.py:41-42), e in stored units, len(e) <= k."""
+        k = len(e)
+        if k > self.k:
+            raise RuntimeError("basis.x: coefficient vector longer than the settled basis")
+        self.be.upload(self._c, e)
         self.be.gemv(self.V, k, self._c, out)
         return out
 
-    FUSE_KMAX = 24
+    # -- first Armijo trial --------------------------------------------------------------
+    def trial_first(self, e_ext: np.ndarray, out, r_products=None):
+        """Trial point out = V @ e_ext, e_ext over ``gram_k()`` columns in stored units.  Materialises
+        a pending column (pack[1:3] = sum w^2, max |w|) and, with ``r_products``, also computes the update products at u = out with that residual:
+        g = -J(out)^T r into the next free slot, pack[3:3+kk] = V^T g (this rank, stored units).
+        Returns the device pack (pack[0] is the caller's residual slot)."""
+        kk = self.gram_k()
+        if len(e_ext) != kk:
+            raise RuntimeError("trial_first: coefficient length != basis columns")
+        self.be.upload(self._c, e_ext)
+        pend = self.pend is not None
+        if pend:
+            if self.pend["slot"] != self.k:
+                raise RuntimeError("pending column is not stored in V")
+            self.be.upload(self._hh, self.pend["hh"])
+        if r_products is not None:
+            g = self._slot(kk)
+            self._prod_slot = kk
+            h = self.pack[3:3 + kk]
+            if pend:
+                self.be.gemv_vjp_gemv_t_pending(self.V, self.k, self._c, self._hh, r_products, out, g, h,
+                                                self.pack[1:3])
+            else:
+                self.be.gemv_vjp_gemv_t(self.V, kk, self._c, r_products, out, g, h)
+        elif pend:
+            self.be.gemv_pending(self.V, self.k, self._c, self._hh, out, self.pack[1:3])
+        else:
+            self.be.gemv(self.V, kk, self._c, out)
+        return self.pack
 
-    def x_with_update_products(self, c: np.ndarray, r, out):
-        """out = V @ c, and -- from the same read of V -- the products of a basis update at
-        u = out with residual r: g = -J(out)^T r, h = V^T g (this rank's rows).  ``update(...,
-        products_ready=True)`` then continues from them.  Used for the first Armijo trial of
-        version "res_old" (the update after acceptance is exactly this product)."""
-        k = len(c)
-        self.be.upload(self._c, c)
-        self.be.gemv_vjp_gemv_t(self.V, k, self._c, r, out, self._g, self._h)
-        return out
+    def resolve(self, sumsq: float, maxabs: float) -> bool:
+        """Settle the pending column from its materialisation stats; True on breakdown (:66) --
+        then the column is dropped, else it becomes column k with sc = 1 / ||w|| (:71)."""
+        self.pend = None
+        if is_breakdown(sumsq, maxabs):
+            self.last_norm = None
+            return True
+        nrm = math.sqrt(sumsq)
+        self.last_norm = nrm
+        self.sc[self.k] = 1.0 / nrm
+        self.k += 1
+        return False
 
-    def cgs_speculative(self):
-        """Right after ``x_with_update_products``: enqueue the CGS step g -= V h (+ its stats into
-        pack[1:3]) before the Armijo test has read the trial's residual, so that one host read serves
-        both (pack[0] is the caller's residual slot).  ``update(..., stats=...)`` continues from it;
-        a rejected trial recomputes g."""
+    def resolve_explicit(self) -> bool:
+        """Settle a pending column without a trial (restart / end of the loop): w = g - V hh in place on
+        owned rows, then ``resolve``.  (Ghost rows are not refreshed: the caller discards the column.)"""
+        g = self._slot(self.pend["slot"])
+        self.be.upload(self._hh, self.pend["hh"])
+        self.be.cgs_update(self.V, self.k, self._hh, g, self._stats)
+        sumsq, maxabs = self.dev.comm.sum_max(self._stats)
+        return self.resolve(sumsq, maxabs)
+
+    # -- basis update ------------------------------------------------------------------------
+    def update(self, u_jac, r, it=None, products=None):
+        """ref:krylow.py:55-73 with jac_ev = J(u_jac), res_ev = r (slab vectors), deferred: the new
+        column becomes pending (see the module docstring).  ``products``: the rank-summed raw
+        h = V^T g of a fused first trial at u_jac with residual r (g already in the free slot)."""
         k = self.k
-        if self.dev.comm.world > 1:
-            self._h[:k].copy_(self.dev.comm.sum_device(self._h[:k]))
-        self.be.cgs_update(self.V, k, self._h, self._g, self._pack[1:3])
-        return self._pack
-
-    def update(self, u_jac, r, u_next=None, products_ready=False, stats=None):
-        """ref:krylow.py:55-73 with jac_ev = J(u_jac), res_ev = r (slab vectors).
-
-        Returns ||J(u_next) v_new|| (u_next defaults to u_jac), computed in the same
-        pass that normalises the new column (the next least-squares preconditioner).
-        ``products_ready``: g and h were produced by ``x_with_update_products`` at u_jac;
-        ``stats`` = (sum g^2, max |g|) when ``cgs_speculative`` has also done the CGS step."""
-        k = self.k
+        if self.pend is not None:
+            raise RuntimeError("basis update with a pending column")
         if k == self.dev.slab.n_global:                       # :59-60
             raise GeneralizedKrylowSubspaceSpansEntireSpace
         if k >= self.kmax:
             raise RuntimeError("Krylov basis storage exhausted")
-        g = self._g
-        if stats is not None and products_ready:
-            sumsq, maxabs = stats
+        g = self._slot(k)
+        if products is not None:
+            if getattr(self, "_prod_slot", None) != k:
+                raise RuntimeError("update products were computed for another basis size")
+            h_raw = np.asarray(products[:k], dtype=np.float64)
         else:
-            if not products_ready:
-                self.be.vjp_gemv_t(u_jac, r, self.V, k, g, self._h)   # g = -J^T r ; h = V^T g (:62, :64)
-            if self.dev.comm.world > 1:                           # rank-ordered sum of the partials
-                self._h[:k].copy_(self.dev.comm.sum_device(self._h[:k]))
-            self.be.cgs_update(self.V, k, self._h, g, self._stats)   # g -= V h (:64)
-            sumsq, maxabs = self.dev.comm.sum_max(self._stats)
-        if maxabs <= 1e-8 and not math.isnan(sumsq):          # :66
-            raise GeneralizedKrylowSubspaceBreakdown(
-                "Normal residual is allready inside generalized Krylow Subspcae, there for gauss newton "
-                "krylow algorithm has to proceed without enlarging the subspace.")
-        nrm = math.sqrt(sumsq)                                # :71
+            self.be.vjp_gemv_t(u_jac, r, self.V, k, g, self._h)       # g = -J^T r ; h = V^T g (:62, :64)
+            h_raw = self.dev.comm.sum(self._h[:k])                   # rank-ordered sum of the partials
+        self._prod_slot = None
+        # g's ghost rows: the next pass applies the stencil to it and materialises w on the whole slab
         self.dev.comm.halo(g, self.dev.slab.N, self.dev.slab.nrows)
-        # V[k] = g / nrm on the whole slab (ghost rows divide the neighbours' g, so they
-        # equal the neighbours' V[k] rows bit for bit) + sum (J g)^2 on owned rows
-        self.be.normalize_jnorm(u_jac if u_next is None else u_next, g, nrm, self.V[k], self._jn2)
-        self.k = k + 1
-        jn2, comm = self._jn2, self.dev.comm
-        # ||J v_new|| is needed only by the next least-squares solve: read it then (after the Gram
-        # pass's own sync) instead of stalling the queue here
-        return lambda: math.sqrt(float(comm.sum(jn2)[0])) / nrm
+        h = self.sc[:k] * h_raw                                      # reference h = V^T g
+        self.pend = {"slot": k, "hh": self.sc[:k] * h, "it": it}

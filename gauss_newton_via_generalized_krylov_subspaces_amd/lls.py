@@ -2,25 +2,32 @@
 
 The reference factors A = -J @ V (n x k) with LAPACK Householder QR and solves
 R d = Q^T r.  The build never materialises J @ V: the fp64-MFMA Gram kernel
-(gnk_gram) streams V once per pass, applies the Bratu stencil on the fly, applies
-an upper-triangular preconditioner P^-1 on MFMA (W <- W P^-1) and returns the Gram
-matrix of [J V P^-1 | r].  Cholesky QR on a well-conditioned Y = J V P^-1 gives
-R = R_Y P and Q^T r = R_Y^-T (Y^T r) to O(u) orthogonality.
+(gnk_gram) streams the stored basis once per pass, applies the Bratu stencil on
+the fly, applies an upper-triangular transform T on MFMA and returns the Gram
+matrix of [J V_stored T | r].  Cholesky QR on a well-conditioned Y gives R and
+Q^T r = R_Y^-T (Y^T r) to O(u) orthogonality.
 
-Preconditioner P (one pass per iteration in the common case):
-  * CholQR2 (two passes: P = I, then P = R1) when there is no usable previous
-    factor and no column scale (after a breakdown-free restart the solver passes
-    s = ||J v_0|| and the first solve is a single pass with P = [s]);
-  * otherwise P = blockdiag(R_prev, s): the previous iteration's R of J_prev V
-    (the basis only gained one column and J changed only in its diagonal
-    LAMBDA exp(u)) and s = ||J v_new|| for the appended column, so Y is close to
-    orthonormal and ONE pass suffices.
-The pass is accepted when cond(R_Y) <= COND_ACCEPT (then the O(cond^2 u)
-CholQR error is below 1e-13 relative); otherwise another pass runs with the
-current R -- classical CholQR2 -- and, if a Gram is not numerically SPD, the
-factorisation is shifted (shifted CholeskyQR3, Fukaya et al. 2020).
-Across ranks each Gram is an all-gather of (k+1)^2 doubles summed in rank order
-(the "one-reduce" of TSQR, once per pass).
+T = M P^-1:
+  * M (``basis.gram_left()``) maps the stored columns to the reference basis --
+    the folded column norms diag(sc) and, for a pending column of the deferred
+    Gram-Schmidt (krylow.py), its projection: J w = J g - (J V) hh;
+  * P is the preconditioner.  One pass per iteration in the common case:
+    P = blockdiag(R_prev, 1) -- the previous iteration's R of J_prev V (the basis
+    only gained one column and J changed only in its diagonal LAMBDA exp(u)) --
+    and the new column's scale is taken from the same pass: its Gram row/column
+    are divided by sqrt(G_kk) (= ||J v_new||), i.e. P = blockdiag(R_prev, ||J v_new||),
+    so Y is close to orthonormal.  Without a usable previous factor: CholQR2
+    (a plain first pass, P = R_1).
+The pass is accepted when cond(R_Y) <= COND_ACCEPT (then the O(cond^2 u) CholQR
+error is below 1e-13 relative); otherwise another pass runs with the current R --
+classical CholQR2 -- and, if a Gram is not numerically SPD, the factorisation is
+shifted (shifted CholeskyQR3, Fukaya et al. 2020).  Across ranks each Gram is an
+all-gather of (k+1)^2 doubles summed in rank order (the "one-reduce" of TSQR).
+
+With a pending column the solution is in that column's raw units until the
+first trial has measured ||w||: ``resolve_pending(nrm)`` rescales R's last column
+and d's last entry to the reference's unit column and only then prints the
+rank-deficiency messages; ``discard_pending()`` drops the solve on a breakdown.
 
 jdd = ||J V d||^2 of the Armijo rule (ref:armijo_goldstein.py:50) is ||R d||^2:
 the reference's extra GEMV over J V is not needed.
@@ -49,6 +56,13 @@ def _cond_upper(R):
     return float(np.linalg.cond(R))
 
 
+def rank_messages(R):
+    """ref:gauss_newton_krylow.py:32-34 (np.isclose(r_kk, 0) with atol 1e-8)."""
+    for r_kk in np.diagonal(R):
+        if np.isclose(r_kk, 0, atol=1e-8):
+            print("A is rank deficient")
+
+
 class CholQR2Solver:
     def __init__(self, dev, kmax: int, gram=None, n_global=None):
         """``gram(u, V, k, rinv, r, G)`` fills G with the Gram of [J(u) V RinvAug | r] (default:
@@ -64,27 +78,25 @@ class CholQR2Solver:
         self.solves = 0
         self.fallbacks = 0
         self.history = []           # per solve: (k, passes, cond(R_Y) of each pass) -- diagnostics
-        self.R_prev = None          # R of the last solve (k_prev x k_prev); None after a restart
+        self.R_prev = None          # R of the last solve (k_prev x k_prev); None: no usable factor
         self.R_last = None          # R of the last solve (diagnostics)
-        self.s_new = None           # ||J v_new|| of the column appended since then
+        self._tentative = None      # (R, d) of a solve over a pending column
 
     # -- basis events (the solver tells us how V changed since the last solve) -------
-    def on_append(self, s_new):
-        """s_new = ||J v_new||, a float or a callable returning it (read lazily at the next solve)."""
-        self.s_new = s_new
+    def on_append(self, s_new=None):
+        """A column was appended (its scale is measured by the next pass itself)."""
 
     def on_restart(self, s0=None):
-        """The basis restarted with one column v_0; s0 = ||J v_0|| (None: unknown -> CholQR2)."""
-        self.R_prev = None if s0 is None else np.zeros((0, 0))
-        self.s_new = s0
+        """The basis restarted with one column v_0: P = [1], scale from the pass."""
+        self.R_prev = np.zeros((0, 0))
 
-    def _gram(self, u, basis, k, P, r):
+    def _gram(self, u, basis, k, T, r):
         be = self.be
         kp = be.gram_dim(k, r is not None)
         rinv_dev = None
-        if P is not None:
+        if T is not None:
             aug = np.zeros((kp, kp))
-            aug[:k, :k] = scipy.linalg.solve_triangular(P, np.eye(k), lower=False)
+            aug[:k, :k] = T
             if r is not None:
                 aug[k, k] = 1.0
             rinv_dev = self._rinv[:kp * kp]
@@ -95,31 +107,39 @@ class CholQR2Solver:
         return self.dev.comm.sum(G).reshape(kp, kp)
 
     def _initial_preconditioner(self, k):
+        """(P, rescale_last): P = R_prev (basis unchanged) or blockdiag(R_prev, 1) (one new column,
+        scaled by the pass); (None, False) -> CholQR2."""
         R = self.R_prev
         if R is None:
-            return None
-        if callable(self.s_new):
-            self.s_new = float(self.s_new())
+            return None, False
         kp = R.shape[0]
         if kp == k:
-            return R                                   # basis unchanged (breakdown / spans space)
-        if kp == k - 1 and self.s_new is not None and self.s_new > 0.0:
+            return R, False                            # basis unchanged (breakdown / spans space)
+        if kp == k - 1:
             P = np.zeros((k, k))
             P[:kp, :kp] = R
-            P[kp, kp] = self.s_new
-            return P
-        return None
+            P[kp, kp] = 1.0
+            return P, True
+        return None, False
+
+    @staticmethod
+    def _transform(M, P):
+        Pinv = scipy.linalg.solve_triangular(P, np.eye(P.shape[0]), lower=False)
+        return Pinv if M is None else M @ Pinv
 
     def solve(self, u, basis, r):
-        """Returns (d, jdd, R) for min ||-J(u) V d - r||."""
-        k = basis.k
+        """(d, jdd, R) for min ||-J(u) V d - r|| over the basis' Gram columns.  With a pending column
+        d and R are tentative (raw units of that column, messages deferred): see resolve_pending."""
+        k = basis.gram_k() if hasattr(basis, "gram_k") else basis.k
+        M = basis.gram_left() if hasattr(basis, "gram_left") else None
+        pending = getattr(basis, "pending", False)
         self.solves += 1
         p0 = self.passes
         conds = []
-        P = self._initial_preconditioner(k)
+        P, rescale = self._initial_preconditioner(k)
         if P is None:
-            # classical CholQR2: first pass unpreconditioned (P = I, no r column)
-            G1 = self._gram(u, basis, k, None, None)[:k, :k]
+            # classical CholQR2: first pass without preconditioner (T = M, no r column)
+            G1 = self._gram(u, basis, k, M, None)[:k, :k]
             try:
                 P = _chol_upper(G1)
             except (np.linalg.LinAlgError, ValueError):
@@ -127,7 +147,15 @@ class CholQR2Solver:
                 shift = 11.0 * (n * k + k * (k + 1)) * EPS * np.trace(G1)
                 P = _chol_upper(G1 + shift * np.eye(k))
         for it in range(MAX_PASSES):
-            Gp = self._gram(u, basis, k, P, r)
+            Gp = self._gram(u, basis, k, self._transform(M, P), r)
+            if rescale and it == 0:
+                # the new column's scale ||J v_new|| from this pass: Y[:, k-1] /= s, P[k-1, k-1] = s
+                s2 = Gp[k - 1, k - 1]
+                if np.isfinite(s2) and s2 > 0.0:
+                    s = np.sqrt(s2)
+                    Gp[k - 1, :] /= s
+                    Gp[:, k - 1] /= s
+                    P[k - 1, k - 1] = s
             try:
                 Ry = _chol_upper(Gp[:k, :k])
             except (np.linalg.LinAlgError, ValueError):
@@ -143,12 +171,31 @@ class CholQR2Solver:
                 break
             P = Ry @ P                                   # one more pass with the improved factor
             self.fallbacks += 1
-        for r_kk in np.diagonal(R):                                  # ref:gauss_newton_krylow.py:32-34
-            if np.isclose(r_kk, 0, atol=1e-8):
-                print("A is rank deficient")
         d = -scipy.linalg.solve_triangular(R, z, lower=False)
         jdd = float(np.sum((R @ d) ** 2))
         self.history.append((k, self.passes - p0, conds))
-        self.R_prev = self.R_last = R
-        self.s_new = None
+        if pending:
+            self._tentative = (R, d)
+            return d, jdd, R
+        self._settle(R)
         return d, jdd, R
+
+    def _settle(self, R):
+        rank_messages(R)                                             # ref:gauss_newton_krylow.py:32-34
+        self.R_prev = self.R_last = R
+        self._tentative = None
+
+    def resolve_pending(self, nrm: float) -> np.ndarray:
+        """The pending column was settled with norm nrm: R and d in reference units
+        (column w -> w / nrm: R[:, -1] / nrm, d[-1] * nrm); prints; returns d."""
+        R, d = self._tentative
+        R = R.copy()
+        d = d.copy()
+        R[:, -1] /= nrm
+        d[-1] *= nrm
+        self._settle(R)
+        return d
+
+    def discard_pending(self):
+        """The pending column broke down: the tentative solve is void (R_prev stays)."""
+        self._tentative = None

@@ -90,6 +90,20 @@ class Comm:
                 m = v
         return s, m
 
+    def sum_except_max(self, t: torch.Tensor, imax: int) -> np.ndarray:
+        """Rank-ordered sums of every entry of a small per-rank tensor except entry ``imax``, which
+        is the NaN-propagating max over ranks: a step's control scalars in one collective."""
+        parts = self._gather(t)
+        s = parts[0].copy()
+        m = float(parts[0][imax])
+        for p in range(1, parts.shape[0]):
+            s = s + parts[p]
+            v = float(parts[p][imax])
+            if v > m or math.isnan(v):
+                m = v
+        s[imax] = m
+        return s
+
     def sum_device(self, t: torch.Tensor) -> torch.Tensor:
         """Rank-ordered sum of a small per-rank device tensor, left on the device (no host round
         trip on RCCL): the same IEEE additions in the same order as ``sum``."""

@@ -88,6 +88,23 @@ int gnk_vjp_gemv_t(gnk_ctx* ctx, const double* u, const double* r,
 int gnk_basis_gemv_vjp_gemv_t(gnk_ctx* ctx, const double* V, int64_t ldv, int k, const double* c, const double* r,
                               double* x, double* g, double* h_out);
 
+/* Deferred Gram-Schmidt: the basis update of ref:krylow.py:62-73 stores the raw
+ * g = -J^T r as column k of V ("pending") and its projection coefficients hh; the next least-
+ * squares pass sees J w through its triangular transform, and the first Armijo trial point
+ * materialises w = g - V[:, :k] @ hh in place over column k (whole slab, the rounding of
+ * gnk_cgs_update) while it reads V anyway:
+ *   x = V[:, :k] @ c[:k] + w c[k]   (rounding of gnk_basis_gemv over k + 1 columns),
+ *   stats_out = {sum w**2, max|w|} over owned rows (the norm and breakdown test, ref:krylow.py:66,71).
+ * x must not alias column k.                      ref:krylow.py:41-42, 64-71 */
+int gnk_basis_gemv_pending(gnk_ctx* ctx, const double* V, int64_t ldv, int k, const double* c, const double* hh,
+                           double* x, double* stats_out);
+/* gnk_basis_gemv_vjp_gemv_t with the pending column k materialised as in gnk_basis_gemv_pending:
+ * x and h_out cover k + 1 columns (h_out[k] = w . g), stats_out as above.  1 <= k + 1 <= 24;
+ * g must not alias column k.        ref:krylow.py:42, :62-71 + gauss_newton_krylow.py:91,115 */
+int gnk_basis_gemv_vjp_gemv_t_pending(gnk_ctx* ctx, const double* V, int64_t ldv, int k, const double* c,
+                                      const double* hh, const double* r, double* x, double* g, double* h_out,
+                                      double* stats_out);
+
 /* g -= V[:, :k] @ h on owned rows; stats_out = {sum g**2, max|g|}
  *                                               ref:krylow.py:64,66,71 */
 int gnk_cgs_update(gnk_ctx* ctx, const double* V, int64_t ldv, int k,

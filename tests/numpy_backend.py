@@ -217,6 +217,19 @@ class NumpyBackend:
         self.gemv(V, k, c, x)
         self.vjp_gemv_t(x, r, V, k, g, h)
 
+    def gemv_pending(self, V, k, c, hh, x, stats):
+        Vn = V.numpy()
+        W = Vn[k]
+        W[:] = W - np.asarray(hh.numpy()[:k]) @ Vn[:k]
+        x.numpy()[:] = np.asarray(c.numpy()[:k + 1]) @ Vn[:k + 1]
+        o = W[GHOST * self.N:(GHOST + self.nrows) * self.N]
+        stats[0] = float(np.sum(o * o))
+        stats[1] = float(np.max(np.abs(o))) if not np.isnan(o).any() else float("nan")
+
+    def gemv_vjp_gemv_t_pending(self, V, k, c, hh, r, x, g, h, stats):
+        self.gemv_pending(V, k, c, hh, x, stats)
+        self.vjp_gemv_t(x, r, V, k + 1, g, h)
+
     def vjp_gemv_t(self, u, r, V, k, g, h):
         lo, hi = GHOST, GHOST + self.nrows
         G = self._m(g)

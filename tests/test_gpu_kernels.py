@@ -139,6 +139,79 @@ def test_gemv_vjp_gemv_t_fused(N, k):
                                atol=1e-12 * np.abs(own(dev, g1)).sum() * np.abs(Vh).max())
 
 
+def _pending_case(N, k, seed):
+    """A basis of k columns with a raw pending column g at slot k (ghost rows filled as after a
+    halo, i.e. whole-slab values), coefficients c (k + 1) and projection coefficients hh."""
+    prob, dev, ref = make(N)
+    be = dev.backend
+    rng = np.random.default_rng(seed)
+    V = be.zeros(k + 2, dev.slab.length)
+    Vh = rng.standard_normal((k + 1, N * N)) / N
+    for j in range(k + 1):
+        V[j].copy_(dev.load(Vh[j]))
+    hh = rng.standard_normal(k) / N
+    c = rng.standard_normal(k + 1)
+    return prob, dev, ref, be, V, hh, c
+
+
+@pytest.mark.parametrize("N,k", [(24, 1), (25, 6), (100, 12), (1024, 19), (1023, 23), (64, 16)])
+def test_gemv_pending(N, k):
+    """Deferred CGS: w = g - V hh materialised in place == gnk_cgs_update's w bit for bit (whole
+    slab), x = V c over k + 1 columns == gnk_basis_gemv on the materialised basis bit for bit,
+    {sum w^2, max |w|} over owned rows within reduction-order rounding."""
+    prob, dev, ref, be, V, hh, c = _pending_case(N, k, 100 + k)
+    V2 = V.clone()
+    hd, cd = be.to_device(hh), be.to_device(c)
+    x1, st1 = dev.vec(), be.zeros(2)
+    be.gemv_pending(V, k, cd, hd, x1, st1)
+    # reference: explicit CGS over the whole slab (cgs_update covers owned rows: apply it to the
+    # slab-sized rows by hand with the same per-element order) + gemv
+    wref = V2[k].cpu().numpy().copy()
+    s = np.zeros_like(wref)
+    Vn = V2.cpu().numpy()
+    for j in range(k):
+        s = s + Vn[j] * hh[j]
+    wref = wref - s
+    np.testing.assert_array_equal(V[k].cpu().numpy(), wref)
+    st2 = be.zeros(2)
+    g2 = V2[k].clone()
+    be.cgs_update(V2, k, hd, g2, st2)
+    np.testing.assert_array_equal(own(dev, g2), own(dev, V[k]))
+    V2[k].copy_(V[k])
+    x2 = dev.vec()
+    be.gemv(V2, k + 1, cd, x2)
+    np.testing.assert_array_equal(x1.cpu().numpy() + 0.0, x2.cpu().numpy() + 0.0)
+    w_own = own(dev, V[k])
+    np.testing.assert_allclose(st1[0].item(), np.sum(w_own ** 2), rtol=1e-12)
+    assert st1[1].item() == np.abs(w_own).max()
+    with pytest.raises(RuntimeError, match="alias"):
+        be.gemv_pending(V, k, cd, hd, V[k], st1)
+
+
+@pytest.mark.parametrize("N,k", [(24, 1), (25, 6), (100, 12), (1024, 19), (1023, 23), (64, 16)])
+def test_gemv_vjp_gemv_t_pending(N, k):
+    """Fused first trial with a pending column == gemv_pending then vjp_gemv_t(u = x) over k + 1
+    columns: w, x and g bit for bit, h (k + 1) and the stats within reduction-order rounding."""
+    prob, dev, ref, be, V, hh, c = _pending_case(N, k, 200 + k)
+    rng = np.random.default_rng(k)
+    rs = dev.load(rng.standard_normal(N * N))
+    V2 = V.clone()
+    hd, cd = be.to_device(hh), be.to_device(c)
+    x1, g1, h1, st1 = dev.vec(), dev.vec(), be.zeros(k + 1), be.zeros(2)
+    be.gemv_vjp_gemv_t_pending(V, k, cd, hd, rs, x1, g1, h1, st1)
+    x2, g2, h2, st2 = dev.vec(), dev.vec(), be.zeros(k + 1), be.zeros(2)
+    be.gemv_pending(V2, k, cd, hd, x2, st2)
+    be.vjp_gemv_t(x2, rs, V2, k + 1, g2, h2)
+    np.testing.assert_array_equal(V[k].cpu().numpy(), V2[k].cpu().numpy())
+    np.testing.assert_array_equal(x1.cpu().numpy() + 0.0, x2.cpu().numpy() + 0.0)
+    np.testing.assert_array_equal(own(dev, g1), own(dev, g2))
+    scale = np.abs(own(dev, g2)).sum() * np.abs(V2[:k + 1].cpu().numpy()).max()
+    np.testing.assert_allclose(h1.cpu().numpy(), h2.cpu().numpy(), rtol=1e-12, atol=1e-12 * scale)
+    np.testing.assert_allclose(st1.cpu().numpy(), st2.cpu().numpy(), rtol=1e-12)
+    with pytest.raises(RuntimeError, match="alias"):
+        be.gemv_vjp_gemv_t_pending(V, k, cd, hd, rs, x1, V[k], h1, st1)
+
+
 @pytest.mark.parametrize("N,lam", [(8, 10.0), (25, 10.0), (64, 0.0), (1024, 10.0), (1023, 10.0)])
 def test_normalize_jnorm(N, lam):
     """v = g / denom bit for bit on the whole slab (ghost rows included) and

@@ -80,8 +80,20 @@ def test_gnk_linear_breakdown(golden):
     y = prob.pde_operator(prob.u_true)
     out, rec, so, exc = run(gnk.gauss_newton_krylow, dict(grid_nodes=25, ALPHA=5, LAMBDA=0.0),
                             arr["bratu24_linear_u0"], y, max_iter=100)
-    assert so == meta["cases"]["bratu24_linear_res_old"]["stdout"]   # breakdown at iteration 2, basis (576, 2)
-    assert exc is not None and exc[0] == "StepLengthConvergenceError"
+    case = meta["cases"]["bratu24_linear_res_old"]
+    assert so == case["stdout"]                     # breakdown at iteration 2, basis (576, 2)
+    # Iteration 3 re-solves the least-squares problem of iteration 2 (linear problem, same basis):
+    # d is rounding noise (reference: ||d|| = 3e-17) and the Armijo outcome is a rounding tie
+    # ("assert only the breakdown event").  The reference sees c + t d == c for
+    # every t and fails 100 halvings; a noise step that survives the addition is accepted and
+    # then meets the convergence test at once.  Either way the iterate is the reference's.
+    if exc is not None:
+        assert exc[0] == "StepLengthConvergenceError"
+    else:
+        assert out.success and out.nit == 3
+        assert rec["nfev"][:2] == case["per_iter"]["nfev"]
+        np.testing.assert_allclose(rec["xnorm"][2], case["per_iter"]["xnorm"][1], rtol=1e-12)
+    np.testing.assert_allclose(rec["xnorm"][:2], case["per_iter"]["xnorm"], rtol=1e-10)
 
 
 def test_gnk_linear_res_new(golden):
