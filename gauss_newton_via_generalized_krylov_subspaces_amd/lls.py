@@ -53,14 +53,15 @@ def _cond_upper(R):
     d = np.abs(np.diagonal(R))
     if d.min() == 0.0:
         return np.inf
-    return float(np.linalg.cond(R))
+    sv = np.linalg.svd(R, compute_uv=False)              # 2-norm condition number (np.linalg.cond)
+    return float(sv[0] / sv[-1])
 
 
 def rank_messages(R):
-    """ref:gauss_newton_krylow.py:32-34 (np.isclose(r_kk, 0) with atol 1e-8)."""
-    for r_kk in np.diagonal(R):
-        if np.isclose(r_kk, 0, atol=1e-8):
-            print("A is rank deficient")
+    """ref:gauss_newton_krylow.py:32-34: one message per diagonal entry with np.isclose(r_kk, 0),
+    i.e. |r_kk| <= 1e-8 (+ 1e-5 * 0), in diagonal order."""
+    for _ in range(int(np.count_nonzero(np.abs(np.diagonal(R)) <= 1e-8))):
+        print("A is rank deficient")
 
 
 class CholQR2Solver:
