@@ -162,6 +162,24 @@ def gn_cg_line(args, prob, u_true, u0, comm, device, world):
                        "algorithmic_bytes_per_launch": m_by}}
 
 
+def prewarm(args, comm, device):
+    """HIP loads a kernel's code object at its first launch (~1 ms each).  One restart cycle on a
+    256^2 grid (same dispatch: N % 128 == 0, same k range and version) makes every kernel variant
+    of the timed steps resident before the clock starts."""
+    import gauss_newton_via_generalized_krylov_subspaces_amd as gnk
+    from gauss_newton_via_generalized_krylov_subspaces_amd._device import SingleRankOperator
+    prob, u_true, u0 = bratu_inputs(256)
+    y = SingleRankOperator(prob, device).forward(u_true)
+    s = gnk.GNKSolver(prob, y, krylow_restart=args.restart, tol=1e-8, max_iter=10 ** 9, version=args.version,
+                      comm=comm, device=device)
+    s.setup(u0)
+    with contextlib.redirect_stdout(io.StringIO()):
+        for _ in range(args.restart + 2):
+            if s.step():
+                break
+    torch.cuda.synchronize()
+
+
 def pmc_traffic(config_key):
     """HBM bytes per Gram launch from the committed rocprofv3 PMC summary, if one matches."""
     for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "pmc_summary.json")), reverse=True):
@@ -195,9 +213,10 @@ def main():
 
     N = args.grid
     n = N * N
+    comm = Comm()
+    prewarm(args, comm, device)
     prob, u_true, u0 = bratu_inputs(N)
     y = SingleRankOperator(prob, device).forward(u_true)            # y = F(u_true) (ref:bratu_pde_test.py:29)
-    comm = Comm()
     solver = gnk.GNKSolver(prob, y, krylow_restart=args.restart, tol=1e-8, max_iter=10 ** 9,
                            version=args.version, comm=comm, device=device)
     del y

@@ -66,6 +66,8 @@ SIGNATURES = {
     "gnk_cg_step_matvec": (_c_int, [_c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_dbl, _c_int, _c_vp, _c_dbl,
                                     _c_vp]),
     "gnk_cg_update_p": (_c_int, [_c_vp, _c_dbl, _c_int, _c_vp, _c_vp]),
+    "gnk_lls_max_k": (_c_int, []),
+    "gnk_lls_solve": (_c_int, [_c_vp, _c_vp, _c_int, _c_int, _c_vp, _c_int, _c_vp, _c_vp, _c_vp, _c_vp]),
     "gnk_probe_mfma_f64": (_c_int, [_c_vp, _c_vp, _c_int, _c_int]),
     "gnk_timer_start": (_c_int, [_c_vp, _c_int, _c_int]),
     "gnk_timer_collect": (_c_int, [_c_vp, ctypes.POINTER(_c_dbl), ctypes.POINTER(_c_dbl), _c_int]),
@@ -277,6 +279,13 @@ class HipBackend:
 
     def vec_axpy(self, x, alpha, d, out, full_slab):
         self._call("gnk_vec_axpy", _p(x), float(alpha), _p(d), _p(out), int(bool(full_slab)))
+
+    def lls_max_k(self):
+        return int(self.lib.gnk_lls_max_k())
+
+    def lls_solve(self, G, kp, k, P, rescale, sdd, e, out, e_try):
+        self._call("gnk_lls_solve", _p(G), int(kp), int(k), _p(P), int(bool(rescale)), _p(sdd), _p(e), _p(out),
+                   _p(e_try))
 
     def gram_dim(self, k, with_r):
         return int(self.lib.gnk_gram_padded_dim(int(k), int(bool(with_r))))

@@ -2000,6 +2000,113 @@ __global__ __launch_bounds__(BLOCK) void k_gram_reduce(const double* __restrict_
   }
 }
 
+// ---------------------------------------------------------------- least squares on the device
+// One preconditioned CholeskyQR solve of the GNK step (lls.py, ref:gauss_newton_krylow.py:16-36)
+// from a Gram of [J V T | r] that is already summed over ranks: one wave, k <= LS_KMAX.
+//   rescale: divide row and then column k-1 of G by s = sqrt(G[k-1][k-1]), P[k-1][k-1] = s
+//   G[:k, :k] = Ry^T Ry (unblocked Cholesky, dpotf2's left-looking order);  z = Ry^-T G[:k, k];
+//   R = Ry P;  d = -R^-1 z (dtrsv's column order);  jdd = ||R d||^2;
+//   e_try = e + s_dd * d  (the first Armijo trial point's stored coefficients).
+// out: [status, jdd, s, d (k), R (k x k), Ry (k x k)]; status 0 = ok, 1 = G[:k, :k] not numerically SPD.
+constexpr int LS_KMAX = 32;
+constexpr int LS_LD = LS_KMAX + 1;
+
+__global__ __launch_bounds__(64) void k_lls(const double* __restrict__ Gm, int kp, int k, const double* __restrict__ P,
+                                            int rescale, const double* __restrict__ sdd,
+                                            const double* __restrict__ e, double* __restrict__ out,
+                                            double* __restrict__ etry) {
+  __shared__ double g[LS_LD][LS_LD + 1];
+  __shared__ double p[LS_KMAX][LS_LD];
+  __shared__ double ry[LS_KMAX][LS_LD];
+  __shared__ double rr[LS_KMAX][LS_LD];
+  __shared__ double sv[LS_KMAX];
+  __shared__ int bad;
+  const int l = threadIdx.x;
+  const int k1 = k + 1;
+  for (int idx = l; idx < k1 * k1; idx += 64) g[idx / k1][idx % k1] = Gm[(idx / k1) * kp + idx % k1];
+  for (int idx = l; idx < k * k; idx += 64) p[idx / k][idx % k] = P[idx];
+  if (l == 0) bad = 0;
+  __syncthreads();
+  double s = 1.0;
+  if (rescale) {
+    const double s2 = g[k - 1][k - 1];
+    if (isfinite(s2) && s2 > 0.0) {
+      s = sqrt(s2);
+      if (l < k1) g[k - 1][l] = g[k - 1][l] / s;          // lls.py: Gp[k-1, :] /= s
+      __syncthreads();
+      if (l < k1) g[l][k - 1] = g[l][k - 1] / s;          //         Gp[:, k-1] /= s
+      if (l == 0) p[k - 1][k - 1] = s;
+      __syncthreads();
+    }
+  }
+  // Cholesky, upper: row j from the rows above it
+  for (int j = 0; j < k; ++j) {
+    double t = 0.0;
+    if (l >= j && l < k) {
+      t = g[j][l];
+      for (int i = 0; i < j; ++i) t = t - ry[i][j] * ry[i][l];
+    }
+    if (l == j) {
+      if (!(t > 0.0)) bad = 1;
+      ry[j][j] = sqrt(t);
+    }
+    __syncthreads();
+    if (l > j && l < k) ry[j][l] = t / ry[j][j];
+    if (l < j) ry[j][l] = 0.0;
+    __syncthreads();
+  }
+  // z = Ry^-T G[:k, k] (forward substitution, subtractions in row order)
+  double b = (l < k) ? g[l][k] : 0.0;
+  for (int j = 0; j < k; ++j) {
+    if (l == j) sv[j] = b / ry[j][j];
+    __syncthreads();
+    if (l > j && l < k) b = b - ry[j][l] * sv[j];
+  }
+  __syncthreads();
+  // R = Ry P (upper x upper)
+  if (l < k) {
+    for (int i = 0; i < k; ++i) {
+      double a = 0.0;
+      for (int m = i; m <= l; ++m) a = a + ry[i][m] * p[m][l];
+      rr[i][l] = (i <= l) ? a : 0.0;
+    }
+  }
+  __syncthreads();
+  // x = R^-1 z, column-oriented back substitution; d = -x
+  double xv = (l < k) ? sv[l] : 0.0;
+  __syncthreads();
+  for (int j = k - 1; j >= 0; --j) {
+    if (l == j) sv[j] = xv / rr[j][j];
+    __syncthreads();
+    if (l < j) xv = xv - sv[j] * rr[l][j];
+    __syncthreads();
+  }
+  const double d = (l < k) ? -sv[l] : 0.0;
+  // jdd = sum_i (R d)_i^2 (lane i: row i; summed by lane 0 in row order)
+  __shared__ double rd2[LS_KMAX];
+  if (l < k) {
+    double a = 0.0;
+    for (int c = l; c < k; ++c) a = a + rr[l][c] * (-sv[c]);
+    rd2[l] = a * a;
+  }
+  __syncthreads();
+  if (l == 0) {
+    double jdd = 0.0;
+    for (int i = 0; i < k; ++i) jdd = jdd + rd2[i];
+    out[0] = bad ? 1.0 : 0.0;
+    out[1] = jdd;
+    out[2] = s;
+  }
+  if (l < k) {
+    out[3 + l] = d;
+    etry[l] = e[l] + sdd[l] * d;
+    for (int i = 0; i < k; ++i) {
+      out[3 + k + i * k + l] = rr[i][l];
+      out[3 + k + k * k + i * k + l] = ry[i][l];
+    }
+  }
+}
+
 // ---------------------------------------------------------------- probes (tooling)
 __global__ void k_probe_mfma(double* out, int iters) {
   d4 c0 = {0, 0, 0, 0}, c1 = c0, c2 = c0, c3 = c0;
@@ -2942,6 +3049,18 @@ int gnk_timer_collect(gnk_ctx* ctx, double* ms_out, double* bytes_out, int capac
 }
 
 // tooling: fp64 MFMA issue-rate probe (not part of the solver)
+int gnk_lls_max_k(void) { return LS_KMAX; }
+
+int gnk_lls_solve(gnk_ctx* ctx, const double* Gm, int kp, int k, const double* P, int rescale, const double* sdd,
+                  const double* e, double* out, double* e_try) {
+  if (!ctx) return -1;
+  if (k < 1 || k > LS_KMAX) return fail(ctx, "lls_solve: k must be in [1, gnk_lls_max_k()]");
+  if (kp < k + 1) return fail(ctx, "lls_solve: kp < k + 1 (G must hold the r column)");
+  if (!Gm || !P || !sdd || !e || !out || !e_try) return fail(ctx, "lls_solve: NULL argument");
+  hipLaunchKernelGGL(k_lls, dim3(1), dim3(64), 0, ctx->stream, Gm, kp, k, P, rescale, sdd, e, out, e_try);
+  return check_launch(ctx, "lls_solve");
+}
+
 int gnk_probe_mfma_f64(gnk_ctx* ctx, double* out, int blocks, int iters) {
   if (!ctx) return -1;
   hipLaunchKernelGGL(k_probe_mfma, dim3(blocks), dim3(BLOCK), 0, ctx->stream, out, iters);

@@ -86,11 +86,15 @@ class BratuOps:
         self.be.residual(x, self.y, r, self._n2)
         return float(self.comm.sum(self._n2)[0])
 
-    def residual_pack(self, x, r, pack):
+    def residual_pack(self, x, r, pack, shared=None):
         """residual partial into pack[0] beside a first trial's device stats (pack[1] = sum w^2,
-        pack[2] = max |w|, pack[3:] = V^T g partials): one collective and one host read for all."""
+        pack[2] = max |w|, pack[3:] = V^T g partials): one collective and one host read for all.
+        ``shared``: a device buffer that is the same on every rank (the device least-squares
+        solve), read in the same round trip -> (rank-combined pack, shared host copy or None)."""
         self.be.residual(x, self.y, r, pack[0:1])
-        return self.comm.sum_except_max(pack, 2)
+        if shared is None:
+            return self.comm.sum_except_max(pack, 2), None
+        return self.comm.sum_except_max(pack, 2, shared)
 
     def to_host(self, x):
         return self.dev.slab.to_host(x)
@@ -188,33 +192,64 @@ class GNKSolver:
         else:
             self._append_coordinate()
 
-    def _first_trial(self, d, jdd, x_t, r_t, r_old, fuse):
-        """Armijo trial t = 1 (ref:armijo_goldstein.py:56).  Settles a pending basis column first --
-        on its breakdown the least-squares solve is redone without it -- and, for the fused res_old
-        path, computes the basis-update products at the trial point.
-        Returns (d, jdd, ds, sum r_t^2, raw h or None); ds = d in stored units."""
+    def _trial_plain(self, e_try, x_t, r_t, r_old, prod):
+        """Trial point x_t = V e_try on a settled basis -> (sum r_t^2, raw h or None)."""
         basis = self.basis
+        if not prod:
+            basis.x(e_try, x_t)
+            return self._residual(x_t, r_t), None
+        kk = basis.gram_k()
+        pack = basis.trial_first(e_try, x_t, r_old)
+        host, _ = self.ops.residual_pack(x_t, r_t, pack[:3 + kk])
+        return float(host[0]), host[3:3 + kk].copy()
+
+    def _first_trial(self, x_t, r_t, r_old, fuse):
+        """Least-squares solve (ref:gauss_newton_krylow.py:86-89) and Armijo trial t = 1
+        (ref:armijo_goldstein.py:56), enqueued back to back when the solve runs on the device (one
+        host read for both).  Settles a pending basis column first -- on its breakdown the solve is
+        redone without it -- and, for the fused res_old path, computes the basis-update products at
+        the trial point.  Returns (d, jdd, ds, sum r_t^2, raw h or None); ds = d in stored units."""
+        basis, lls = self.basis, self.lls
+        u = self.xb[self.uJ]
         while True:
             kk = basis.gram_k()
-            ds = basis.stored_step(d)
-            e_try = np.append(self.e, np.zeros(kk - len(self.e))) + 1.0 * ds
-            prod = fuse and kk <= basis.FUSE_KMAX
             pend = basis.pending
-            if not (prod or pend):
-                basis.x(e_try, x_t)
-                return d, jdd, ds, self._residual(x_t, r_t), None
-            pack = basis.trial_first(e_try, x_t, r_old if prod else None)
-            host = self.ops.residual_pack(x_t, r_t, pack[:3 + kk])
+            prod = fuse and kk <= basis.FUSE_KMAX
+            e_ext = np.append(self.e, np.zeros(kk - len(self.e)))
+            sdd = basis.step_scale()
+            ls = lls.launch(u, basis, r_old, e_ext, sdd)
+            if not ls.device and not pend:
+                ds = sdd * ls.d
+                rr, h = self._trial_plain(e_ext + 1.0 * ds, x_t, r_t, r_old, prod)
+                return ls.d, ls.jdd, ds, rr, h
+            if ls.device:
+                pack = basis.trial_first(None, x_t, r_old if prod else None, coef_dev=ls.e_try)
+                host, lsout = self.ops.residual_pack(x_t, r_t, pack[:3 + kk], ls.out)
+                res = lls.finish(ls, lsout)
+            else:
+                res = (ls.d, ls.jdd)
+                pack = basis.trial_first(e_ext + 1.0 * (sdd * ls.d), x_t, r_old if prod else None)
+                host, _ = self.ops.residual_pack(x_t, r_t, pack[:3 + kk])
             if pend:
                 it = basis.pend["it"]
                 if basis.resolve(float(host[1]), float(host[2])):
                     # ref:krylow.py:66-69 raised in iteration `it`: the basis was not enlarged
                     self._breakdown_message(it)
-                    self.lls.discard_pending()
-                    d, jdd, _ = self.lls.solve(self.xb[self.uJ], basis, r_old)
+                    lls.discard_pending()
                     continue
                 self._append_coordinate()                                 # :124 of iteration `it`
-                d = self.lls.resolve_pending(basis.last_norm)
+            if res is None:
+                # the device solve needs more passes: finish it on the host, then a new first trial
+                d, jdd = lls.continue_host(ls, u, basis, r_old)
+                ds = sdd * d
+                if pend:
+                    d = lls.resolve_pending(basis.last_norm)
+                rr, h = self._trial_plain(self.e + 1.0 * ds, x_t, r_t, r_old, prod)
+                return d, jdd, ds, rr, h
+            d, jdd = res
+            ds = sdd * d
+            if pend:
+                d = lls.resolve_pending(basis.last_norm)
             return d, jdd, ds, float(host[0]), (host[3:3 + basis.k].copy() if prod else None)
 
     def step(self) -> bool:
@@ -222,14 +257,13 @@ class GNKSolver:
         it = self.iter + 1
         basis = self.basis
         r_old = self.rb[self.ri]
-        d, jdd, _ = self.lls.solve(self.xb[self.uJ], basis, r_old)       # :86-89
         xi = self._free_x(self.uJ)
         rti = 1 - self.ri
         x_t, r_t = self.xb[xi], self.rb[rti]
         # res_old: the update after an accepted first trial is g = -J(x_t)^T r_old, h = V^T g --
         # computed from the same read of V as the trial point itself (speculative)
         fuse = self.ops.fuse_trial and self.version == "res_old"
-        d, jdd, ds, rr1, h1 = self._first_trial(d, jdd, x_t, r_t, r_old, fuse)
+        d, jdd, ds, rr1, h1 = self._first_trial(x_t, r_t, r_old, fuse)     # :86-89, first trial
         last = {"rr": rr1}
 
         def trial(t):                                                     # res_krylow(c + t d)

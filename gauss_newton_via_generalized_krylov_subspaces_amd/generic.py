@@ -96,8 +96,8 @@ class FlatKrylovBasis:
     def gram_k(self):
         return self.k
 
-    def stored_step(self, d):
-        return np.asarray(d, dtype=np.float64)     # columns are stored normalised
+    def step_scale(self):
+        return np.ones(self.k)                     # columns are stored normalised
 
     def start(self, x):
         """ref:krylow.py:30-39."""
@@ -285,4 +285,4 @@ class HostCallableOps:
         return FlatKrylovBasis(self, kmax)
 
     def make_lls(self, kmax):
-        return CholQR2Solver(self, kmax, gram=self.gram, n_global=self.n)
+        return CholQR2Solver(self, kmax, gram=self.gram, n_global=self.n, device_solve=False)

@@ -103,13 +103,10 @@ class DeviceKrylovBasis:
     def _slot(self, j):
         return self.V[j] if j < self.kmax else self._g
 
-    def stored_step(self, d: np.ndarray) -> np.ndarray:
-        """A least-squares step in stored units: sc * d on the settled columns; a pending column's
-        entry is already in its raw (stored) units."""
-        ds = np.array(d, dtype=np.float64)
-        k = min(len(ds), self.k)
-        ds[:k] *= self.sc[:k]
-        return ds
+    def step_scale(self) -> np.ndarray:
+        """Per-column factor from a least-squares step to stored units (ds = step_scale * d): sc on
+        the settled columns, 1 on a pending one (its step is already in raw units)."""
+        return np.append(self.sc[:self.k], 1.0) if self.pend is not None else self.sc[:self.k].copy()
 
     def start(self, x):
         """ref:krylow.py:30-39.  ``x`` is a slab vector valid on owned +-GHOST rows; returns [||x||]."""
@@ -134,15 +131,22 @@ class DeviceKrylovBasis:
         return out
 
     # -- first Armijo trial --------------------------------------------------------------
-    def trial_first(self, e_ext: np.ndarray, out, r_products=None):
+    def trial_first(self, e_ext, out, r_products=None, coef_dev=None):
         """Trial point out = V @ e_ext, e_ext over ``gram_k()`` columns in stored units.  Materialises
         a pending column (pack[1:3] = sum w^2, max |w|) and, with ``r_products``, also computes the update products at u = out with that residual:
         g = -J(out)^T r into the next free slot, pack[3:3+kk] = V^T g (this rank, stored units).
-        Returns the device pack (pack[0] is the caller's residual slot)."""
+        ``coef_dev``: the coefficients already on the device (the device least-squares solve's e_try)
+        instead of the host array e_ext.  Returns the device pack (pack[0]: the caller's residual slot)."""
         kk = self.gram_k()
-        if len(e_ext) != kk:
-            raise RuntimeError("trial_first: coefficient length != basis columns")
-        self.be.upload(self._c, e_ext)
+        if coef_dev is None:
+            if len(e_ext) != kk:
+                raise RuntimeError("trial_first: coefficient length != basis columns")
+            self.be.upload(self._c, e_ext)
+            cdev = self._c
+        else:
+            if coef_dev.numel() < kk:
+                raise RuntimeError("trial_first: device coefficients shorter than the basis")
+            cdev = coef_dev
         pend = self.pend is not None
         if pend:
             if self.pend["slot"] != self.k:
@@ -153,14 +157,14 @@ class DeviceKrylovBasis:
             self._prod_slot = kk
             h = self.pack[3:3 + kk]
             if pend:
-                self.be.gemv_vjp_gemv_t_pending(self.V, self.k, self._c, self._hh, r_products, out, g, h,
+                self.be.gemv_vjp_gemv_t_pending(self.V, self.k, cdev, self._hh, r_products, out, g, h,
                                                 self.pack[1:3])
             else:
-                self.be.gemv_vjp_gemv_t(self.V, kk, self._c, r_products, out, g, h)
+                self.be.gemv_vjp_gemv_t(self.V, kk, cdev, r_products, out, g, h)
         elif pend:
-            self.be.gemv_pending(self.V, self.k, self._c, self._hh, out, self.pack[1:3])
+            self.be.gemv_pending(self.V, self.k, cdev, self._hh, out, self.pack[1:3])
         else:
-            self.be.gemv(self.V, kk, self._c, out)
+            self.be.gemv(self.V, kk, cdev, out)
         return self.pack
 
     def resolve(self, sumsq: float, maxabs: float) -> bool:

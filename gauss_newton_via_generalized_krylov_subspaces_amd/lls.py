@@ -64,10 +64,30 @@ def rank_messages(R):
         print("A is rank deficient")
 
 
+class DeviceSolve:
+    """A least-squares solve enqueued on the device (``CholQR2Solver.launch``): its first pass and
+    the k_lls solve are in the stream; ``out`` / ``e_try`` are device buffers (read with the first
+    Armijo trial's scalars, so the Gram -> trial sequence has no host round trip)."""
+
+    device = True
+
+    def __init__(self, k, kp, M, M_cont, P, rescale, pending, G, out, e_try):
+        self.k, self.kp, self.M, self.M_cont, self.P, self.rescale = k, kp, M, M_cont, P, rescale
+        self.pending, self.G, self.out, self.e_try = pending, G, out, e_try
+
+
+class HostSolve:
+    device = False
+
+    def __init__(self, d, jdd):
+        self.d, self.jdd = d, jdd
+
+
 class CholQR2Solver:
-    def __init__(self, dev, kmax: int, gram=None, n_global=None):
+    def __init__(self, dev, kmax: int, gram=None, n_global=None, device_solve=True):
         """``gram(u, V, k, rinv, r, G)`` fills G with the Gram of [J(u) V RinvAug | r] (default:
-        the Bratu stencil kernel); ``n_global`` = parameter count (for the sCholQR3 shift)."""
+        the Bratu stencil kernel); ``n_global`` = parameter count (for the sCholQR3 shift);
+        ``device_solve``: allow ``launch`` to solve on the device (k_lls)."""
         self.dev = dev
         self.be = dev.backend
         self._gram_fn = gram if gram is not None else self.be.gram
@@ -78,10 +98,21 @@ class CholQR2Solver:
         self.passes = 0
         self.solves = 0
         self.fallbacks = 0
+        self.device_solves = 0
         self.history = []           # per solve: (k, passes, cond(R_Y) of each pass) -- diagnostics
         self.R_prev = None          # R of the last solve (k_prev x k_prev); None: no usable factor
         self.R_last = None          # R of the last solve (diagnostics)
         self._tentative = None      # (R, d) of a solve over a pending column
+        # device solve (k_lls): k <= lsk
+        self.lsk = (min(int(self.be.lls_max_k()), int(kmax))
+                    if device_solve and hasattr(self.be, "lls_solve") else 0)
+        if self.lsk:
+            L = self.lsk
+            self._Pd = self.be.zeros(L * L)
+            self._sdd = self.be.zeros(L)
+            self._ed = self.be.zeros(L)
+            self._out = self.be.zeros(3 + L + 2 * L * L)
+            self._etry = self.be.zeros(L)
 
     # -- basis events (the solver tells us how V changed since the last solve) -------
     def on_append(self, s_new=None):
@@ -91,21 +122,30 @@ class CholQR2Solver:
         """The basis restarted with one column v_0: P = [1], scale from the pass."""
         self.R_prev = np.zeros((0, 0))
 
-    def _gram(self, u, basis, k, T, r):
-        be = self.be
-        kp = be.gram_dim(k, r is not None)
+    def _augment(self, k, T, with_r):
+        kp = self.be.gram_dim(k, with_r)
+        aug = np.zeros((kp, kp))
+        aug[:k, :k] = T
+        if with_r:
+            aug[k, k] = 1.0
+        return aug
+
+    def _gram_device(self, u, basis, k, T, r):
+        """Enqueue one pass; returns the rank-summed Gram as a device tensor (no host read)."""
+        kp = self.be.gram_dim(k, r is not None)
         rinv_dev = None
         if T is not None:
-            aug = np.zeros((kp, kp))
-            aug[:k, :k] = T
-            if r is not None:
-                aug[k, k] = 1.0
             rinv_dev = self._rinv[:kp * kp]
-            be.upload(rinv_dev, aug.reshape(-1))
+            self.be.upload(rinv_dev, self._augment(k, T, r is not None).reshape(-1))
         G = self._G[:kp * kp]
         self._gram_fn(u, basis.V, k, rinv_dev, r, G)
         self.passes += 1
-        return self.dev.comm.sum(G).reshape(kp, kp)
+        return self.dev.comm.sum_device(G)
+
+    def _gram(self, u, basis, k, T, r):
+        kp = self.be.gram_dim(k, r is not None)
+        G = self._gram_device(u, basis, k, T, r)
+        return G.to("cpu").numpy().reshape(kp, kp).copy()
 
     def _initial_preconditioner(self, k):
         """(P, rescale_last): P = R_prev (basis unchanged) or blockdiag(R_prev, 1) (one new column,
@@ -128,16 +168,84 @@ class CholQR2Solver:
         Pinv = scipy.linalg.solve_triangular(P, np.eye(P.shape[0]), lower=False)
         return Pinv if M is None else M @ Pinv
 
+    # -- device solve ------------------------------------------------------------------------
+    def launch(self, u, basis, r, e_ext, sdd):
+        """Start the solve of min ||-J(u) V d - r||.  When the device can take it (a usable
+        preconditioner and k <= lsk): enqueue the first pass and k_lls, which also forms the first
+        trial's coefficients e_try = e_ext + sdd * d on the device -> DeviceSolve.  Otherwise solve
+        on the host -> HostSolve (d, jdd; tentative when a column is pending)."""
+        k = basis.gram_k() if hasattr(basis, "gram_k") else basis.k
+        P, rescale = self._initial_preconditioner(k)
+        if P is None or k > self.lsk:
+            d, jdd, _ = self.solve(u, basis, r)
+            return HostSolve(d, jdd)
+        M = basis.gram_left() if hasattr(basis, "gram_left") else None
+        pending = getattr(basis, "pending", False)
+        if pending:
+            # after the first trial settles the column, its stored vector is w in the units this solve
+            # uses: further passes (continue_host) map it with 1, not sc
+            M_cont = np.diag(np.append(basis.sc[:k - 1], 1.0))
+        else:
+            M_cont = M
+        self.solves += 1
+        self.device_solves += 1
+        P = P.copy()
+        G = self._gram_device(u, basis, k, self._transform(M, P), r)
+        be = self.be
+        be.upload(self._Pd, P.reshape(-1))
+        be.upload(self._sdd, np.asarray(sdd, dtype=np.float64))
+        be.upload(self._ed, np.asarray(e_ext, dtype=np.float64))
+        kp = be.gram_dim(k, True)
+        be.lls_solve(G, kp, k, self._Pd, rescale, self._sdd, self._ed, self._out, self._etry)
+        return DeviceSolve(k, kp, M, M_cont, P, rescale, pending, G, self._out[:3 + k + 2 * k * k],
+                           self._etry[:k])
+
+    def finish(self, ls: DeviceSolve, out: np.ndarray):
+        """Accept the device solve (host copy ``out`` of ls.out) -> (d, jdd), or None when it needs
+        more passes (not SPD, non-finite, or cond(R_Y) > COND_ACCEPT): then ``continue_host``."""
+        k = ls.k
+        status, jdd = out[0], float(out[1])
+        d = out[3:3 + k].copy()
+        R = out[3 + k:3 + k + k * k].reshape(k, k).copy()
+        Ry = out[3 + k + k * k:3 + k + 2 * k * k].reshape(k, k)
+        if status != 0.0 or not (np.isfinite(jdd) and np.all(np.isfinite(d)) and np.all(np.isfinite(R))):
+            return None
+        cond = _cond_upper(Ry)
+        if cond > COND_ACCEPT:
+            return None
+        self.history.append((k, 1, [cond]))
+        if ls.pending:
+            self._tentative = (R, d)
+        else:
+            self._settle(R)
+        return d, jdd
+
+    def continue_host(self, ls: DeviceSolve, u, basis, r):
+        """The device solve needs more passes: continue the CholQR2 / shifted-CholQR passes on the
+        host from the first pass's Gram (a pending column has been settled by the trial since: it is
+        mapped by ls.M_cont).  -> (d, jdd) in the units of the launch (tentative if it was pending)."""
+        self.solves -= 1            # counted again by _passes
+        G0 = ls.G.to("cpu").numpy().reshape(ls.kp, ls.kp).copy()
+        d, jdd, _ = self._passes(u, basis, ls.k, ls.M_cont, ls.P.copy(), ls.rescale, r, ls.pending, G0=G0,
+                                 passes_before=1)
+        return d, jdd
+
+    # -- host solve -------------------------------------------------------------------------
     def solve(self, u, basis, r):
         """(d, jdd, R) for min ||-J(u) V d - r|| over the basis' Gram columns.  With a pending column
         d and R are tentative (raw units of that column, messages deferred): see resolve_pending."""
         k = basis.gram_k() if hasattr(basis, "gram_k") else basis.k
         M = basis.gram_left() if hasattr(basis, "gram_left") else None
         pending = getattr(basis, "pending", False)
-        self.solves += 1
-        p0 = self.passes
-        conds = []
         P, rescale = self._initial_preconditioner(k)
+        if P is not None:
+            P = P.copy()
+        return self._passes(u, basis, k, M, P, rescale, r, pending)
+
+    def _passes(self, u, basis, k, M, P, rescale, r, pending, G0=None, passes_before=0):
+        self.solves += 1
+        p0 = self.passes - passes_before
+        conds = []
         if P is None:
             # classical CholQR2: first pass without preconditioner (T = M, no r column)
             G1 = self._gram(u, basis, k, M, None)[:k, :k]
@@ -148,7 +256,10 @@ class CholQR2Solver:
                 shift = 11.0 * (n * k + k * (k + 1)) * EPS * np.trace(G1)
                 P = _chol_upper(G1 + shift * np.eye(k))
         for it in range(MAX_PASSES):
-            Gp = self._gram(u, basis, k, self._transform(M, P), r)
+            if it == 0 and G0 is not None:
+                Gp = G0
+            else:
+                Gp = self._gram(u, basis, k, self._transform(M, P), r)
             if rescale and it == 0:
                 # the new column's scale ||J v_new|| from this pass: Y[:, k-1] /= s, P[k-1, k-1] = s
                 s2 = Gp[k - 1, k - 1]

@@ -90,9 +90,17 @@ class Comm:
                 m = v
         return s, m
 
-    def sum_except_max(self, t: torch.Tensor, imax: int) -> np.ndarray:
+    def sum_except_max(self, t: torch.Tensor, imax: int, shared: torch.Tensor = None):
         """Rank-ordered sums of every entry of a small per-rank tensor except entry ``imax``, which
-        is the NaN-propagating max over ranks: a step's control scalars in one collective."""
+        is the NaN-propagating max over ranks: a step's control scalars in one collective.  With
+        ``shared`` (a device buffer identical on every rank) -> (sums, host copy of shared), read in
+        the same device-to-host copy on one rank."""
+        if shared is not None:
+            n = t.numel()
+            if self.world == 1:
+                both = torch.cat([t.reshape(-1), shared.reshape(-1)]).to("cpu", torch.float64).numpy()
+                return both[:n].copy(), both[n:].copy()
+            return self.sum_except_max(t, imax), shared.to("cpu", torch.float64).numpy().copy()
         parts = self._gather(t)
         s = parts[0].copy()
         m = float(parts[0][imax])

@@ -88,7 +88,7 @@ int gnk_vjp_gemv_t(gnk_ctx* ctx, const double* u, const double* r,
 int gnk_basis_gemv_vjp_gemv_t(gnk_ctx* ctx, const double* V, int64_t ldv, int k, const double* c, const double* r,
                               double* x, double* g, double* h_out);
 
-/* Deferred Gram-Schmidt (DESIGN.md §5): the basis update of ref:krylow.py:62-73 stores the raw
+/* Deferred Gram-Schmidt (DESIGN.md §5a): the basis update of ref:krylow.py:62-73 stores the raw
  * g = -J^T r as column k of V ("pending") and its projection coefficients hh; the next least-
  * squares pass sees J w through its triangular transform, and the first Armijo trial point
  * materialises w = g - V[:, :k] @ hh in place over column k (whole slab, the rounding of
@@ -104,6 +104,16 @@ int gnk_basis_gemv_pending(gnk_ctx* ctx, const double* V, int64_t ldv, int k, co
 int gnk_basis_gemv_vjp_gemv_t_pending(gnk_ctx* ctx, const double* V, int64_t ldv, int k, const double* c,
                                       const double* hh, const double* r, double* x, double* g, double* h_out,
                                       double* stats_out);
+
+/* One preconditioned CholeskyQR least-squares solve on the device (lls.py), from a
+ * Gram G (kp x kp, row-major, already summed over ranks) of [J V T | r]: optionally rescale the last
+ * column (P[k-1][k-1] = sqrt(G[k-1][k-1])), G[:k,:k] = Ry^T Ry, z = Ry^-T G[:k,k], R = Ry P,
+ * d = -R^-1 z, jdd = ||R d||^2, e_try = e + sdd * d (elementwise).  P: k x k upper triangular.
+ * out = [status (0 ok, 1 not SPD), jdd, s, d (k), R (k*k), Ry (k*k)].  1 <= k <= gnk_lls_max_k().
+ *                                      ref:gauss_newton_krylow.py:16-36, armijo_goldstein.py:50 */
+int gnk_lls_max_k(void);
+int gnk_lls_solve(gnk_ctx* ctx, const double* G, int kp, int k, const double* P, int rescale, const double* sdd,
+                  const double* e, double* out, double* e_try);
 
 /* g -= V[:, :k] @ h on owned rows; stats_out = {sum g**2, max|g|}
  *                                               ref:krylow.py:64,66,71 */

@@ -50,6 +50,39 @@ class NumpyBackend:
     def to_device(self, a):
         return torch.as_tensor(np.asarray(a, dtype=np.float64)).clone()
 
+    def lls_max_k(self):
+        return 32
+
+    def lls_solve(self, G, kp, k, P, rescale, sdd, e, out, e_try):
+        """NumPy double of gnk_lls_solve (same layout of out)."""
+        import scipy.linalg
+        g = G.numpy()[:kp * kp].reshape(kp, kp)[:k + 1, :k + 1].copy()
+        p = P.numpy()[:k * k].reshape(k, k).copy()
+        s = 1.0
+        if rescale:
+            s2 = g[k - 1, k - 1]
+            if np.isfinite(s2) and s2 > 0.0:
+                s = np.sqrt(s2)
+                g[k - 1, :] /= s
+                g[:, k - 1] /= s
+                p[k - 1, k - 1] = s
+        o = out.numpy()
+        o[:3 + k + 2 * k * k] = np.nan
+        try:
+            ry = scipy.linalg.cholesky(g[:k, :k], lower=False)
+            bad = 0.0
+        except np.linalg.LinAlgError:
+            o[0] = 1.0
+            return
+        z = scipy.linalg.solve_triangular(ry, g[:k, k], trans="T", lower=False)
+        R = ry @ p
+        d = -scipy.linalg.solve_triangular(R, z, lower=False)
+        o[0], o[1], o[2] = bad, float(np.sum((R @ d) ** 2)), s
+        o[3:3 + k] = d
+        o[3 + k:3 + k + k * k] = R.reshape(-1)
+        o[3 + k + k * k:3 + k + 2 * k * k] = ry.reshape(-1)
+        e_try.numpy()[:k] = e.numpy()[:k] + sdd.numpy()[:k] * d
+
     def gram_dim(self, k, with_r):
         return ((k + (1 if with_r else 0) + 15) // 16) * 16
 

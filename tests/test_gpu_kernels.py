@@ -430,3 +430,57 @@ def test_jvp_adjoint_and_linearity_8192():
     be.jvp(u, v2, jv2)
     assert torch.equal(jv2, jv * 2.0)
     assert L == (N + 2 * G) * N
+
+
+@pytest.mark.parametrize("k,rescale", [(1, True), (2, False), (7, True), (16, True), (21, True), (32, False)])
+def test_lls_solve_device(k, rescale):
+    """k_lls (one preconditioned CholeskyQR solve on the device) == the host algebra of lls.py
+    (scipy Cholesky / triangular solves) to rounding: d, R, Ry, jdd to 1e-12 relative, e_try exact
+    given the device d."""
+    import scipy.linalg
+    prob, dev, ref = make(24)
+    be = dev.backend
+    rng = np.random.default_rng(k)
+    n = 400
+    Y = rng.standard_normal((n, k + 1))
+    Y[:, :k] = np.linalg.qr(Y[:, :k])[0] @ np.diag(rng.uniform(0.5, 2.0, k))
+    if rescale:
+        Y[:, k - 1] *= 1e3
+    kp = be.gram_dim(k, True)
+    Gh = np.zeros((kp, kp))
+    Gh[:k + 1, :k + 1] = Y.T @ Y
+    P = np.triu(rng.standard_normal((k, k))) + 3 * np.eye(k)
+    if rescale:
+        P[k - 1, :] = 0.0
+        P[k - 1, k - 1] = 1.0
+    sdd = rng.uniform(0.5, 2, k)
+    e = rng.standard_normal(k)
+    out = be.zeros(3 + k + 2 * k * k)
+    etry = be.zeros(k)
+    be.lls_solve(be.to_device(Gh.reshape(-1)), kp, k, be.to_device(P.reshape(-1)), rescale,
+                 be.to_device(sdd), be.to_device(e), out, etry)
+    o = out.cpu().numpy()
+    g = Gh[:k + 1, :k + 1].copy()
+    p = P.copy()
+    if rescale:
+        s = np.sqrt(g[k - 1, k - 1])
+        g[k - 1, :] /= s
+        g[:, k - 1] /= s
+        p[k - 1, k - 1] = s
+        assert o[2] == s
+    ry = scipy.linalg.cholesky(g[:k, :k], lower=False)
+    z = scipy.linalg.solve_triangular(ry, g[:k, k], trans="T", lower=False)
+    R = ry @ p
+    d = -scipy.linalg.solve_triangular(R, z, lower=False)
+    assert o[0] == 0.0
+    np.testing.assert_allclose(o[3:3 + k], d, rtol=1e-11, atol=1e-12 * np.abs(d).max())
+    np.testing.assert_allclose(o[3 + k:3 + k + k * k].reshape(k, k), R, rtol=1e-12, atol=1e-13 * np.abs(R).max())
+    np.testing.assert_allclose(o[3 + k + k * k:].reshape(k, k), ry, rtol=1e-12, atol=1e-13 * np.abs(ry).max())
+    np.testing.assert_allclose(o[1], np.sum((R @ d) ** 2), rtol=1e-11)
+    np.testing.assert_array_equal(etry.cpu().numpy(), e + sdd * o[3:3 + k])
+    # not SPD -> status 1
+    Gb = Gh.copy()
+    Gb[0, 0] = -1.0
+    be.lls_solve(be.to_device(Gb.reshape(-1)), kp, k, be.to_device(P.reshape(-1)), False,
+                 be.to_device(sdd), be.to_device(e), out, etry)
+    assert out[0].item() == 1.0
