@@ -41,6 +41,17 @@ class BratuDevice:
         return self.backend.zeros(n)
 
 
+class DeviceIterate:
+    """What a solver callback receives with ``callback_format="device"``: this rank's slab vector
+    of the iterate (valid on owned +-GHOST rows) and the solver's sum of squares of the residual
+    at it (over all ranks), so per-iteration diagnostics need no host copy of x."""
+
+    __slots__ = ("x", "sumsq", "ops")
+
+    def __init__(self, x, sumsq, ops):
+        self.x, self.sumsq, self.ops = x, sumsq, ops
+
+
 class SingleRankOperator:
     """Evaluate F, J v, J^T w, diag(J^T J) on whole-grid host arrays (one rank) --
     the drop-in behaviour of the reference closures."""

@@ -68,6 +68,8 @@ SIGNATURES = {
     "gnk_cg_update_p": (_c_int, [_c_vp, _c_dbl, _c_int, _c_vp, _c_vp]),
     "gnk_lls_max_k": (_c_int, []),
     "gnk_lls_solve": (_c_int, [_c_vp, _c_vp, _c_int, _c_int, _c_vp, _c_int, _c_vp, _c_vp, _c_vp, _c_vp]),
+    "gnk_lls_next": (_c_int, [_c_vp, _c_int, _c_int, _c_vp, _c_vp, _c_vp, _c_vp, _c_int, _c_vp, _c_vp, _c_vp, _c_vp,
+                              _c_vp, _c_vp]),
     "gnk_probe_mfma_f64": (_c_int, [_c_vp, _c_vp, _c_int, _c_int]),
     "gnk_timer_start": (_c_int, [_c_vp, _c_int, _c_int]),
     "gnk_timer_collect": (_c_int, [_c_vp, ctypes.POINTER(_c_dbl), ctypes.POINTER(_c_dbl), _c_int]),
@@ -286,6 +288,10 @@ class HipBackend:
     def lls_solve(self, G, kp, k, P, rescale, sdd, e, out, e_try):
         self._call("gnk_lls_solve", _p(G), int(kp), int(k), _p(P), int(bool(rescale)), _p(sdd), _p(e), _p(out),
                    _p(e_try))
+
+    def lls_next(self, k, pending, out, e_try, pack, sc, kp_next, T, P, sdd, e, hh, scn):
+        self._call("gnk_lls_next", int(k), int(bool(pending)), _p(out), _p(e_try), _p(pack), _p(sc), int(kp_next),
+                   _p(T), _p(P), _p(sdd), _p(e), _p(hh), _p(scn))
 
     def gram_dim(self, k, with_r):
         return int(self.lib.gnk_gram_padded_dim(int(k), int(bool(with_r))))

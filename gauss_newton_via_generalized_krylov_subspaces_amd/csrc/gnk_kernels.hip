@@ -2007,7 +2007,8 @@ __global__ __launch_bounds__(BLOCK) void k_gram_reduce(const double* __restrict_
 //   G[:k, :k] = Ry^T Ry (unblocked Cholesky, dpotf2's left-looking order);  z = Ry^-T G[:k, k];
 //   R = Ry P;  d = -R^-1 z (dtrsv's column order);  jdd = ||R d||^2;
 //   e_try = e + s_dd * d  (the first Armijo trial point's stored coefficients).
-// out: [status, jdd, s, d (k), R (k x k), Ry (k x k)]; status 0 = ok, 1 = G[:k, :k] not numerically SPD.
+// out: [status, jdd, s, d (k), R (k x k), Ry (k x k), R^-1 (k x k)]; status 0 = ok, 1 = G[:k, :k] not
+// numerically SPD.  (R^-1 feeds the next step's transform, k_lls_next.)
 constexpr int LS_KMAX = 32;
 constexpr int LS_LD = LS_KMAX + 1;
 
@@ -2104,6 +2105,68 @@ __global__ __launch_bounds__(64) void k_lls(const double* __restrict__ Gm, int k
       out[3 + k + i * k + l] = rr[i][l];
       out[3 + k + k * k + i * k + l] = ry[i][l];
     }
+    // column l of R^-1 (back substitution on e_l); rows below l are zero
+    double* rinv = out + 3 + k + 2 * k * k;
+    double xc[LS_KMAX];
+    for (int i = k - 1; i >= 0; --i) {
+      double a = (i == l) ? 1.0 : 0.0;
+      for (int m = i + 1; m <= l; ++m) a = a - rr[i][m] * xc[m];
+      xc[i] = (i <= l) ? a / rr[i][i] : 0.0;
+    }
+    for (int i = 0; i < k; ++i) rinv[i * k + l] = xc[i];
+  }
+}
+
+// The next GNK step's least-squares inputs, on the device (speculative enqueue; lls.py / krylow.py
+// bookkeeping restated): this step solved over k columns (the last one pending if `pending`), its
+// first trial was accepted (t = 1) and the basis update appended a pending column with raw products
+// h = pack[3:3+k] (rank-summed); pack[1] = sum w^2 of this step's pending column.
+//   sc' = [sc[:k-1], 1 / ||w||] (pending) or sc[:k];  hh' = sc' (sc' h);
+//   R_true = R with its last column / ||w|| (pending);  P' = blockdiag(R_true, 1);
+//   T' = [[diag(sc') D R^-1, -hh'], [0, 1]] (+ the r column), D = diag(1, .., ||w||)  (= M' P'^-1);
+//   sdd' = [sc', 1];  e' = [e_try, 0].
+__global__ __launch_bounds__(64) void k_lls_next(int k, int pending, const double* __restrict__ out,
+                                                 const double* __restrict__ etry, const double* __restrict__ pack,
+                                                 const double* __restrict__ sc, int kpn, double* __restrict__ T,
+                                                 double* __restrict__ Pn, double* __restrict__ sddn,
+                                                 double* __restrict__ en, double* __restrict__ hhn,
+                                                 double* __restrict__ scn) {
+  const int l = threadIdx.x;
+  const int kn = k + 1;
+  const double* R = out + 3 + k;
+  const double* rinv = out + 3 + k + 2 * k * k;
+  const double nrm = pending ? sqrt(pack[1]) : 1.0;
+  for (int j = l; j < k; j += 64) {
+    const double scj = (pending && j == k - 1) ? 1.0 / nrm : sc[j];
+    scn[j] = scj;
+    sddn[j] = scj;
+    en[j] = etry[j];
+    hhn[j] = scj * (scj * pack[3 + j]);
+  }
+  if (l == 0) {
+    sddn[k] = 1.0;
+    en[k] = 0.0;
+  }
+  __syncthreads();
+  for (int idx = l; idx < kpn * kpn; idx += 64) {
+    const int i = idx / kpn, j = idx % kpn;
+    double t = 0.0;
+    if (i < k && j < k) {
+      const double di = (pending && i == k - 1) ? nrm : 1.0;
+      t = (scn[i] * di) * rinv[i * k + j];
+    } else if (i < k && j == k) {
+      t = -hhn[i];
+    } else if (i == j && i <= kn) {
+      t = 1.0;                                      // the pending column (i = k) and r (i = k + 1)
+    }
+    T[idx] = t;
+  }
+  for (int idx = l; idx < kn * kn; idx += 64) {
+    const int i = idx / kn, j = idx % kn;
+    double pv = 0.0;
+    if (i < k && j < k) pv = (pending && j == k - 1) ? R[i * k + j] / nrm : R[i * k + j];
+    else if (i == k && j == k) pv = 1.0;
+    Pn[idx] = pv;
   }
 }
 
@@ -3050,6 +3113,19 @@ int gnk_timer_collect(gnk_ctx* ctx, double* ms_out, double* bytes_out, int capac
 
 // tooling: fp64 MFMA issue-rate probe (not part of the solver)
 int gnk_lls_max_k(void) { return LS_KMAX; }
+
+int gnk_lls_next(gnk_ctx* ctx, int k, int pending, const double* out, const double* e_try, const double* pack,
+                 const double* sc, int kp_next, double* T_next, double* P_next, double* sdd_next, double* e_next,
+                 double* hh_next, double* sc_next) {
+  if (!ctx) return -1;
+  if (k < 1 || k + 1 > LS_KMAX) return fail(ctx, "lls_next: k + 1 must be in [2, gnk_lls_max_k()]");
+  if (kp_next < k + 2) return fail(ctx, "lls_next: kp_next < k + 2");
+  if (!out || !e_try || !pack || !sc || !T_next || !P_next || !sdd_next || !e_next || !hh_next || !sc_next)
+    return fail(ctx, "lls_next: NULL argument");
+  hipLaunchKernelGGL(k_lls_next, dim3(1), dim3(64), 0, ctx->stream, k, pending, out, e_try, pack, sc, kp_next,
+                     T_next, P_next, sdd_next, e_next, hh_next, sc_next);
+  return check_launch(ctx, "lls_next");
+}
 
 int gnk_lls_solve(gnk_ctx* ctx, const double* Gm, int kp, int k, const double* P, int rescale, const double* sdd,
                   const double* e, double* out, double* e_try) {

@@ -32,7 +32,7 @@ from typing import Optional
 import numpy as np
 import torch
 
-from ._device import BratuDevice
+from ._device import BratuDevice, DeviceIterate
 from .armijo_goldstein import armijo_device
 from .bratu_pde_problem import BratuJacobianFunction, BratuResidual
 from .krylow import (DeviceKrylovBasis, GeneralizedKrylowSubspaceBreakdown,
@@ -65,6 +65,7 @@ class BratuOps:
 
     jacobian_is_free = True        # J(u) is u itself on the device: no evaluation to schedule
     fuse_trial = True              # the res_old first trial may carry the update products
+    speculate = True               # the next step's solve may be enqueued before this one is read
 
     def __init__(self, problem, y, comm=None, device=None, backend=None):
         self.dev = BratuDevice(problem, comm, device, backend)
@@ -95,6 +96,13 @@ class BratuOps:
         if shared is None:
             return self.comm.sum_except_max(pack, 2), None
         return self.comm.sum_except_max(pack, 2, shared)
+
+    def residual_read(self, x, r, pack, shared, pinned):
+        """``residual_pack`` without waiting: the cross-rank gather and the copy to host are
+        enqueued (slab.Comm.read_async) and ``comm.complete`` waits for them, so the host can
+        enqueue more work in between; the rank-summed pack stays usable on the device."""
+        self.be.residual(x, self.y, r, pack[0:1])
+        return self.comm.read_async(pack, shared, pinned)
 
     def to_host(self, x):
         return self.dev.slab.to_host(x)
@@ -135,6 +143,13 @@ class GNKSolver:
         self.xb = [self.ops.vec() for _ in range(3)]
         self.rb = None           # residual buffers: allocated at setup (generic problems learn m there)
         self.trace = []          # per-iteration (t, k, trials) for tests / diagnostics
+        # speculative enqueue of the next step's least-squares solve
+        self.pipeline = bool(getattr(self.ops, "speculate", False)) and getattr(self.lls, "lsk", 0) > 0
+        self._spec = None        # the next step's device solve, enqueued before this step was read
+        self._halo_done = False  # the pending column's ghost rows were exchanged for the speculation
+        self._par = 0            # device buffer set of the current step's solve (two sets alternate)
+        self._pin = None
+        self.spec_stats = {"hit": 0, "miss": 0}
 
     # -- pieces -------------------------------------------------------------------------
     def _residual(self, x, r) -> float:
@@ -146,11 +161,44 @@ class GNKSolver:
                 return i
         raise RuntimeError("no free iterate buffer")
 
-    def _emit(self, xslab):
+    def _emit(self, xslab, sumsq=None):
         if self.callback is None:
             return
-        x = self.ops.own(xslab) if self.callback_format == "torch" else self.ops.to_host(xslab)
+        if self.callback_format == "device":
+            x = DeviceIterate(xslab, sumsq, self.ops)
+        else:
+            x = self.ops.own(xslab) if self.callback_format == "torch" else self.ops.to_host(xslab)
         self.callback(x=x, nfev=self.nfev, cg_iter=None)
+
+    def _pinned(self):
+        """Host landing buffer of a step's control scalars (pinned, so the read is enqueued)."""
+        if self._pin is None and getattr(self.be, "device", torch.device("cpu")).type == "cuda":
+            L = self.lls.lsk
+            n = self.comm.world * (4 + self.basis.kmax) + 3 + L + 3 * L * L
+            self._pin = torch.empty(n, dtype=torch.float64, pin_memory=True)
+        return self._pin
+
+    def _can_speculate(self, it, kk):
+        """The next step is a plain continuation of this one when it runs at all: no restart or end
+        of the loop after iteration ``it``, and room for one more column in every device buffer."""
+        b = self.basis
+        return (self.pipeline and it % self.restart != 0 and it < self.max_iter - 1
+                and kk + 1 <= min(self.lls.lsk, b.FUSE_KMAX, b.kmax) and kk < self.ops.n_global)
+
+    def _launch_spec(self, ls, rd, x_t, r_t, slot):
+        """Enqueue the next step's Gram pass and device solve now, assuming this step
+        accepts its first trial, its pending column (if any) does not break down and the res_old
+        update appends g = -J(x_t)^T r_old, which the fused trial already wrote into ``slot``:
+        the next pass runs at u = x_t with r = r_t."""
+        par = self._par ^ 1
+        self.basis.halo_slot(slot)
+        sc_dev = self.basis.sc_device(par, ls.k)
+        return self.lls.launch_next(x_t, self.basis, r_t, ls, self.comm.device_sum(rd), sc_dev, par)
+
+    def _drop_spec(self):
+        if self._spec is not None:
+            self._spec = None
+            self.spec_stats["miss"] += 1
 
     # -- loop ---------------------------------------------------------------------------
     def setup(self, x0):
@@ -193,64 +241,81 @@ class GNKSolver:
             self._append_coordinate()
 
     def _trial_plain(self, e_try, x_t, r_t, r_old, prod):
-        """Trial point x_t = V e_try on a settled basis -> (sum r_t^2, raw h or None)."""
+        """Trial point x_t = V e_try on a settled basis -> (sum r_t^2, raw h or None, product slot)."""
         basis = self.basis
         if not prod:
             basis.x(e_try, x_t)
-            return self._residual(x_t, r_t), None
+            return self._residual(x_t, r_t), None, None
         kk = basis.gram_k()
-        pack = basis.trial_first(e_try, x_t, r_old)
+        pack, slot = basis.trial_first(e_try, x_t, r_old)
         host, _ = self.ops.residual_pack(x_t, r_t, pack[:3 + kk])
-        return float(host[0]), host[3:3 + kk].copy()
+        return float(host[0]), host[3:3 + kk].copy(), slot
 
-    def _first_trial(self, x_t, r_t, r_old, fuse):
+    def _first_trial(self, x_t, r_t, r_old, fuse, it):
         """Least-squares solve (ref:gauss_newton_krylow.py:86-89) and Armijo trial t = 1
         (ref:armijo_goldstein.py:56), enqueued back to back when the solve runs on the device (one
         host read for both).  Settles a pending basis column first -- on its breakdown the solve is
         redone without it -- and, for the fused res_old path, computes the basis-update products at
-        the trial point.  Returns (d, jdd, ds, sum r_t^2, raw h or None); ds = d in stored units."""
+        the trial point.  A solve the previous step enqueued speculatively for this basis is adopted
+        instead of launching one; before waiting for this step's read the next step's solve is
+        enqueued the same way when possible.
+        Returns (d, jdd, ds, sum r_t^2, raw h or None, product slot); ds = d in stored units."""
         basis, lls = self.basis, self.lls
         u = self.xb[self.uJ]
+        spec, self._spec = self._spec, None
+        self._par ^= 1
+        self._halo_done = False
         while True:
             kk = basis.gram_k()
             pend = basis.pending
             prod = fuse and kk <= basis.FUSE_KMAX
             e_ext = np.append(self.e, np.zeros(kk - len(self.e)))
             sdd = basis.step_scale()
-            ls = lls.launch(u, basis, r_old, e_ext, sdd)
+            if spec is not None and pend and spec.k == kk:
+                ls = spec
+                lls.adopt(ls, basis)
+            else:
+                ls = lls.launch(u, basis, r_old, e_ext, sdd, par=self._par)
+            spec = None
             if not ls.device and not pend:
                 ds = sdd * ls.d
-                rr, h = self._trial_plain(e_ext + 1.0 * ds, x_t, r_t, r_old, prod)
-                return ls.d, ls.jdd, ds, rr, h
+                rr, h, slot = self._trial_plain(e_ext + 1.0 * ds, x_t, r_t, r_old, prod)
+                return ls.d, ls.jdd, ds, rr, h, slot
             if ls.device:
-                pack = basis.trial_first(None, x_t, r_old if prod else None, coef_dev=ls.e_try)
-                host, lsout = self.ops.residual_pack(x_t, r_t, pack[:3 + kk], ls.out)
+                pack, slot = basis.trial_first(None, x_t, r_old if prod else None, coef_dev=ls.e_try)
+                rd = self.ops.residual_read(x_t, r_t, pack[:3 + kk], ls.out, self._pinned())
+                if prod and self._can_speculate(it, kk):
+                    self._spec = self._launch_spec(ls, rd, x_t, r_t, slot)
+                host, lsout = self.comm.complete(rd, 2)
                 res = lls.finish(ls, lsout)
             else:
                 res = (ls.d, ls.jdd)
-                pack = basis.trial_first(e_ext + 1.0 * (sdd * ls.d), x_t, r_old if prod else None)
+                pack, slot = basis.trial_first(e_ext + 1.0 * (sdd * ls.d), x_t, r_old if prod else None)
                 host, _ = self.ops.residual_pack(x_t, r_t, pack[:3 + kk])
             if pend:
-                it = basis.pend["it"]
+                it_p = basis.pend["it"]
                 if basis.resolve(float(host[1]), float(host[2])):
-                    # ref:krylow.py:66-69 raised in iteration `it`: the basis was not enlarged
-                    self._breakdown_message(it)
+                    # ref:krylow.py:66-69 raised in iteration `it_p`: the basis was not enlarged
+                    self._breakdown_message(it_p)
                     lls.discard_pending()
+                    self._drop_spec()
                     continue
-                self._append_coordinate()                                 # :124 of iteration `it`
+                self._append_coordinate()                                 # :124 of iteration `it_p`
             if res is None:
                 # the device solve needs more passes: finish it on the host, then a new first trial
+                self._drop_spec()
                 d, jdd = lls.continue_host(ls, u, basis, r_old)
                 ds = sdd * d
                 if pend:
                     d = lls.resolve_pending(basis.last_norm)
-                rr, h = self._trial_plain(self.e + 1.0 * ds, x_t, r_t, r_old, prod)
-                return d, jdd, ds, rr, h
+                rr, h, slot = self._trial_plain(self.e + 1.0 * ds, x_t, r_t, r_old, prod)
+                return d, jdd, ds, rr, h, slot
             d, jdd = res
             ds = sdd * d
             if pend:
                 d = lls.resolve_pending(basis.last_norm)
-            return d, jdd, ds, float(host[0]), (host[3:3 + basis.k].copy() if prod else None)
+            self._halo_done = self._spec is not None
+            return d, jdd, ds, float(host[0]), (host[3:3 + basis.k].copy() if prod else None), slot
 
     def step(self) -> bool:
         """One pass of ref:gauss_newton_krylow.py:84-136; returns True when the loop has ended."""
@@ -263,7 +328,7 @@ class GNKSolver:
         # res_old: the update after an accepted first trial is g = -J(x_t)^T r_old, h = V^T g --
         # computed from the same read of V as the trial point itself (speculative)
         fuse = self.ops.fuse_trial and self.version == "res_old"
-        d, jdd, ds, rr1, h1 = self._first_trial(x_t, r_t, r_old, fuse)     # :86-89, first trial
+        d, jdd, ds, rr1, h1, slot1 = self._first_trial(x_t, r_t, r_old, fuse, it)   # :86-89, first trial
         last = {"rr": rr1}
 
         def trial(t):                                                     # res_krylow(c + t d)
@@ -280,12 +345,13 @@ class GNKSolver:
         self.c += t * d                                                   # :98
         self.e = self.e + t * ds              # the coefficients of the accepted trial point, bit for bit
         self.trace.append({"t": t, "k": basis.k, "trials": ntrial})
-        self._emit(x_t)                                                   # :100
+        self._emit(x_t, last["rr"])                                       # :100
         self.iter = it
         self.x_last = xi
         if t ** 2 * np.sum(d ** 2) <= self.tol ** 2 * s:                  # :102-104
             self.success = True
             self.done = True
+            self._drop_spec()
             return True
         uJ_old, self.uJ = self.uJ, xi                                     # :106-108
         self.ops.on_jacobian(self.xb[self.uJ])
@@ -294,7 +360,8 @@ class GNKSolver:
         products = h1 if (h1 is not None and ntrial == 1) else None
         try:
             if self.version == "res_old":
-                basis.update(u_new, r_old, it=it, products=products)
+                basis.update(u_new, r_old, it=it, products=products, prod_slot=slot1,
+                             halo=not self._halo_done)
             elif self.version == "res_new":
                 basis.update(u_new, r_t, it=it)
             elif self.version == "jac_old_res_old":
@@ -325,6 +392,14 @@ class GNKSolver:
             self.c = basis.start(self.xb[xr])
             self.e = self.c.copy()
             self.lls.on_restart()
+        if self._spec is not None:
+            # the guess of _launch_spec: first trial accepted, fused products appended as the pending
+            # column, no restart / end of the loop
+            if (ntrial == 1 and products is not None and not self.done and not restart and basis.pending
+                    and basis.gram_k() == self._spec.k):
+                self.spec_stats["hit"] += 1
+            else:
+                self._drop_spec()
         return self.done
 
     def finish(self, result_format="numpy"):

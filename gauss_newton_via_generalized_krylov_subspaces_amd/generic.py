@@ -116,7 +116,7 @@ class FlatKrylovBasis:
         self.be.flat_gemv(self.V, k, self._c, out)
         return out
 
-    def update(self, u_jac, r, it=None, products=None):
+    def update(self, u_jac, r, it=None, products=None, prod_slot=None, halo=True):
         """ref:krylow.py:55-73 with jac_ev = J(u_jac), res_ev = r (CGS done here, not deferred)."""
         k = self.k
         if k == self.ops.n:                                   # :59-60

@@ -71,8 +71,11 @@ class DeviceKrylovBasis:
         self._hh = self.be.zeros(self.kmax)
         self._h = self.be.zeros(self.kmax + 1)
         self._stats = self.be.zeros(2)
-        # [sum r^2, sum w^2, max |w|, h_0 .. h_k] of a first trial: one collective / host read
-        self.pack = self.be.zeros(3 + self.kmax + 1)
+        # [sum r^2, sum w^2, max |w|, h_0 .. h_k] of a first trial: one collective / host read;
+        # two (a speculatively enqueued next step has its own)
+        self.packs = [self.be.zeros(3 + self.kmax + 1) for _ in range(2)]
+        self.pack = self.packs[0]
+        self._sc_dev = [self.be.zeros(self.kmax) for _ in range(2)]
         self._g = dev.vec()              # raw g when V has no free slot (never pending in a Gram)
 
     @property
@@ -131,41 +134,63 @@ class DeviceKrylovBasis:
         return out
 
     # -- first Armijo trial --------------------------------------------------------------
-    def trial_first(self, e_ext, out, r_products=None, coef_dev=None):
-        """Trial point out = V @ e_ext, e_ext over ``gram_k()`` columns in stored units.  Materialises
-        a pending column (pack[1:3] = sum w^2, max |w|) and, with ``r_products``, also computes the update products at u = out with that residual:
-        g = -J(out)^T r into the next free slot, pack[3:3+kk] = V^T g (this rank, stored units).
-        ``coef_dev``: the coefficients already on the device (the device least-squares solve's e_try)
-        instead of the host array e_ext.  Returns the device pack (pack[0]: the caller's residual slot)."""
+    def enqueue_trial(self, k, pend, out, coef_dev, hh_dev, pack, r_products=None):
+        """First trial point on an explicit basis size (no host state read): k settled columns plus,
+        when ``pend``, the pending raw column k, materialised in place with the device coefficients
+        hh_dev (pack[1:3] = sum w^2, max |w|); out = V @ coef_dev over k + pend columns.  With
+        ``r_products``: also g = -J(out)^T r into slot k + pend and pack[3:] = V^T g (this rank).
+        Returns the product slot (or None)."""
+        kk = k + (1 if pend else 0)
+        if r_products is not None:
+            if kk > self.FUSE_KMAX:
+                raise RuntimeError("fused first trial: too many basis columns")
+            g = self._slot(kk)
+            h = pack[3:3 + kk]
+            if pend:
+                self.be.gemv_vjp_gemv_t_pending(self.V, k, coef_dev, hh_dev, r_products, out, g, h, pack[1:3])
+            else:
+                self.be.gemv_vjp_gemv_t(self.V, kk, coef_dev, r_products, out, g, h)
+            return kk
+        if pend:
+            self.be.gemv_pending(self.V, k, coef_dev, hh_dev, out, pack[1:3])
+        else:
+            self.be.gemv(self.V, kk, coef_dev, out)
+        return None
+
+    def halo_slot(self, j):
+        """Exchange the ghost rows of stored column j (a raw g the next pass reads off-rank)."""
+        self.dev.comm.halo(self._slot(j), self.dev.slab.N, self.dev.slab.nrows)
+
+    def sc_device(self, par, k):
+        """The folded column scales sc[:k] uploaded into device buffer ``par`` (k_lls_next input)."""
+        self.be.upload(self._sc_dev[par], self.sc[:k])
+        return self._sc_dev[par]
+
+    def enqueue_products(self, u_jac, r, k, pack):
+        """The basis-update products of ref:krylow.py:62,64 for a basis of k settled columns:
+        g = -J(u_jac)^T r into slot k, pack[3:3+k] = V^T g (this rank).  Returns the slot."""
+        self.be.vjp_gemv_t(u_jac, r, self.V, k, self._slot(k), pack[3:3 + k])
+        return k
+
+    def trial_first(self, e_ext, out, r_products=None, coef_dev=None, pack=None):
+        """``enqueue_trial`` on the host's current basis (settled k, pending column if any; its hh
+        uploaded), coefficients e_ext (host, stored units) or ``coef_dev``.  Returns (pack, slot)."""
+        pack = self.pack if pack is None else pack
         kk = self.gram_k()
         if coef_dev is None:
             if len(e_ext) != kk:
                 raise RuntimeError("trial_first: coefficient length != basis columns")
             self.be.upload(self._c, e_ext)
-            cdev = self._c
-        else:
-            if coef_dev.numel() < kk:
-                raise RuntimeError("trial_first: device coefficients shorter than the basis")
-            cdev = coef_dev
+            coef_dev = self._c
+        elif coef_dev.numel() < kk:
+            raise RuntimeError("trial_first: device coefficients shorter than the basis")
         pend = self.pend is not None
         if pend:
             if self.pend["slot"] != self.k:
                 raise RuntimeError("pending column is not stored in V")
             self.be.upload(self._hh, self.pend["hh"])
-        if r_products is not None:
-            g = self._slot(kk)
-            self._prod_slot = kk
-            h = self.pack[3:3 + kk]
-            if pend:
-                self.be.gemv_vjp_gemv_t_pending(self.V, self.k, cdev, self._hh, r_products, out, g, h,
-                                                self.pack[1:3])
-            else:
-                self.be.gemv_vjp_gemv_t(self.V, kk, cdev, r_products, out, g, h)
-        elif pend:
-            self.be.gemv_pending(self.V, self.k, cdev, self._hh, out, self.pack[1:3])
-        else:
-            self.be.gemv(self.V, kk, cdev, out)
-        return self.pack
+        slot = self.enqueue_trial(self.k, pend, out, coef_dev, self._hh, pack, r_products)
+        return pack, slot
 
     def resolve(self, sumsq: float, maxabs: float) -> bool:
         """Settle the pending column from its materialisation stats; True on breakdown (:66) --
@@ -190,10 +215,11 @@ class DeviceKrylovBasis:
         return self.resolve(sumsq, maxabs)
 
     # -- basis update ------------------------------------------------------------------------
-    def update(self, u_jac, r, it=None, products=None):
+    def update(self, u_jac, r, it=None, products=None, prod_slot=None, halo=True):
         """ref:krylow.py:55-73 with jac_ev = J(u_jac), res_ev = r (slab vectors), deferred: the new
         column becomes pending (see the module docstring).  ``products``: the rank-summed raw
-        h = V^T g of a fused first trial at u_jac with residual r (g already in the free slot)."""
+        h = V^T g already computed at u_jac with residual r, g in slot ``prod_slot``; ``halo``:
+        False when g's ghost rows were already exchanged (a speculative next step did it)."""
         k = self.k
         if self.pend is not None:
             raise RuntimeError("basis update with a pending column")
@@ -203,14 +229,15 @@ class DeviceKrylovBasis:
             raise RuntimeError("Krylov basis storage exhausted")
         g = self._slot(k)
         if products is not None:
-            if getattr(self, "_prod_slot", None) != k:
+            if prod_slot != k:
                 raise RuntimeError("update products were computed for another basis size")
             h_raw = np.asarray(products[:k], dtype=np.float64)
         else:
             self.be.vjp_gemv_t(u_jac, r, self.V, k, g, self._h)       # g = -J^T r ; h = V^T g (:62, :64)
             h_raw = self.dev.comm.sum(self._h[:k])                   # rank-ordered sum of the partials
-        self._prod_slot = None
+            halo = True
         # g's ghost rows: the next pass applies the stencil to it and materialises w on the whole slab
-        self.dev.comm.halo(g, self.dev.slab.N, self.dev.slab.nrows)
+        if halo:
+            self.dev.comm.halo(g, self.dev.slab.N, self.dev.slab.nrows)
         h = self.sc[:k] * h_raw                                      # reference h = V^T g
         self.pend = {"slot": k, "hh": self.sc[:k] * h, "it": it}

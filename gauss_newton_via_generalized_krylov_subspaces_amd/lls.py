@@ -76,6 +76,22 @@ class DeviceSolve:
         self.pending, self.G, self.out, self.e_try = pending, G, out, e_try
 
 
+class _LSBuffers:
+    """Device inputs / outputs of one device solve; two sets, so that a speculatively enqueued next
+    step never overwrites what the host has not read yet."""
+
+    def __init__(self, be, L, kp):
+        self.T = be.zeros(kp * kp)            # augmented transform of the first pass
+        self.G = be.zeros(kp * kp)            # its Gram
+        self.P = be.zeros(L * L)
+        self.sdd = be.zeros(L)
+        self.e = be.zeros(L)
+        self.out = be.zeros(3 + L + 3 * L * L)
+        self.etry = be.zeros(L)
+        self.hh = be.zeros(L)                 # next step's projection coefficients (k_lls_next)
+        self.sc = be.zeros(L)
+
+
 class HostSolve:
     device = False
 
@@ -106,13 +122,7 @@ class CholQR2Solver:
         # device solve (k_lls): k <= lsk
         self.lsk = (min(int(self.be.lls_max_k()), int(kmax))
                     if device_solve and hasattr(self.be, "lls_solve") else 0)
-        if self.lsk:
-            L = self.lsk
-            self._Pd = self.be.zeros(L * L)
-            self._sdd = self.be.zeros(L)
-            self._ed = self.be.zeros(L)
-            self._out = self.be.zeros(3 + L + 2 * L * L)
-            self._etry = self.be.zeros(L)
+        self.bufs = [_LSBuffers(self.be, self.lsk, kp) for _ in range(2)] if self.lsk else []
 
     # -- basis events (the solver tells us how V changed since the last solve) -------
     def on_append(self, s_new=None):
@@ -130,14 +140,15 @@ class CholQR2Solver:
             aug[k, k] = 1.0
         return aug
 
-    def _gram_device(self, u, basis, k, T, r):
-        """Enqueue one pass; returns the rank-summed Gram as a device tensor (no host read)."""
+    def _gram_device(self, u, basis, k, T, r, T_dev=None, G_dev=None):
+        """Enqueue one pass; returns the rank-summed Gram as a device tensor (no host read).
+        ``T_dev``: the augmented transform already on the device; ``G_dev``: output buffer."""
         kp = self.be.gram_dim(k, r is not None)
-        rinv_dev = None
-        if T is not None:
+        rinv_dev = T_dev[:kp * kp] if T_dev is not None else None
+        if T is not None and T_dev is None:
             rinv_dev = self._rinv[:kp * kp]
             self.be.upload(rinv_dev, self._augment(k, T, r is not None).reshape(-1))
-        G = self._G[:kp * kp]
+        G = (G_dev if G_dev is not None else self._G)[:kp * kp]
         self._gram_fn(u, basis.V, k, rinv_dev, r, G)
         self.passes += 1
         return self.dev.comm.sum_device(G)
@@ -169,7 +180,7 @@ class CholQR2Solver:
         return Pinv if M is None else M @ Pinv
 
     # -- device solve ------------------------------------------------------------------------
-    def launch(self, u, basis, r, e_ext, sdd):
+    def launch(self, u, basis, r, e_ext, sdd, par=0):
         """Start the solve of min ||-J(u) V d - r||.  When the device can take it (a usable
         preconditioner and k <= lsk): enqueue the first pass and k_lls, which also forms the first
         trial's coefficients e_try = e_ext + sdd * d on the device -> DeviceSolve.  Otherwise solve
@@ -190,15 +201,40 @@ class CholQR2Solver:
         self.solves += 1
         self.device_solves += 1
         P = P.copy()
-        G = self._gram_device(u, basis, k, self._transform(M, P), r)
+        B = self.bufs[par]
+        G = self._gram_device(u, basis, k, self._transform(M, P), r, G_dev=B.G)
         be = self.be
-        be.upload(self._Pd, P.reshape(-1))
-        be.upload(self._sdd, np.asarray(sdd, dtype=np.float64))
-        be.upload(self._ed, np.asarray(e_ext, dtype=np.float64))
+        be.upload(B.P, P.reshape(-1))
+        be.upload(B.sdd, np.asarray(sdd, dtype=np.float64))
+        be.upload(B.e, np.asarray(e_ext, dtype=np.float64))
         kp = be.gram_dim(k, True)
-        be.lls_solve(G, kp, k, self._Pd, rescale, self._sdd, self._ed, self._out, self._etry)
-        return DeviceSolve(k, kp, M, M_cont, P, rescale, pending, G, self._out[:3 + k + 2 * k * k],
-                           self._etry[:k])
+        be.lls_solve(G, kp, k, B.P, rescale, B.sdd, B.e, B.out, B.etry)
+        return DeviceSolve(k, kp, M, M_cont, P, rescale, pending, G, B.out[:3 + k + 3 * k * k], B.etry[:k])
+
+    def launch_next(self, u, basis, r, ls: "DeviceSolve", pack_sum, sc_dev, par):
+        """Speculative device solve of the NEXT step, enqueued before the host has read this one:
+        assumes this step (``ls``, pending column or not) accepts its first trial and the basis update
+        appends a pending column with the products in ``pack_sum`` (k_lls_next builds T, P, sdd, e and
+        hh on the device).  The host fields of the returned DeviceSolve (M, M_cont, P) are filled by
+        ``adopt`` once the host state has caught up."""
+        k = ls.k + 1
+        B = self.bufs[par]
+        kp = self.be.gram_dim(k, True)
+        self.be.lls_next(ls.k, ls.pending, ls.out, ls.e_try, pack_sum, sc_dev, kp, B.T, B.P, B.sdd, B.e, B.hh, B.sc)
+        G = self._gram_device(u, basis, k, None, r, T_dev=B.T, G_dev=B.G)
+        self.be.lls_solve(G, kp, k, B.P, True, B.sdd, B.e, B.out, B.etry)
+        return DeviceSolve(k, kp, None, None, None, True, True, G, B.out[:3 + k + 3 * k * k], B.etry[:k])
+
+    def adopt(self, ls: "DeviceSolve", basis):
+        """A speculative solve became the current step: fill its host-side fields from the (now
+        updated) host state -- the same values k_lls_next computed on the device."""
+        k = ls.k
+        self.solves += 1
+        self.device_solves += 1
+        P, rescale = self._initial_preconditioner(k)
+        ls.P = P.copy()
+        ls.M = basis.gram_left()
+        ls.M_cont = np.diag(np.append(basis.sc[:k - 1], 1.0))
 
     def finish(self, ls: DeviceSolve, out: np.ndarray):
         """Accept the device solve (host copy ``out`` of ls.out) -> (d, jdd), or None when it needs

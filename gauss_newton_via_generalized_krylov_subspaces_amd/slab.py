@@ -112,6 +112,71 @@ class Comm:
         s[imax] = m
         return s
 
+    # -- asynchronous read of a step's control scalars ------------------
+    def read_async(self, t: torch.Tensor, shared: torch.Tensor = None, pinned: torch.Tensor = None):
+        """Enqueue the cross-rank gather of a small per-rank device tensor ``t`` (and a copy of
+        ``shared``, identical on every rank) into host memory; returns a handle for ``complete``
+        (the host does not wait here).  ``device_sum(handle)``: the rank-ordered sum on the device,
+        for device-side consumers that must not wait for the host."""
+        n = t.numel()
+        m = shared.numel() if shared is not None else 0
+        on_gpu = t.device.type != "cpu" and pinned is not None
+        if not on_gpu or (self.world > 1 and self.stage):
+            parts = self._gather(t)
+            sh = shared.detach().to("cpu", torch.float64).numpy().copy() if shared is not None else None
+            return _ReadHandle(None, None, n, parts, sh, t)
+        if self.world == 1:
+            gath = t.reshape(-1)
+        else:
+            gath = torch.empty(self.world * n, dtype=t.dtype, device=t.device)
+            dist.all_gather_into_tensor(gath, t.contiguous().reshape(-1), group=self.group)
+        wn = self.world * n
+        host = pinned[:wn + m]
+        host[:wn].copy_(gath, non_blocking=True)
+        if shared is not None:
+            host[wn:].copy_(shared.reshape(-1), non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(t.device))
+        return _ReadHandle(host, ev, n, None, None, gath)
+
+    def device_sum(self, h) -> torch.Tensor:
+        """Rank-ordered sum (on the device) of the tensor behind a read handle."""
+        if self.world == 1:
+            return h.gath
+        if h.gath.numel() == h.n:                 # staged / CPU path: sum on the host, copy back
+            return torch.from_numpy(self._rank_sum(h.parts)).to(h.gath.device)
+        parts = h.gath.view(self.world, -1)
+        s = parts[0].clone()
+        for p in range(1, self.world):
+            s.add_(parts[p])
+        return s
+
+    @staticmethod
+    def _rank_sum(parts):
+        s = parts[0].copy()
+        for p in range(1, parts.shape[0]):
+            s = s + parts[p]
+        return s
+
+    def complete(self, h, imax: int):
+        """Wait for a read handle -> (rank-ordered sums except entry ``imax``: NaN-propagating max
+        over ranks, shared host copy or None)."""
+        if h.ev is not None:
+            h.ev.synchronize()
+            wn = self.world * h.n
+            a = h.host.numpy()
+            h.parts = a[:wn].reshape(self.world, h.n).copy()
+            h.shared = a[wn:].copy() if a.size > wn else None
+        parts = h.parts
+        s = self._rank_sum(parts)
+        m = float(parts[0][imax])
+        for p in range(1, parts.shape[0]):
+            v = float(parts[p][imax])
+            if v > m or math.isnan(v):
+                m = v
+        s[imax] = m
+        return s, h.shared
+
     def sum_device(self, t: torch.Tensor) -> torch.Tensor:
         """Rank-ordered sum of a small per-rank device tensor, left on the device (no host round
         trip on RCCL): the same IEEE additions in the same order as ``sum``."""
@@ -164,6 +229,13 @@ class Comm:
         parts = [None] * self.world
         dist.all_gather_object(parts, host, group=self.group)
         return np.concatenate(parts)
+
+
+class _ReadHandle:
+    __slots__ = ("host", "ev", "n", "parts", "shared", "gath")
+
+    def __init__(self, host, ev, n, parts, shared, gath):
+        self.host, self.ev, self.n, self.parts, self.shared, self.gath = host, ev, n, parts, shared, gath
 
 
 class Slab:

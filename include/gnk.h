@@ -109,11 +109,21 @@ int gnk_basis_gemv_vjp_gemv_t_pending(gnk_ctx* ctx, const double* V, int64_t ldv
  * Gram G (kp x kp, row-major, already summed over ranks) of [J V T | r]: optionally rescale the last
  * column (P[k-1][k-1] = sqrt(G[k-1][k-1])), G[:k,:k] = Ry^T Ry, z = Ry^-T G[:k,k], R = Ry P,
  * d = -R^-1 z, jdd = ||R d||^2, e_try = e + sdd * d (elementwise).  P: k x k upper triangular.
- * out = [status (0 ok, 1 not SPD), jdd, s, d (k), R (k*k), Ry (k*k)].  1 <= k <= gnk_lls_max_k().
- *                                      ref:gauss_newton_krylow.py:16-36, armijo_goldstein.py:50 */
+ * out = [status (0 ok, 1 not SPD), jdd, s, d (k), R (k*k), Ry (k*k), R^-1 (k*k)].
+ * 1 <= k <= gnk_lls_max_k().           ref:gauss_newton_krylow.py:16-36, armijo_goldstein.py:50 */
 int gnk_lls_max_k(void);
 int gnk_lls_solve(gnk_ctx* ctx, const double* G, int kp, int k, const double* P, int rescale, const double* sdd,
                   const double* e, double* out, double* e_try);
+/* The next step's least-squares inputs on the device, assuming this step (k columns, the last one
+ * pending if pending != 0) accepts its first trial and appends a pending column with the rank-summed
+ * raw products h = pack[3:3+k] (pack[1] = sum w**2 of this step's pending column): sc_next, hh_next
+ * (k), the augmented transform T_next (kp_next x kp_next) = [[diag(sc') D R^-1, -hh'], [0, 1]] (+ r),
+ * P_next = blockdiag(R_true, 1) ((k+1) x (k+1)), sdd_next = [sc', 1], e_next = [e_try, 0].
+ * Lets the host enqueue step i+1 before it has read step i.
+ *                                         ref:krylow.py:64-73, gauss_newton_krylow.py:98,124 */
+int gnk_lls_next(gnk_ctx* ctx, int k, int pending, const double* out, const double* e_try, const double* pack,
+                 const double* sc, int kp_next, double* T_next, double* P_next, double* sdd_next, double* e_next,
+                 double* hh_next, double* sc_next);
 
 /* g -= V[:, :k] @ h on owned rows; stats_out = {sum g**2, max|g|}
  *                                               ref:krylow.py:64,66,71 */

@@ -67,7 +67,7 @@ class NumpyBackend:
                 g[:, k - 1] /= s
                 p[k - 1, k - 1] = s
         o = out.numpy()
-        o[:3 + k + 2 * k * k] = np.nan
+        o[:3 + k + 3 * k * k] = np.nan
         try:
             ry = scipy.linalg.cholesky(g[:k, :k], lower=False)
             bad = 0.0
@@ -81,7 +81,36 @@ class NumpyBackend:
         o[3:3 + k] = d
         o[3 + k:3 + k + k * k] = R.reshape(-1)
         o[3 + k + k * k:3 + k + 2 * k * k] = ry.reshape(-1)
+        o[3 + k + 2 * k * k:3 + k + 3 * k * k] = scipy.linalg.solve_triangular(R, np.eye(k), lower=False).reshape(-1)
         e_try.numpy()[:k] = e.numpy()[:k] + sdd.numpy()[:k] * d
+
+    def lls_next(self, k, pending, out, e_try, pack, sc, kp_next, T, P, sdd, e, hh, scn):
+        """NumPy double of gnk_lls_next (the next step's transform, preconditioner, scales)."""
+        o, pk = out.numpy(), pack.numpy()
+        R = o[3 + k:3 + k + k * k].reshape(k, k)
+        rinv = o[3 + k + 2 * k * k:3 + k + 3 * k * k].reshape(k, k)
+        nrm = np.sqrt(pk[1]) if pending else 1.0
+        s = sc.numpy()[:k].copy()
+        dd = np.ones(k)
+        if pending:
+            s[k - 1] = 1.0 / nrm
+            dd[k - 1] = nrm
+        h = s * (s * pk[3:3 + k])
+        t = np.zeros((kp_next, kp_next))
+        t[:k, :k] = (s * dd)[:, None] * rinv
+        t[:k, k] = -h
+        t[k, k] = t[k + 1, k + 1] = 1.0
+        T.numpy()[:kp_next * kp_next] = t.reshape(-1)
+        p = np.zeros((k + 1, k + 1))
+        p[:k, :k] = R
+        if pending:
+            p[:k, k - 1] = R[:, k - 1] / nrm
+        p[k, k] = 1.0
+        P.numpy()[:(k + 1) ** 2] = p.reshape(-1)
+        scn.numpy()[:k] = s
+        hh.numpy()[:k] = h
+        sdd.numpy()[:k + 1] = np.append(s, 1.0)
+        e.numpy()[:k + 1] = np.append(e_try.numpy()[:k], 0.0)
 
     def gram_dim(self, k, with_r):
         return ((k + (1 if with_r else 0) + 15) // 16) * 16

@@ -455,7 +455,7 @@ def test_lls_solve_device(k, rescale):
         P[k - 1, k - 1] = 1.0
     sdd = rng.uniform(0.5, 2, k)
     e = rng.standard_normal(k)
-    out = be.zeros(3 + k + 2 * k * k)
+    out = be.zeros(3 + k + 3 * k * k)
     etry = be.zeros(k)
     be.lls_solve(be.to_device(Gh.reshape(-1)), kp, k, be.to_device(P.reshape(-1)), rescale,
                  be.to_device(sdd), be.to_device(e), out, etry)
@@ -484,3 +484,36 @@ def test_lls_solve_device(k, rescale):
     be.lls_solve(be.to_device(Gb.reshape(-1)), kp, k, be.to_device(P.reshape(-1)), False,
                  be.to_device(sdd), be.to_device(e), out, etry)
     assert out[0].item() == 1.0
+
+
+@pytest.mark.parametrize("k,pending", [(1, False), (1, True), (5, True), (12, False), (20, True), (31, True)])
+def test_lls_next_device(k, pending):
+    """k_lls_next (the next step's transform / preconditioner / scales) == the NumPy
+    double of the same bookkeeping (tests/numpy_backend.py), and k_lls's R^-1 block == R^-1."""
+    from tests.numpy_backend import NumpyBackend
+    prob, dev, ref = make(24)
+    be = dev.backend
+    rng = np.random.default_rng(100 + k)
+    kp = be.gram_dim(k, True)
+    Y = rng.standard_normal((300, k + 1))
+    Gh = np.zeros((kp, kp))
+    Gh[:k + 1, :k + 1] = Y.T @ Y
+    P = np.triu(rng.standard_normal((k, k))) + 3 * np.eye(k)
+    sdd, e = rng.uniform(0.5, 2, k), rng.standard_normal(k)
+    out, etry = be.zeros(3 + k + 3 * k * k), be.zeros(k)
+    be.lls_solve(be.to_device(Gh.reshape(-1)), kp, k, be.to_device(P.reshape(-1)), True, be.to_device(sdd),
+                 be.to_device(e), out, etry)
+    o = out.cpu().numpy()
+    R = o[3 + k:3 + k + k * k].reshape(k, k)
+    Rinv = o[3 + k + 2 * k * k:].reshape(k, k)
+    np.testing.assert_allclose(Rinv @ R, np.eye(k), rtol=0, atol=1e-12)
+    pack = np.concatenate([[1.0, rng.uniform(0.5, 3.0), 0.1], rng.standard_normal(k)])
+    sc = rng.uniform(0.5, 2.0, k)
+    kpn = be.gram_dim(k + 1, True)
+    nb = NumpyBackend()
+    dv = [be.zeros(n) for n in (kpn * kpn, (k + 1) ** 2, k + 1, k + 1, k, k)]
+    hv = [torch.zeros(n, dtype=torch.float64) for n in (kpn * kpn, (k + 1) ** 2, k + 1, k + 1, k, k)]
+    be.lls_next(k, pending, out, etry, be.to_device(pack), be.to_device(sc), kpn, *dv)
+    nb.lls_next(k, pending, out.cpu(), etry.cpu(), torch.from_numpy(pack), torch.from_numpy(sc), kpn, *hv)
+    for d_, h_ in zip(dv, hv):
+        np.testing.assert_allclose(d_.cpu().numpy(), h_.numpy(), rtol=1e-15, atol=0)
