@@ -308,6 +308,7 @@ def main():
                 "frac_of_peak": j_gbs / HBM_PEAK_GBS, "algorithmic_bytes": jl[0][1]},
         "step_algorithmic_GBs": total_bytes / elapsed / 1e9,
         "gram_passes_per_step": ppi,
+        "speculated_solves": dict(solver.spec_stats),
     }
     if cg_line is not None:
         result["gn_cg"] = cg_line

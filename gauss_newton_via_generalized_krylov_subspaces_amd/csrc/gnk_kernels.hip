@@ -1798,6 +1798,134 @@ __global__ __launch_bounds__(64 * GS_NW) __attribute__((amdgpu_waves_per_eu(WPE)
   for (int t = tid; t < PL; t += blockDim.x) out[t] = red[t];
 }
 
+// ---------------------------------------------------------------- VALU Gram pass (k <= 8, with r)
+// An f64 MFMA issues no more flops per cycle than f64 VALU FMAs on MI355X (tools/probes), and a
+// 16 x 16 MFMA tile spends most of them on padding when the Gram has K + 1 <= 9 columns.  Here the
+// whole pass is VALU: every lane owns two adjacent grid points of a 128-point strip and marches
+// down a range of rows, loading ONE new row of every column per step (16 B per lane; the row above
+// and the current row stay in registers, in-row neighbours come from the adjacent lanes, the
+// strip's outer neighbours from the edge lanes' own loads).  Per point it builds J v in the staged
+// kernel's FMA order, applies the upper-triangular transform T (wave-uniform: scalar operands),
+// appends r, and accumulates the (K + 1)(K + 2) / 2 Gram entries in registers (point 2l, then
+// 2l + 1, row by row).  partial[block][NT]: the block's packed upper triangle, row-major
+// (row i holds columns i..K), waves summed in order.
+template <int K>
+__device__ __forceinline__ void gram_v_point(const double (&a)[K], double rv, const double* __restrict__ T, int ldt,
+                                             double (&acc)[(K + 1) * (K + 2) / 2]) {
+  double y[K + 1];
+#pragma unroll
+  for (int col = 0; col < K; ++col) {
+    double t = a[0] * T[col];
+#pragma unroll
+    for (int i = 1; i <= col; ++i) t = fma(a[i], T[i * ldt + col], t);
+    y[col] = t;
+  }
+  y[K] = rv;
+  int q = 0;
+#pragma unroll
+  for (int i = 0; i <= K; ++i)
+#pragma unroll
+    for (int j = i; j <= K; ++j, ++q) acc[q] = fma(y[i], y[j], acc[q]);
+}
+
+constexpr int GV_KMAX = 8;
+constexpr int GV_SW = 128;           // strip width: 64 lanes x 2 points
+
+template <int K>
+__global__ __launch_bounds__(BLOCK) void k_gram_v(const double* __restrict__ u, const double* __restrict__ V,
+                                                  int64_t ldv, const double* __restrict__ T, int ldt,
+                                                  const double* __restrict__ r, Geo geo, Coef c, int64_t rpr,
+                                                  double* __restrict__ partial) {
+  constexpr int NT = (K + 1) * (K + 2) / 2;
+  __shared__ double red[BLOCK / 64][NT];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int64_t N = geo.N;
+  const int64_t nstrips = N / GV_SW;
+  const int64_t gw = int64_t(blockIdx.x) * (BLOCK / 64) + wave;
+  const int64_t x0 = (gw / nstrips) * rpr;
+  const int64_t x1 = min(geo.nrows, x0 + rpr);
+  const int64_t iy0 = (gw % nstrips) * GV_SW + 2 * lane;
+  const double cw0 = iy0 > 0 ? c.hm2 : 0.0, ce1 = iy0 + 2 < N ? c.hm2 : 0.0;
+  const double up = -c.j_lin_up;
+  const bool edge_w = lane == 0, edge_e = lane == 63;
+  const int eoff = edge_w ? -1 : 2;                 // the edge lanes' outer neighbour (others: unused)
+  double acc[NT];
+#pragma unroll
+  for (int q = 0; q < NT; ++q) acc[q] = 0.0;
+  if (x0 < x1) {
+    d2 vn[K], vc[K];
+    int64_t i = (G + x0) * N + iy0;
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+      vn[j] = *reinterpret_cast<const d2*>(V + j * ldv + i - N);
+      vc[j] = *reinterpret_cast<const d2*>(V + j * ldv + i);
+    }
+    for (int64_t x = x0; x < x1; ++x, i += N) {
+      d2 vs[K];
+      double eo[K];
+#pragma unroll
+      for (int j = 0; j < K; ++j) {
+        const double* cp = V + j * ldv + i;
+        vs[j] = *reinterpret_cast<const d2*>(cp + N);
+        eo[j] = cp[eoff];
+      }
+      const d2 uu = *reinterpret_cast<const d2*>(u + i);
+      const d2 rr = *reinterpret_cast<const d2*>(r + i);
+      const double dn0 = -jdiag(c, uu.x), dn1 = -jdiag(c, uu.y);
+      double a[K];
+#pragma unroll
+      for (int j = 0; j < K; ++j) {
+        double w = __shfl_up(vc[j].y, 1);
+        if (edge_w) w = eo[j];
+        double s0 = c.hm2 * vn[j].x;
+        s0 = fma(cw0, w, s0);
+        s0 = fma(dn0, vc[j].x, s0);
+        s0 = fma(c.hm2, vc[j].y, s0);
+        s0 = fma(up, vs[j].x, s0);
+        a[j] = s0;
+      }
+      gram_v_point<K>(a, rr.x, T, ldt, acc);
+#pragma unroll
+      for (int j = 0; j < K; ++j) {
+        double e = __shfl_down(vc[j].x, 1);
+        if (edge_e) e = eo[j];
+        double s1 = c.hm2 * vn[j].y;
+        s1 = fma(c.hm2, vc[j].x, s1);
+        s1 = fma(dn1, vc[j].y, s1);
+        s1 = fma(ce1, e, s1);
+        s1 = fma(up, vs[j].y, s1);
+        a[j] = s1;
+        vn[j] = vc[j];
+        vc[j] = vs[j];
+      }
+      gram_v_point<K>(a, rr.y, T, ldt, acc);
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < NT; ++q) {
+    const double sq = wave_sum(acc[q]);
+    if (lane == 0) red[wave][q] = sq;
+  }
+  __syncthreads();
+  for (int q = threadIdx.x; q < NT; q += BLOCK) {
+    double sq = red[0][q];
+    for (int w = 1; w < BLOCK / 64; ++w) sq += red[w][q];
+    partial[size_t(blockIdx.x) * NT + q] = sq;
+  }
+}
+
+// packed upper triangle (K1 columns) -> symmetric G[KP][KP]
+__global__ __launch_bounds__(64) void k_gram_scatter_v(const double* __restrict__ red, int K1, int KP,
+                                                       double* __restrict__ Gout) {
+  for (int i = 0, q = 0; i < K1; ++i)
+    for (int j = i; j < K1; ++j, ++q)
+      if (q % 64 == int(threadIdx.x)) {
+        Gout[i * KP + j] = red[q];
+        Gout[j * KP + i] = red[q];
+      }
+}
+
 // staged-kernel scatter: red = block-summed partials [256 MFMA tile | 64 lanes x NACC]
 //   G[c][c'] (c, c' < 16) from the MFMA tile, G[16 + t][c] from the tail sums, G[k][c], G[k][k]
 //   from the r sums; lane groups g = l >> 4 (points) summed in order 0..3.
@@ -2646,6 +2774,50 @@ int gnk_gram(gnk_ctx* ctx, const double* u, const double* V, int64_t ldv, int k,
   if (rinv && ldr != KP) return fail(ctx, "gram: rinv must be the kp x kp augmented inverse (ldr == kp)");
   const int nb = KP / 16;
   const int P = nb * (nb + 1) / 2;
+  // VALU pass for small k with r (every preconditioned pass at k <= 8); GNK_GRAM_VALU=0 disables it,
+  // GNK_GRAM_STAGED=2 (tests) forces the staged kernel instead
+  const char* valu_s = getenv("GNK_GRAM_VALU");
+  const char* staged_f = getenv("GNK_GRAM_STAGED");
+  if (r && k <= GV_KMAX && ctx->geo.N % GV_SW == 0 && !(valu_s && atoi(valu_s) == 0) &&
+      !(staged_f && atoi(staged_f) == 2) && !getenv("GNK_DEBUG_GRAM")) {
+    const double* tv = rinv ? rinv : ctx->ident + ident_offset(KP / 16);
+    const int64_t nstrips = ctx->geo.N / GV_SW;
+    const int64_t nrows = ctx->geo.nrows;
+    // about 8 waves per CU, whole row ranges per strip
+    int64_t nranges = std::max<int64_t>(1, std::min<int64_t>(nrows, int64_t(ctx->num_cus) * 8 / nstrips));
+    const int64_t rpr = (nrows + nranges - 1) / nranges;
+    nranges = (nrows + rpr - 1) / rpr;
+    const int64_t nwaves = nstrips * nranges;
+    const int64_t nblk = (nwaves + BLOCK / 64 - 1) / (BLOCK / 64);
+    const int NT = (k + 1) * (k + 2) / 2;
+    if (nblk > (1 << 20) || size_t(nblk) * NT > SCRATCH_DOUBLES - size_t(NT))
+      return fail(ctx, "gram: scratch too small (valu)");
+    const int64_t nown = nrows * ctx->geo.N;
+    TimedLaunch tlv(ctx, GNK_TIMER_GRAM, 8.0 * double(nown) * double(k + 2));
+#define GRAMV(KV)                                                                                            \
+  hipLaunchKernelGGL((k_gram_v<KV>), dim3(unsigned(nblk)), dim3(BLOCK), 0, ctx->stream, u, V, ldv, tv, KP, r, \
+                     ctx->geo, ctx->coef, rpr, ctx->scratch)
+    switch (k) {
+      case 1: GRAMV(1); break;
+      case 2: GRAMV(2); break;
+      case 3: GRAMV(3); break;
+      case 4: GRAMV(4); break;
+      case 5: GRAMV(5); break;
+      case 6: GRAMV(6); break;
+      case 7: GRAMV(7); break;
+      default: GRAMV(8); break;
+    }
+#undef GRAMV
+    tlv.done();
+    int rcv = check_launch(ctx, "gram_v");
+    if (rcv) return rcv;
+    (void)hipMemsetAsync(G_out, 0, size_t(KP) * KP * sizeof(double), ctx->stream);
+    double* red = ctx->scratch + (SCRATCH_DOUBLES - size_t(NT));
+    rcv = wreduce(ctx, ctx->scratch, int(nblk), NT, int64_t(NT), NT, 0, nullptr, red);
+    if (rcv) return rcv;
+    hipLaunchKernelGGL(k_gram_scatter_v, dim3(1), dim3(64), 0, ctx->stream, red, k + 1, KP, G_out);
+    return check_launch(ctx, "gram scatter (valu)");
+  }
   // staged kernel (measured faster than the chunked / marching kernels for the preconditioned
   // pass from k = 4 up; the marching kernel stays faster for the plain pass);
   // GNK_GRAM_STAGED=2 forces it for every pass (tests), 0 disables it

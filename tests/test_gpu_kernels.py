@@ -250,7 +250,11 @@ def test_cgs_max_propagates_nan():
                                                   # staged kernel: one block, k = 16 with r, tails 1..4
                                                   (256, 16, True, True), (256, 17, True, True), (128, 18, False, True),
                                                   (256, 19, True, False), (1024, 16, True, True), (256, 4, True, True),
-                                                  (512, 12, True, True), (384, 9, False, True)])
+                                                  (512, 12, True, True), (384, 9, False, True),
+                                                  # VALU kernel (N % 128 == 0, k <= 8 with r)
+                                                  (128, 1, True, False), (256, 2, True, True), (384, 3, True, True),
+                                                  (256, 5, True, True), (1024, 6, True, True), (640, 7, True, False),
+                                                  (1024, 8, True, True)])
 @pytest.mark.parametrize("staged", ["default", "forced", "ring4"])
 def test_gram_mfma(N, k, with_r, with_rinv, staged, monkeypatch):
     """W = [J V | r] @ RinvAug on fp64 MFMA vs an fp64 NumPy Gram (host BLAS).  "forced" runs
@@ -475,9 +479,10 @@ def test_lls_solve_device(k, rescale):
     assert o[0] == 0.0
     np.testing.assert_allclose(o[3:3 + k], d, rtol=1e-11, atol=1e-12 * np.abs(d).max())
     np.testing.assert_allclose(o[3 + k:3 + k + k * k].reshape(k, k), R, rtol=1e-12, atol=1e-13 * np.abs(R).max())
-    np.testing.assert_allclose(o[3 + k + k * k:].reshape(k, k), ry, rtol=1e-12, atol=1e-13 * np.abs(ry).max())
+    np.testing.assert_allclose(o[3 + k + k * k:3 + k + 2 * k * k].reshape(k, k), ry, rtol=1e-12, atol=1e-13 * np.abs(ry).max())
     np.testing.assert_allclose(o[1], np.sum((R @ d) ** 2), rtol=1e-11)
     np.testing.assert_array_equal(etry.cpu().numpy(), e + sdd * o[3:3 + k])
+    np.testing.assert_allclose(o[3 + k + 2 * k * k:].reshape(k, k) @ R, np.eye(k), rtol=0, atol=1e-12)
     # not SPD -> status 1
     Gb = Gh.copy()
     Gb[0, 0] = -1.0
