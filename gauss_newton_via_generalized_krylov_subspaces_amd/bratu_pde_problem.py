@@ -112,8 +112,18 @@ class BratuPdeProblem:
         return BratuJacobianFunction(self)
 
     def make_error(self):
-        """ref:bratu_pde_problem.py:98-99"""
-        return lambda u: np.linalg.norm(self.u_true - _host(u))
+        """u -> ||u_true - u|| (ref:bratu_pde_problem.py:98-99); recognised by ``benchmark_method``."""
+        return BratuError(self)
+
+
+class BratuError:
+    """error(u) = ||u_true - u||; ``benchmark.benchmark_method`` evaluates it on the device."""
+
+    def __init__(self, problem: BratuPdeProblem):
+        self.problem = problem
+
+    def __call__(self, u):
+        return np.linalg.norm(self.problem.u_true - _host(u))
 
 
 def _host(a):

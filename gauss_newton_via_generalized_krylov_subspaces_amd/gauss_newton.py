@@ -28,7 +28,7 @@ from typing import Optional
 import numpy as np
 import torch
 
-from ._device import BratuDevice
+from ._device import BratuDevice, DeviceIterate
 from .armijo_goldstein import armijo_device
 from .gauss_newton_krylow import _noop, resolve_bratu
 from .regression_result import RegressionResult
@@ -325,7 +325,10 @@ class GNSolver:
         self.trace.append({"t": t, "trials": ntrial, "cg_iter": self.cg_iter})
         if self.callback is not None:
             xs = self.xb[self.xi]
-            xo = ops.own(xs) if self.callback_format == "torch" else ops.to_host(xs)
+            if self.callback_format == "device":
+                xo = DeviceIterate(xs, self.rr, ops)
+            else:
+                xo = ops.own(xs) if self.callback_format == "torch" else ops.to_host(xs)
             self.callback(x=xo, nfev=self.nfev, cg_iter=self.cg_iter)
         if t ** 2 * dd <= self.tol ** 2 * s:                         # :129-131
             self.success = True

@@ -1,0 +1,99 @@
+"""benchmark_method (ref:benchmark.py:14-55): device-side traces vs the traces the
+reference's own host recipe produces on the CPU oracle run, and vs the golden per-iteration
+residual norms / nfev.  CPU: the NumPy test double of the C-ABI; GPU: the HIP path."""
+import contextlib
+import io
+
+import numpy as np
+import pytest
+
+import gauss_newton_via_generalized_krylov_subspaces_amd as gnk
+from oracle import gnk_oracle as O
+
+
+def host_traces(method, prob_o, y, u0, kwargs):
+    """The reference's benchmark_method recipe on the oracle (host callables, host error/loss)."""
+    res, jac = prob_o.make_res(y), prob_o.make_jac()
+    u_true = prob_o.u_true
+
+    def error(u):
+        return np.linalg.norm(u_true - u)
+
+    with contextlib.redirect_stdout(io.StringIO()):
+        return gnk.benchmark_method(method, res, u0, jac, error, kwargs=kwargs)
+
+
+def device_traces(method, N, y, u0, kwargs):
+    prob = gnk.BratuPdeProblem(N + 1, 5, 10)
+    with contextlib.redirect_stdout(io.StringIO()):
+        return gnk.benchmark_method(method, prob.make_res(y), u0, prob.make_jac(), prob.make_error(), kwargs=kwargs)
+
+
+def compare(dev, ref, golden_case=None):
+    err_d, loss_d, nfev_d, cg_d = dev
+    err_r, loss_r, nfev_r, cg_r = ref
+    assert nfev_d == nfev_r
+    assert cg_d == cg_r
+    assert len(err_d) == len(err_r) == len(loss_d) == len(loss_r)
+    np.testing.assert_allclose(err_d, err_r, rtol=1e-10)
+    np.testing.assert_allclose(loss_d, loss_r, rtol=1e-10, atol=1e-10 * loss_r[0])
+    if golden_case is not None:
+        pi = golden_case["per_iter"]
+        assert nfev_d == gnk.reverse_accumulation(pi["nfev"])
+        np.testing.assert_allclose(loss_d[1:], 0.5 * np.asarray(pi["rnorm"]) ** 2, rtol=2e-10,
+                                   atol=1e-10 * loss_r[0])
+
+
+def test_reverse_accumulation():
+    assert gnk.reverse_accumulation([]) == []
+    assert gnk.reverse_accumulation([2, 3, 7, 8]) == [2, 1, 4, 1]
+
+
+@pytest.mark.parametrize("method,kw,case", [
+    ("gnk", {"max_iter": 100}, "bratu24_res_old_rNone"),
+    ("gnk", {"version": "res_new", "max_iter": 100, "krylow_restart": 20}, None),
+    ("gn", {}, "bratu24_gn")])
+def test_benchmark_traces_host_logic(golden, method, kw, case):
+    from tests.numpy_backend import NumpyBackend
+    meta, arr = golden
+    prob_o = O.BratuPdeProblem(25, 5, 10)
+    y, u0 = arr["bratu24_y"], arr["bratu24_u0"]
+    mo = O.gauss_newton_krylow if method == "gnk" else O.gauss_newton
+    md = gnk.gauss_newton_krylow if method == "gnk" else gnk.gauss_newton
+    ref = host_traces(mo, prob_o, y, u0, kw)
+    dev = device_traces(md, 24, y, u0, dict(kw, _backend=NumpyBackend()))
+    compare(dev, ref, meta["cases"][case] if case else None)
+
+
+def test_benchmark_generic_callables_match_reference_recipe(golden):
+    """Non-Bratu callables (here the oracle's own closures) take the reference's host path."""
+    meta, arr = golden
+    prob_o = O.BratuPdeProblem(25, 5, 10)
+    y, u0 = arr["bratu24_y"], arr["bratu24_u0"]
+    a = host_traces(O.gauss_newton_krylow, prob_o, y, u0, {"max_iter": 30})
+    res, jac = prob_o.make_res(y), prob_o.make_jac()
+    errs = []
+    with contextlib.redirect_stdout(io.StringIO()):
+        O.gauss_newton_krylow(res, u0, jac, max_iter=30,
+                              callback=lambda x, nfev, cg_iter: errs.append(np.linalg.norm(prob_o.u_true - x)))
+    np.testing.assert_array_equal(a[0][1:], errs)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("N,method,kw,case", [
+    (24, "gnk", {"max_iter": 100}, "bratu24_res_old_rNone"),
+    (24, "gnk", {"version": "res_new", "max_iter": 100}, "bratu24_res_new_rNone"),
+    (24, "gn", {"cg_preconditioner": True}, "bratu24_gn_precond"),
+    (100, "gnk", {"version": "res_new", "max_iter": 100}, "bratu100_res_new_rNone")])
+def test_benchmark_traces_gpu(golden, N, method, kw, case):
+    meta, arr = golden
+    if N == 24:
+        prob_o = O.BratuPdeProblem(25, 5, 10)
+        y, u0 = arr["bratu24_y"], arr["bratu24_u0"]
+    else:
+        prob_o, y, u0 = O.bratu_workload(N)
+    mo = O.gauss_newton_krylow if method == "gnk" else O.gauss_newton
+    md = gnk.gauss_newton_krylow if method == "gnk" else gnk.gauss_newton
+    ref = host_traces(mo, prob_o, y, u0, kw)
+    dev = device_traces(md, N, y, u0, kw)
+    compare(dev, ref, meta["cases"].get(case))

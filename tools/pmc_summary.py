@@ -22,7 +22,7 @@ def load(d, counter):
     return vals
 
 
-GRAM = re.compile(r"k_gram_[smw]<")     # every Gram-pass kernel (staged / marching / chunked)
+GRAM = re.compile(r"k_gram_[smwv]<")    # every Gram-pass kernel (staged / marching / chunked / VALU)
 
 
 def main(d, config=None):
@@ -30,7 +30,11 @@ def main(d, config=None):
     w = load(d, "WRITE_SIZE")
     out = {"correction": "FETCH_SIZE x2 (16-B/lane reads on gfx950), WRITE_SIZE x1; KiB -> bytes", "kernels": {}}
     for name in sorted(set(f) | set(w)):
-        fv, wv = f.get(name, []), w.get(name, [])
+        # launches on the bench grid only (the 256^2 pre-warm cycle moves < 100 MB per launch)
+        fa, wa = f.get(name, []), w.get(name, [])
+        keep = [i for i, v in enumerate(fa) if v > 50e6]
+        fv = [fa[i] for i in keep]
+        wv = [wa[i] for i in keep if i < len(wa)] if len(wa) == len(fa) else wa[-len(fv):] if fv else []
         if not fv:
             continue
         fm = sum(fv) / len(fv)
