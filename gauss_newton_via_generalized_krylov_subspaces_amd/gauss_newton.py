@@ -3,8 +3,9 @@
 Problems: the matrix-free Bratu problem of this package (``BratuGNOps``: slab vectors, fused
 stencils, multi-GPU) or any ``res`` / ``jac`` callables (``generic.HostCallableOps``: J uploaded as
 CSR per iteration, J v / J^T w / the Jacobi vector in ``gnk_csr_spmv``, flat vector kernels).
-Dense-ndarray Jacobians take the reference's ``lstsq`` branch there, which is out of scope (f4):
-the generic GN path raises NotImplementedError for them (GNK accepts dense Jacobians).
+Dense-ndarray Jacobians take the reference's ``scipy.linalg.lstsq`` branch (ref:gauss_newton.py:
+115-116): the least-squares step is a preconditioned CholeskyQR over the identity basis
+on the device (``generic.HostCallableOps.dense_lstsq``, at most 63 parameters).
 
 ``cg_least_squares`` restates scipy 1.15.3 ``scipy.sparse.linalg.cg``
 (iterative.py:305-422: x0 = 0, atol = rtol * ||b||, strict ``<`` test before
@@ -285,6 +286,11 @@ class GNSolver:
     def _residual(self, x, r):
         return self.ops.residual(x, r)
 
+    def _dvec(self):
+        if getattr(self, "_d", None) is None:
+            self._d = self.ops.vec()
+        return self._d
+
     def setup(self, x0):
         self.xi, self.ri = 0, 0
         self.xb[0].copy_(self.ops.load(x0))                          # x = x0.copy() (:95)
@@ -305,7 +311,10 @@ class GNSolver:
         x, r = self.xb[self.xi], self.rb[self.ri]
         ops.on_jacobian(x)                                           # J = jac(x) (:107)
         self.njev += 1                                               # :108
-        d, self.cg_iter = self.cg.solve(x, r, cg_rtol=self.cg_rtol, preconditioner=self.cg_pre)   # :111-114
+        if getattr(ops, "jacobian_is_dense", None) is not None and ops.jacobian_is_dense(x):
+            d = ops.dense_lstsq(x, r, self._dvec())                 # :115-116 (cg_iter keeps its value)
+        else:
+            d, self.cg_iter = self.cg.solve(x, r, cg_rtol=self.cg_rtol, preconditioner=self.cg_pre)  # :111-114
         jdd = ops.jvp_sumsq(x, d)                                    # sum((J d)^2) (ref:armijo_goldstein.py:50)
         xt, rt = self.xb[1 - self.xi], self.rb[1 - self.ri]
         last = {}
@@ -377,7 +386,7 @@ def gauss_newton(res, x0, jac, args: tuple = (), tol: float = 1e-8, max_iter=100
         from .generic import HostCallableOps
         problem, y = None, None
         x0h = x0.detach().cpu().numpy() if torch.is_tensor(x0) else np.asarray(x0, dtype=np.float64)
-        ops = HostCallableOps(res, jac, x0h.size, args, device=device, backend=_backend, dense_jacobian=False)
+        ops = HostCallableOps(res, jac, x0h.size, args, device=device, backend=_backend)
     solver = GNSolver(problem, y, tol=tol, max_iter=max_iter, cg_preconditioner=cg_preconditioner, cg_rtol=cg_rtol,
                       comm=comm, device=device, backend=_backend, callback=cb, callback_format=callback_format,
                       ops=ops)

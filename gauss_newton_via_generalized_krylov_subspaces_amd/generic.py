@@ -137,6 +137,22 @@ class FlatKrylovBasis:
         self.k = k + 1
 
 
+class _IdentityBasis:
+    """V = I_n as a basis (the dense least-squares solve: J V = J)."""
+
+    pending = False
+
+    def __init__(self, be, n):
+        self.V = be.to_device(np.eye(n))
+        self.k = n
+
+    def gram_k(self):
+        return self.k
+
+    def gram_left(self):
+        return None
+
+
 class HostCallableOps:
     """Problem side of the GNK loop (gauss_newton_krylow.GNKSolver) for user callables."""
 
@@ -153,6 +169,8 @@ class HostCallableOps:
         self.m = None                  # learnt from the first res / jac evaluation
         self.dense_jacobian = dense_jacobian
         self._J = {}                   # iterate buffer -> DeviceCSR of jac at its value
+        self._dense = {}               # iterate buffer -> jac returned a dense ndarray there
+        self._lsq = None               # dense least-squares solver of gauss_newton
         self._W = None
         self._st = self.be.zeros(2)
 
@@ -193,11 +211,7 @@ class HostCallableOps:
     def on_jacobian(self, u):
         """jac(u, *args) (the user's function) -> device CSR of J and J^T, kept for u's buffer."""
         Jh = self.jac(self.to_host(u), *self.args)
-        if not self.dense_jacobian and not scipy.sparse.issparse(Jh):
-            raise NotImplementedError(
-                "gauss_newton with a dense ndarray Jacobian takes the reference's scipy.linalg.lstsq branch "
-                "(ref:gauss_newton.py:115-116), which is out of scope (SURVEY §8 f4); pass a scipy.sparse "
-                "Jacobian for the CGLS branch")
+        self._dense[u.data_ptr()] = not scipy.sparse.issparse(Jh)
         J = DeviceCSR(self.be, Jh)
         if J.shape[1] != self.n:
             raise ValueError(f"jac returned shape {J.shape}, expected (m, {self.n})")
@@ -232,6 +246,24 @@ class HostCallableOps:
         self.be.flat_gram(self._W, k, rinv, r, self.m, G)
 
     # -- Gauss-Newton / CGLS (gauss_newton.GNSolver, DeviceCG) -----------------------------
+    def jacobian_is_dense(self, u) -> bool:
+        """jac(u) returned an ndarray: gauss_newton takes the lstsq branch (ref:gauss_newton.py:115-116)."""
+        return self._dense.get(u.data_ptr(), False)
+
+    def dense_lstsq(self, u, r, d):
+        """d = argmin ||-J(u) d - r|| (scipy.linalg.lstsq(-1 * jac_ev, res_ev), ref:gauss_newton.py:116)
+        on the device: preconditioned CholeskyQR over the identity basis (the Gram of [J T | r] by
+        gnk_flat_gram, T = the previous step's R^-1 when it still conditions J, else CholQR2)."""
+        if self.n > FLAT_GRAM_KMAX:
+            raise NotImplementedError(f"gauss_newton with a dense Jacobian: at most {FLAT_GRAM_KMAX} parameters "
+                                      "(the reference's lstsq branch is for small dense problems, SURVEY §8 f4)")
+        if self._lsq is None:
+            self._lsq = CholQR2Solver(self, self.n, gram=self.gram, n_global=self.n, device_solve=False)
+            self._lsq.quiet = True
+            self._eye = _IdentityBasis(self.be, self.n)
+        dh, _, _ = self._lsq.solve(u, self._eye, r)
+        d.copy_(self.be.to_device(dh))
+        return d
     def jvp_sumsq(self, u, d) -> float:
         """jdd = sum((J(u) d)^2) (ref:armijo_goldstein.py:50)."""
         if getattr(self, "_jd", None) is None:

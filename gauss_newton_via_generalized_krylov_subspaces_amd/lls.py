@@ -111,6 +111,7 @@ class CholQR2Solver:
         kp = self.be.gram_dim(kmax, True)
         self._G = self.be.zeros(kp * kp)
         self._rinv = self.be.zeros(kp * kp)
+        self.quiet = False          # True: no rank-deficiency messages (GN's lstsq branch prints none)
         self.passes = 0
         self.solves = 0
         self.fallbacks = 0
@@ -329,7 +330,8 @@ class CholQR2Solver:
         return d, jdd, R
 
     def _settle(self, R):
-        rank_messages(R)                                             # ref:gauss_newton_krylow.py:32-34
+        if not self.quiet:
+            rank_messages(R)                                         # ref:gauss_newton_krylow.py:32-34
         self.R_prev = self.R_last = R
         self._tentative = None
 

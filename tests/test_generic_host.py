@@ -6,6 +6,9 @@ the NumPy test double of the C-ABI and must reproduce the reference's golden Ros
 stdout, exceptions and bookkeeping exact, per-iteration ||x_k|| within 1e-10 (p = 2) / 1e-9
 (p = 1000, as the oracle's own pin).
 """
+import contextlib
+import io
+
 import numpy as np
 import pytest
 
@@ -42,10 +45,28 @@ def test_generic_gnk_rosenbrock(golden, p, x0name, version):
         np.testing.assert_allclose(out.x, arr[name + "__x"], rtol=1e-10, atol=1e-14)
 
 
-def test_generic_gn_rejects_dense_jacobian():
-    res, jac = O.rosenbrock(2)
-    with pytest.raises(NotImplementedError, match="lstsq"):
-        gnk.gauss_newton(res, np.array([2.0, 2.0]), lambda x: jac(x).toarray(), _backend=NumpyBackend())
+@pytest.mark.parametrize("p,x0", [(2, [2.0, 2.0]), (2, [-1.0, 1.0]), (10, None), (40, None)])
+def test_generic_gn_dense_jacobian_lstsq_branch(p, x0):
+    """gauss_newton with an ndarray Jacobian (ref:gauss_newton.py:115-116): the device
+    CholeskyQR solve vs scipy.linalg.lstsq in the oracle (the reference's own call) -- bookkeeping
+    and cg_iter (None) exact, ||x_k|| within 1e-10, no rank messages."""
+    res, jac = O.rosenbrock(p)
+    djac = lambda x: jac(x).toarray()  # noqa: E731
+    x0 = np.asarray(x0) if x0 is not None else np.random.default_rng(p).uniform(-1.5, 1.5, p)
+    ra, rb = [], []
+    out_a = io.StringIO()
+    with contextlib.redirect_stdout(out_a):
+        a = gnk.gauss_newton(res, x0, djac, _backend=NumpyBackend(),
+                             callback=lambda x, nfev, cg_iter: ra.append((np.linalg.norm(x), nfev, cg_iter)))
+    out_b = io.StringIO()
+    with contextlib.redirect_stdout(out_b):
+        b = O.gauss_newton(res, x0, djac,
+                           callback=lambda x, nfev, cg_iter: rb.append((np.linalg.norm(x), nfev, cg_iter)))
+    assert out_a.getvalue() == out_b.getvalue()
+    assert (a.nit, a.nrev, a.njev, a.success) == (b.nit, b.nrev, b.njev, b.success)
+    assert [r[1:] for r in ra] == [r[1:] for r in rb]
+    np.testing.assert_allclose([r[0] for r in ra], [r[0] for r in rb], rtol=1e-10)
+    np.testing.assert_allclose(a.x, b.x, rtol=1e-9, atol=1e-12)
 
 
 def test_generic_args_and_dense_jacobian():

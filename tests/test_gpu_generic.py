@@ -149,3 +149,25 @@ def test_gpu_generic_bratu_csr_matches_matrix_free():
         traj[kind] = (r.nit, r.nrev, r.njev, np.array(xs))
     assert traj["generic"][:3] == traj["bratu"][:3]
     np.testing.assert_allclose(traj["generic"][3], traj["bratu"][3], rtol=1e-10)
+
+
+@pytest.mark.parametrize("p,x0", [(2, [2.0, 2.0]), (2, [-1.0, 1.0]), (10, None), (40, None)])
+def test_gpu_gn_dense_jacobian_lstsq_branch(p, x0):
+    """gauss_newton's lstsq branch (ref:gauss_newton.py:115-116) on the GPU: device
+    CholeskyQR over gnk_flat_gram vs scipy.linalg.lstsq in the oracle -- bookkeeping exact, no
+    rank messages, ||x_k|| within 1e-10."""
+    import contextlib
+    import io
+    res, jac = O.rosenbrock(p)
+    djac = lambda x: jac(x).toarray()  # noqa: E731
+    x0 = np.asarray(x0) if x0 is not None else np.random.default_rng(p).uniform(-1.5, 1.5, p)
+    ra, rb = [], []
+    sa, sb = io.StringIO(), io.StringIO()
+    with contextlib.redirect_stdout(sa):
+        a = gnk.gauss_newton(res, x0, djac, callback=lambda x, nfev, cg_iter: ra.append((np.linalg.norm(x), nfev, cg_iter)))
+    with contextlib.redirect_stdout(sb):
+        b = O.gauss_newton(res, x0, djac, callback=lambda x, nfev, cg_iter: rb.append((np.linalg.norm(x), nfev, cg_iter)))
+    assert sa.getvalue() == sb.getvalue()
+    assert (a.nit, a.nrev, a.njev, a.success) == (b.nit, b.nrev, b.njev, b.success)
+    assert [r[1:] for r in ra] == [r[1:] for r in rb]
+    np.testing.assert_allclose([r[0] for r in ra], [r[0] for r in rb], rtol=1e-10)
