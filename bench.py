@@ -277,6 +277,9 @@ def main():
     j_ms = float(np.median([m for m, _ in jl]))
     j_gbs = jl[0][1] / (j_ms * 1e-3) / 1e9
 
+    spec_stats = dict(solver.spec_stats)
+    del solver, v, out, uu                      # free the GNK state (the basis) before the CG line
+    torch.cuda.empty_cache()
     cg_line = gn_cg_line(args, prob, u_true, u0, comm, device, world) if args.cg_iters > 0 else None
 
     config_key = f"bratu{N}_gnk_restart{args.restart}_{args.version}_ranks{world}"
@@ -308,7 +311,7 @@ def main():
                 "frac_of_peak": j_gbs / HBM_PEAK_GBS, "algorithmic_bytes": jl[0][1]},
         "step_algorithmic_GBs": total_bytes / elapsed / 1e9,
         "gram_passes_per_step": ppi,
-        "speculated_solves": dict(solver.spec_stats),
+        "speculated_solves": spec_stats,
     }
     if cg_line is not None:
         result["gn_cg"] = cg_line
