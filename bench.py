@@ -133,6 +133,7 @@ def gn_cg_line(args, prob, u_true, u0, comm, device, world):
     u = ops.load(u0)
     be = ops.be
     cg.solve(u, ops.y, cg_rtol=1e-8, preconditioner=True, maxiter=5)          # warm-up
+    cg.solve(u, ops.y, cg_rtol=1e-8, preconditioner=True, maxiter=5, variant="single_reduction")
     cap = args.cg_iters + 8
     be.timer_start(_native.TIMER_CG_MATVEC, cap)
     comm.barrier()
@@ -147,6 +148,19 @@ def gn_cg_line(args, prob, u_true, u0, comm, device, world):
         t = torch.tensor([elapsed], dtype=torch.float64, device=device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = t.item()
+    # the single-reduction recurrence (SURVEY f2 option): one host read per CG iteration instead of two
+    comm.barrier()
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    _, iters_sr = cg.solve(u, ops.y, cg_rtol=1e-8, preconditioner=True, maxiter=args.cg_iters,
+                           variant="single_reduction")
+    torch.cuda.synchronize()
+    comm.barrier()
+    el_sr = time.perf_counter() - t1
+    if world > 1:
+        t = torch.tensor([el_sr], dtype=torch.float64, device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el_sr = t.item()
     m_ms = float(np.mean([m for m, _ in ml])) if ml else float("nan")
     m_by = float(np.mean([b for _, b in ml])) if ml else float("nan")
     m_gbs = m_by / (m_ms * 1e-3) / 1e9 if ml else float("nan")
@@ -154,6 +168,10 @@ def gn_cg_line(args, prob, u_true, u0, comm, device, world):
             "value": iters / elapsed, "unit": "cg_iters/s", "ms_per_iter": 1e3 * elapsed / max(iters, 1),
             "algorithmic_GBs": CG_BYTES_PER_ITER * n * iters / elapsed / 1e9,
             "bytes_per_iter": CG_BYTES_PER_ITER * n,
+            "single_reduction": {"cg_iters": iters_sr, "value": iters_sr / el_sr, "unit": "cg_iters/s",
+                                 "ms_per_iter": 1e3 * el_sr / max(iters_sr, 1),
+                                 "note": "cg_variant='single_reduction' (Chronopoulos-Gear, non-parity option): "
+                                         "one host read per iteration, 120 n bytes"},
             "note": "timed: one CGLS solve capped at cg_iters (b = A^T y, Jacobi diag and the initial update "
                     "included); scipy's 10 n cap would need millions of iterations at rtol 1e-8",
             "matvec": {"kernel": "k_cg_matvec_m (p = z + beta p, lagged x += alpha p, q = J^T J p, 13-point, "

@@ -66,6 +66,8 @@ SIGNATURES = {
     "gnk_cg_step_matvec": (_c_int, [_c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_dbl, _c_int, _c_vp, _c_dbl,
                                     _c_vp]),
     "gnk_cg_update_p": (_c_int, [_c_vp, _c_dbl, _c_int, _c_vp, _c_vp]),
+    "gnk_cg_sr_update": (_c_int, [_c_vp, _c_dbl, _c_dbl, _c_int, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp,
+                                  _c_vp]),
     "gnk_lls_max_k": (_c_int, []),
     "gnk_lls_solve": (_c_int, [_c_vp, _c_vp, _c_int, _c_int, _c_vp, _c_int, _c_vp, _c_vp, _c_vp, _c_vp]),
     "gnk_lls_next": (_c_int, [_c_vp, _c_int, _c_int, _c_vp, _c_vp, _c_vp, _c_vp, _c_int, _c_vp, _c_vp, _c_vp, _c_vp,
@@ -281,6 +283,10 @@ class HipBackend:
 
     def vec_axpy(self, x, alpha, d, out, full_slab):
         self._call("gnk_vec_axpy", _p(x), float(alpha), _p(d), _p(out), int(bool(full_slab)))
+
+    def cg_sr_update(self, alpha, beta, first, w, p, s, x, r, dinv, u, out):
+        self._call("gnk_cg_sr_update", float(alpha), float(beta), int(bool(first)), _p(w), _p(p), _p(s), _p(x), _p(r),
+                   _p(dinv), _p(u), _p(out))
 
     def lls_max_k(self):
         return int(self.lib.gnk_lls_max_k())

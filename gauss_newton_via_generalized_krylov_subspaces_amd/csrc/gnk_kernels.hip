@@ -900,6 +900,37 @@ __global__ __launch_bounds__(BLOCK) void k_cg_xr(double alpha, const double* __r
   block_sum_store<2>(acc, 2, partial + 2 * (blockIdx.y * gridDim.x + blockIdx.x), sh);
 }
 
+// Single-reduction CG iteration (Chronopoulos-Gear; the build's non-parity option) on
+// owned rows: p = u + beta p, s = w + beta s (first: p = u, s = w); x += alpha p; r -= alpha s;
+// u = M r (dinv NULL: u = r); partials {r . u, r . r}.  With w = A^T A u from the normal matvec and
+// its u . w, one host read per iteration carries all three scalars.
+template <int VEC>
+__global__ __launch_bounds__(BLOCK) void k_cg_sr(double alpha, double beta, int first, const double* __restrict__ w,
+                                                 double* __restrict__ p, double* __restrict__ sv,
+                                                 double* __restrict__ x, double* __restrict__ r,
+                                                 const double* __restrict__ dinv, double* __restrict__ u, Geo geo,
+                                                 int64_t lr0, int64_t nlr, double* __restrict__ partial) {
+  __shared__ double sh[(BLOCK / 64) * 2];
+  double acc[2] = {0.0, 0.0};
+  ROW_LOOP_BEGIN(VEC)
+  for (int qq = 0; qq < VEC && iy + qq < N; ++qq) {
+    const int64_t i = li + qq;
+    const double pi = first ? u[i] : u[i] + beta * p[i];
+    const double si = first ? w[i] : w[i] + beta * sv[i];
+    p[i] = pi;
+    sv[i] = si;
+    x[i] = x[i] + alpha * pi;
+    const double ri = r[i] - alpha * si;
+    r[i] = ri;
+    const double ui = dinv ? 0.0 + dinv[i] * ri : ri;
+    u[i] = ui;
+    acc[0] += ri * ui;
+    acc[1] += ri * ri;
+  }
+  ROW_LOOP_END
+  block_sum_store<2>(acc, 2, partial + 2 * (blockIdx.y * gridDim.x + blockIdx.x), sh);
+}
+
 template <int VEC>
 __global__ __launch_bounds__(BLOCK) void k_cg_p(double beta, int first, const double* __restrict__ z,
                                                 double* __restrict__ p, Geo geo, int64_t lr0, int64_t nlr) {
@@ -3246,6 +3277,18 @@ int gnk_cg_update_xr(gnk_ctx* ctx, double alpha, const double* p, const double* 
   return reduce(ctx, ctx->scratch, nblk, 2, 2, nullptr, out);
 }
 
+int gnk_cg_sr_update(gnk_ctx* ctx, double alpha, double beta, int first, const double* w, double* p, double* s,
+                     double* x, double* r, const double* dinv, double* u, double* out) {
+  if (!ready(ctx)) return -1;
+  if (!w || !p || !s || !x || !r || !u || !out) return fail(ctx, "cg_sr_update: NULL argument");
+  RowLaunch L = rows(ctx, G, ctx->geo.nrows, vec_of(ctx));
+  const int nblk = L.grid.x * L.grid.y;
+  DISPATCH_VEC(ctx, k_cg_sr, L, 0, alpha, beta, first, w, p, s, x, r, dinv, u, ctx->geo, L.lr0, L.nlr, ctx->scratch);
+  int rc = check_launch(ctx, "cg_sr_update");
+  if (rc) return rc;
+  return reduce(ctx, ctx->scratch, nblk, 2, 2, nullptr, out);
+}
+
 int gnk_cg_update_p(gnk_ctx* ctx, double beta, int first, const double* z, double* p) {
   if (!ready(ctx)) return -1;
   RowLaunch L = rows(ctx, G, ctx->geo.nrows, vec_of(ctx), 1 << 30);
@@ -3283,7 +3326,6 @@ int gnk_timer_collect(gnk_ctx* ctx, double* ms_out, double* bytes_out, int capac
   return n;
 }
 
-// tooling: fp64 MFMA issue-rate probe (not part of the solver)
 int gnk_lls_max_k(void) { return LS_KMAX; }
 
 int gnk_lls_next(gnk_ctx* ctx, int k, int pending, const double* out, const double* e_try, const double* pack,
@@ -3309,6 +3351,7 @@ int gnk_lls_solve(gnk_ctx* ctx, const double* Gm, int kp, int k, const double* P
   return check_launch(ctx, "lls_solve");
 }
 
+// tooling: fp64 MFMA issue-rate probe (not part of the solver)
 int gnk_probe_mfma_f64(gnk_ctx* ctx, double* out, int blocks, int iters) {
   if (!ctx) return -1;
   hipLaunchKernelGGL(k_probe_mfma, dim3(blocks), dim3(BLOCK), 0, ctx->stream, out, iters);

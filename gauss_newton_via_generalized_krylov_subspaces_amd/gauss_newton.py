@@ -58,6 +58,9 @@ class BratuGNOps:
 
     rvec = vec
 
+    def scalar3(self):
+        return self.dev.scalar(3)
+
     def load(self, x0):
         return self.dev.load(x0)
 
@@ -138,6 +141,19 @@ class BratuGNOps:
     def cg_axpy(self, x, alpha, p):
         self.be.vec_axpy(x, alpha, p, x, False)                     # x + alpha p (owned rows)
 
+    # single-reduction iteration (cg_variant="single_reduction"): the three scalars of one
+    # iteration are partial sums in one device buffer, read with one collective
+    def cg_sr_update(self, alpha, beta, first, w, p, s, x, r, dinv, u, out):
+        self.be.cg_sr_update(alpha, beta, first, w, p, s, x, r, dinv, u, out)
+
+    def cg_sr_matvec(self, u, w, out):
+        sl = self.dev.slab
+        self.comm.halo(u, sl.N, sl.nrows)
+        self.be.cg_matvec(self.dvec, u, w, out)
+
+    def cg_sr_read(self, buf):
+        return self.comm.sum(buf)
+
 
 class DeviceCG:
     """Device state of the CGLS solve (one rank of a Bratu slab, or a generic problem)."""
@@ -152,9 +168,15 @@ class DeviceCG:
         self.dinv = v()
         self.total_iters = 0
 
-    def solve(self, u, y, cg_rtol=1e-4, preconditioner=True, callback=None, maxiter=None):
+    def solve(self, u, y, cg_rtol=1e-4, preconditioner=True, callback=None, maxiter=None, variant="scipy"):
         """x = argmin ||y - A x||, A = -J(u); returns (x, cg_iter) like ref:gauss_newton.py:11-60.
-        ``maxiter`` (tooling, bench.py) caps each CG run below scipy's 10 n."""
+        ``maxiter`` (tooling, bench.py) caps each CG run below scipy's 10 n.  ``variant``:
+        "scipy" (the reference's recurrence, parity) or "single_reduction" (Chronopoulos-Gear: the
+        same Krylov iterates in exact arithmetic, one reduction per iteration instead of two; not
+        bit-compatible with scipy, so iteration counts may differ by rounding)."""
+        if variant not in ("scipy", "single_reduction"):
+            raise ValueError("cg_variant must be 'scipy' or 'single_reduction'")
+        self._variant = variant
         ops = self.ops
         ops.cg_rhs(u, y, self.b)                                    # b = A.T @ y
         ops.cg_prepare(u)
@@ -175,6 +197,8 @@ class DeviceCG:
 
     def _cg(self, rtol, dinv, cb, maxiter=None):
         """scipy iterative.py:305-422 with x0 = 0, atol = 0."""
+        if getattr(self, "_variant", "scipy") == "single_reduction":
+            return self._cg_single_reduction(rtol, dinv, cb, maxiter)
         if self.p2 is not None:
             return self._cg_fused(rtol, dinv, cb, maxiter)
         ops = self.ops
@@ -248,6 +272,47 @@ class DeviceCG:
             ops.cg_axpy(self.x, alpha_prev, p_in)                       # the last x += alpha p
         return done
 
+    def _cg_single_reduction(self, rtol, dinv, cb, maxiter):
+        """Chronopoulos-Gear PCG (non-parity option): with u = M r, w = A u,
+        gamma = r . u, delta = u . w the step and direction coefficients follow from one reduction:
+            beta = gamma / gamma_prev,  alpha = gamma / (delta - beta gamma / alpha_prev)
+            p = u + beta p,  s = w + beta s (= A p),  x += alpha p,  r -= alpha s,  u = M r
+        Stopping and counting as scipy: the loop ends when ||r|| < rtol ||b|| (tested on the residual
+        of the last update), each update is one iteration; x0 = 0."""
+        ops = self.ops
+        if getattr(self, "_sr", None) is None:
+            v = ops.vec
+            self._sr = (v(), v(), v(), ops.scalar3())          # u, w, s, [r.u, r.r, u.w]
+        u, w, sv, buf = self._sr
+        bnrm2 = math.sqrt(ops.sumsq(self.b))
+        atol = max(0.0, float(rtol) * float(bnrm2))
+        self.x.zero_()
+        if bnrm2 == 0:
+            self.x.copy_(self.b)
+            return 0
+        maxiter = ops.n_global * 10 if maxiter is None else min(int(maxiter), ops.n_global * 10)
+        self.r.copy_(self.b)
+        if math.sqrt(ops.sumsq(self.r)) < atol:
+            return 0
+        # u0 = M r0 (alpha = 0 update: x, r unchanged, p = u, s = w are overwritten below)
+        w.zero_()
+        ops.cg_sr_update(0.0, 0.0, True, w, self.p, sv, self.x, self.r, dinv, u, buf[0:2])
+        ops.cg_sr_matvec(u, w, buf[2:3])
+        gamma, rr, delta = ops.cg_sr_read(buf)
+        alpha, beta, first = gamma / delta, 0.0, True
+        for iteration in range(maxiter):
+            ops.cg_sr_update(alpha, beta, first, w, self.p, sv, self.x, self.r, dinv, u, buf[0:2])
+            ops.cg_sr_matvec(u, w, buf[2:3])
+            gamma_new, rr, delta = ops.cg_sr_read(buf)
+            cb()
+            if math.sqrt(rr) < atol:
+                return iteration + 1
+            beta = gamma_new / gamma
+            alpha_prev = alpha
+            alpha = gamma_new / (delta - beta * gamma_new / alpha_prev)
+            gamma, first = gamma_new, False
+        return maxiter
+
 
 def cg_least_squares(A, y, x0=None, cg_rtol=1e-4, preconditioner=True):
     """Drop-in for ref:gauss_newton.py:11-60 with A = -jac(u) (a matrix-free BratuJacobian
@@ -270,13 +335,14 @@ class GNSolver:
 
     def __init__(self, problem, y, tol=1e-8, max_iter=100, cg_preconditioner=False, cg_rtol=1e-4,
                  comm: Optional[Comm] = None, device=None, backend=None, callback: Callable = None,
-                 callback_format="numpy", ops=None):
+                 callback_format="numpy", ops=None, cg_variant="scipy"):
         self.ops = ops if ops is not None else BratuGNOps(problem, y, comm, device, backend)
         self.dev = getattr(self.ops, "dev", None)
         self.be = self.ops.be
         self.comm = self.ops.comm
         self.tol, self.max_iter = tol, int(max_iter)
         self.cg_pre, self.cg_rtol = cg_preconditioner, cg_rtol
+        self.cg_variant = cg_variant
         self.callback, self.callback_format = callback, callback_format
         self.cg = DeviceCG(self.ops)
         self.xb = [self.ops.vec(), self.ops.vec()]
@@ -314,7 +380,8 @@ class GNSolver:
         if getattr(ops, "jacobian_is_dense", None) is not None and ops.jacobian_is_dense(x):
             d = ops.dense_lstsq(x, r, self._dvec())                 # :115-116 (cg_iter keeps its value)
         else:
-            d, self.cg_iter = self.cg.solve(x, r, cg_rtol=self.cg_rtol, preconditioner=self.cg_pre)  # :111-114
+            d, self.cg_iter = self.cg.solve(x, r, cg_rtol=self.cg_rtol, preconditioner=self.cg_pre,  # :111-114
+                                            variant=self.cg_variant)
         jdd = ops.jvp_sumsq(x, d)                                    # sum((J d)^2) (ref:armijo_goldstein.py:50)
         xt, rt = self.xb[1 - self.xi], self.rb[1 - self.ri]
         last = {}
@@ -370,9 +437,11 @@ def d_norm_host(solver, d):
 
 def gauss_newton(res, x0, jac, args: tuple = (), tol: float = 1e-8, max_iter=100, step_length_control=None,
                  callback: Callable = _noop, cg_preconditioner: bool = False, *, cg_rtol: float = 1e-4,
+                 cg_variant: str = "scipy",
                  comm: Optional[Comm] = None, device=None, callback_format: str = "numpy",
                  result_format: str = "numpy", _backend=None) -> RegressionResult:
-    """Drop-in for ref:gauss_newton.py:63-138 (sparse-Jacobian / CGLS branch); ``cg_rtol`` added."""
+    """Drop-in for ref:gauss_newton.py:63-138; ``cg_rtol`` added, and ``cg_variant="single_reduction"``
+    (Bratu path) selects the one-reduction CG recurrence (not bit-compatible with scipy)."""
     bratu = resolve_bratu(res, jac)
     if step_length_control is not None:
         raise NotImplementedError("the device solver uses the reference's armijo_goldstein rule")
@@ -387,9 +456,11 @@ def gauss_newton(res, x0, jac, args: tuple = (), tol: float = 1e-8, max_iter=100
         problem, y = None, None
         x0h = x0.detach().cpu().numpy() if torch.is_tensor(x0) else np.asarray(x0, dtype=np.float64)
         ops = HostCallableOps(res, jac, x0h.size, args, device=device, backend=_backend)
+    if cg_variant != "scipy" and ops is not None:
+        raise NotImplementedError("cg_variant='single_reduction' is implemented for the matrix-free Bratu path")
     solver = GNSolver(problem, y, tol=tol, max_iter=max_iter, cg_preconditioner=cg_preconditioner, cg_rtol=cg_rtol,
                       comm=comm, device=device, backend=_backend, callback=cb, callback_format=callback_format,
-                      ops=ops)
+                      ops=ops, cg_variant=cg_variant)
     solver.setup(x0 if not torch.is_tensor(x0) else x0.detach().cpu().numpy())
     while not solver.step():
         pass

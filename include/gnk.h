@@ -180,6 +180,14 @@ int gnk_cg_update_xr(gnk_ctx* ctx, double alpha, const double* p, const double* 
                      double* x, double* r, const double* dinv, double* z, double* out);
 /* p = z (first) or p = beta * p + z (owned rows) */
 int gnk_cg_update_p(gnk_ctx* ctx, double beta, int first, const double* z, double* p);
+/* Single-reduction CG (Chronopoulos-Gear) iteration update, the non-parity option of gauss_newton
+ * (cg_variant="single_reduction"), owned rows: p = u + beta p, s = w + beta s (first != 0:
+ * p = u, s = w); x += alpha p; r -= alpha s; u = dinv * r (dinv NULL: u = r);
+ * out[0] = r . u, out[1] = r . r.  w = A^T A u comes from gnk_cg_normal_matvec (its u . w).
+ *                                   restates scipy iterative.py:401-415 with one reduction */
+int gnk_cg_sr_update(gnk_ctx* ctx, double alpha, double beta, int first, const double* w, double* p, double* s,
+                     double* x, double* r, const double* dinv, double* u, double* out);
+
 
 /* ---- generic problems: flat length-n vectors, no gnk_set_bratu needed ------ */
 /* x = V[:, :k] @ c                                                    ref:krylow.py:41-42 */

@@ -385,6 +385,17 @@ class NumpyBackend:
         out[0] = float(np.dot(rv[own], rv[own]))
         out[1] = float(np.dot(rv[own], zz))
 
+    def cg_sr_update(self, alpha, beta, first, w, p, s, x, r, dinv, u, out):
+        own = slice(GHOST * self.N, (GHOST + self.nrows) * self.N)
+        P, S, X, R, U, W = p.numpy(), s.numpy(), x.numpy(), r.numpy(), u.numpy(), w.numpy()
+        P[own] = U[own] if first else U[own] + beta * P[own]
+        S[own] = W[own] if first else W[own] + beta * S[own]
+        X[own] = X[own] + alpha * P[own]
+        R[own] = R[own] - alpha * S[own]
+        U[own] = 0.0 + dinv.numpy()[own] * R[own] if dinv is not None else R[own]
+        out[0] = float(np.dot(R[own], U[own]))
+        out[1] = float(np.dot(R[own], R[own]))
+
     def cg_update_p(self, beta, first, z, p):
         own = slice(GHOST * self.N, (GHOST + self.nrows) * self.N)
         if first:

@@ -85,7 +85,7 @@ def _run(world, method, kw):
 @pytest.mark.parametrize("world", [2, 3])
 @pytest.mark.parametrize("method,kw", [("gnk", {"version": "res_old", "max_iter": 30}),
                                        ("gnk", {"version": "res_new", "max_iter": 45, "krylow_restart": 20}),
-                                       ("gn", {})])
+                                       ("gn", {}), ("gn", {"cg_variant": "single_reduction"})])
 def test_multi_rank_matches_golden(golden, world, method, kw):
     meta, arr = golden
     outs = _run(world, method, kw)

@@ -144,6 +144,27 @@ def test_gn_bratu100(golden):
     np.testing.assert_allclose(rec["xnorm"], ref["xnorm"], rtol=1e-6)
 
 
+@pytest.mark.parametrize("N,name", [(24, "bratu24_gn"), (100, "bratu100_gn")])
+def test_gn_single_reduction_cg_gpu(golden, N, name):
+    """cg_variant="single_reduction" (Chronopoulos-Gear: one reduction per CG iteration)
+    on the GPU against the golden GN runs: outer bookkeeping exact, cg_iter within 1 (a different
+    recurrence, so a long solve may stop one iteration apart), iterates within 1e-6."""
+    meta, arr = golden
+    if N == 24:
+        u0, y = arr["bratu24_u0"], arr["bratu24_y"]
+    else:
+        u0, y = arr["bratu100_u0"], O.BratuPdeProblem(101, 5, 10).pde_operator(O.BratuPdeProblem(101, 5, 10).u_true)
+    out, rec, so, exc = run(gnk.gauss_newton, dict(grid_nodes=N + 1, ALPHA=5, LAMBDA=10), u0, y,
+                            cg_variant="single_reduction")
+    case = meta["cases"][name]
+    assert so == case["stdout"] and exc is None
+    assert (out.nit, out.nrev, out.njev, out.success) == (case["nit"], case["nrev"], case["njev"], case["success"])
+    ref = case["per_iter"]
+    assert rec["nfev"] == ref["nfev"]
+    assert all(abs(a - b) <= 1 for a, b in zip(rec["cg_iter"], ref["cg_iter"]))
+    np.testing.assert_allclose(rec["xnorm"], ref["xnorm"], rtol=1e-6)
+
+
 @pytest.mark.parametrize("N", [24, 100])
 @pytest.mark.parametrize("pre,rtol", [(False, 1e-4), (True, 1e-4), (True, 1e-8)])
 def test_cg_least_squares(golden, N, pre, rtol):

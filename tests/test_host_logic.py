@@ -104,3 +104,14 @@ def test_row_partition_covers_grid():
             assert sum(n for _, n in parts) == N
             for (a0, an), (b0, _) in zip(parts, parts[1:]):
                 assert a0 + an == b0
+
+
+@pytest.mark.parametrize("name,kw", [("bratu24_gn", {}), ("bratu24_gn_precond", {"cg_preconditioner": True})])
+def test_gn_single_reduction_cg(golden, name, kw):
+    """cg_variant="single_reduction" (Chronopoulos-Gear): not bit-compatible with scipy's
+    recurrence, but on the golden GN runs the CG counts and the outer bookkeeping are unchanged and
+    the iterates agree to 1e-9."""
+    meta, arr = golden
+    out, rec, so, exc = run(gnk.gauss_newton, dict(grid_nodes=25, ALPHA=5, LAMBDA=10), arr["bratu24_u0"],
+                            arr["bratu24_y"], cg_variant="single_reduction", **kw)
+    check(meta["cases"][name], out, rec, so, exc, rtol=1e-9)
