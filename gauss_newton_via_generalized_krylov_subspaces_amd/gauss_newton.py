@@ -147,9 +147,16 @@ class BratuGNOps:
         self.be.cg_sr_update(alpha, beta, first, w, p, s, x, r, dinv, u, out)
 
     def cg_sr_matvec(self, u, w, out):
+        """w = A^T A u and u . w: the row-marching kernel (first-iteration form, p_out = u) when N is
+        even, else the point-wise one."""
         sl = self.dev.slab
         self.comm.halo(u, sl.N, sl.nrows)
-        self.be.cg_matvec(self.dvec, u, w, out)
+        if self.cg_fused:
+            if getattr(self, "_sr_p", None) is None:
+                self._sr_p = self.dev.vec()
+            self.be.cg_step_matvec(self.dvec, u, u, self._sr_p, w, 0.0, True, None, 0.0, out)
+        else:
+            self.be.cg_matvec(self.dvec, u, w, out)
 
     def cg_sr_read(self, buf):
         return self.comm.sum(buf)
