@@ -30,6 +30,8 @@ class BratuDevice:
                                problem.ALPHA, problem.LAMBDA)
         if self.backend.slab_len() != self.slab.length:
             raise RuntimeError("slab length mismatch between host and libgnk")
+        if self.comm.world > 1 and not self.comm.stage and hasattr(self.backend, "rank_sum"):
+            self.comm.device_rank_sum = self.backend.rank_sum
 
     def vec(self):
         return self.backend.zeros(self.slab.length)

@@ -68,6 +68,7 @@ SIGNATURES = {
     "gnk_cg_update_p": (_c_int, [_c_vp, _c_dbl, _c_int, _c_vp, _c_vp]),
     "gnk_cg_sr_update": (_c_int, [_c_vp, _c_dbl, _c_dbl, _c_int, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp,
                                   _c_vp]),
+    "gnk_rank_sum": (_c_int, [_c_vp, _c_vp, _c_int, _c_i64, _c_vp]),
     "gnk_lls_max_k": (_c_int, []),
     "gnk_lls_solve": (_c_int, [_c_vp, _c_vp, _c_int, _c_int, _c_vp, _c_int, _c_vp, _c_vp, _c_vp, _c_vp]),
     "gnk_lls_next": (_c_int, [_c_vp, _c_int, _c_int, _c_vp, _c_vp, _c_vp, _c_vp, _c_int, _c_vp, _c_vp, _c_vp, _c_vp,
@@ -287,6 +288,12 @@ class HipBackend:
     def cg_sr_update(self, alpha, beta, first, w, p, s, x, r, dinv, u, out):
         self._call("gnk_cg_sr_update", float(alpha), float(beta), int(bool(first)), _p(w), _p(p), _p(s), _p(x), _p(r),
                    _p(dinv), _p(u), _p(out))
+
+    def rank_sum(self, parts, world, out):
+        """out = rank-ordered sum of parts (world x n, contiguous) on the device, one launch."""
+        n = out.numel()
+        self._call("gnk_rank_sum", _p(parts), int(world), int(n), _p(out))
+        return out
 
     def lls_max_k(self):
         return int(self.lib.gnk_lls_max_k())

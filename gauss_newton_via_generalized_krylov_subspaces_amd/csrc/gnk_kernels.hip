@@ -943,6 +943,17 @@ __global__ __launch_bounds__(BLOCK) void k_cg_p(double beta, int first, const do
 }
 
 // ---------------------------------------------------------------- deterministic partial reduction
+// rank-ordered sum of all-gathered per-rank partials: out[j] = ((p_0[j] + p_1[j]) + p_2[j]) + ...,
+// the host's order (slab.Comm), in one launch instead of world - 1 elementwise adds
+__global__ __launch_bounds__(BLOCK) void k_rank_sum(const double* __restrict__ parts, int world, int64_t n,
+                                                    double* __restrict__ out) {
+  for (int64_t j = int64_t(blockIdx.x) * BLOCK + threadIdx.x; j < n; j += int64_t(gridDim.x) * BLOCK) {
+    double s = parts[j];
+    for (int p = 1; p < world; ++p) s = s + parts[int64_t(p) * n + j];
+    out[j] = s;
+  }
+}
+
 // Wave-per-output deterministic reduction over a fixed partition of the partials.
 // Output j reads partial[base(j) + b * sb] for b in [split * span, min(nblk, (split+1) * span)),
 // base(j) = (j / cw) * cs + (j % cw).  Lane l folds b = l, l + 64, ... with 8 independent
@@ -3324,6 +3335,16 @@ int gnk_timer_collect(gnk_ctx* ctx, double* ms_out, double* bytes_out, int capac
   ctx->timer_kernel = 0;
   ctx->timer_count = 0;
   return n;
+}
+
+int gnk_rank_sum(gnk_ctx* ctx, const double* parts, int world, int64_t n, double* out) {
+  if (!ctx) return -1;
+  if (world < 1 || n < 0) return fail(ctx, "rank_sum: world < 1 or n < 0");
+  if (n == 0) return 0;
+  if (!parts || !out) return fail(ctx, "rank_sum: NULL argument");
+  const int64_t nb = std::min<int64_t>((n + BLOCK - 1) / BLOCK, 1024);
+  hipLaunchKernelGGL(k_rank_sum, dim3(unsigned(nb)), dim3(BLOCK), 0, ctx->stream, parts, world, n, out);
+  return check_launch(ctx, "rank_sum");
 }
 
 int gnk_lls_max_k(void) { return LS_KMAX; }

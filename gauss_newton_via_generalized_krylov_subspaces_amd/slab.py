@@ -52,6 +52,19 @@ class Comm:
             self.group = None
             self.rank, self.world = 0, 1
             self.stage = False
+        # device-side rank-ordered sum of all-gathered partials (one kernel, set by the device
+        # backend: HipBackend.rank_sum); None: elementwise torch adds in the same order
+        self.device_rank_sum = None
+
+    def _sum_parts_device(self, gath: torch.Tensor, n: int) -> torch.Tensor:
+        if self.device_rank_sum is not None:
+            out = torch.empty(n, dtype=gath.dtype, device=gath.device)
+            return self.device_rank_sum(gath, self.world, out)
+        parts = gath.view(self.world, -1)
+        s = parts[0].clone()
+        for p in range(1, self.world):
+            s.add_(parts[p])
+        return s
 
     # -- reductions -------------------------------------------------------------
     def _gather(self, t: torch.Tensor) -> np.ndarray:
@@ -145,11 +158,7 @@ class Comm:
             return h.gath
         if h.gath.numel() == h.n:                 # staged / CPU path: sum on the host, copy back
             return torch.from_numpy(self._rank_sum(h.parts)).to(h.gath.device)
-        parts = h.gath.view(self.world, -1)
-        s = parts[0].clone()
-        for p in range(1, self.world):
-            s.add_(parts[p])
-        return s
+        return self._sum_parts_device(h.gath, h.n)
 
     @staticmethod
     def _rank_sum(parts):
@@ -187,11 +196,7 @@ class Comm:
         t = t.contiguous().reshape(-1)
         buf = torch.empty(self.world * t.numel(), dtype=t.dtype, device=t.device)
         dist.all_gather_into_tensor(buf, t, group=self.group)
-        parts = buf.view(self.world, -1)
-        s = parts[0].clone()
-        for p in range(1, self.world):
-            s.add_(parts[p])
-        return s
+        return self._sum_parts_device(buf, t.numel())
 
     def barrier(self):
         if self.world > 1:

@@ -111,6 +111,9 @@ int gnk_basis_gemv_vjp_gemv_t_pending(gnk_ctx* ctx, const double* V, int64_t ldv
  * d = -R^-1 z, jdd = ||R d||^2, e_try = e + sdd * d (elementwise).  P: k x k upper triangular.
  * out = [status (0 ok, 1 not SPD), jdd, s, d (k), R (k*k), Ry (k*k), R^-1 (k*k)].
  * 1 <= k <= gnk_lls_max_k().           ref:gauss_newton_krylow.py:16-36, armijo_goldstein.py:50 */
+/* out[j] = sum over p in rank order of parts[p * n + j] (left to right, as the host sums all-gathered
+ * partials; slab.Comm): the rank-ordered reduction of a small per-rank vector after all_gather. */
+int gnk_rank_sum(gnk_ctx* ctx, const double* parts, int world, int64_t n, double* out);
 int gnk_lls_max_k(void);
 int gnk_lls_solve(gnk_ctx* ctx, const double* G, int kp, int k, const double* P, int rescale, const double* sdd,
                   const double* e, double* out, double* e_try);

@@ -522,3 +522,17 @@ def test_lls_next_device(k, pending):
     nb.lls_next(k, pending, out.cpu(), etry.cpu(), torch.from_numpy(pack), torch.from_numpy(sc), kpn, *hv)
     for d_, h_ in zip(dv, hv):
         np.testing.assert_allclose(d_.cpu().numpy(), h_.numpy(), rtol=1e-15, atol=0)
+
+
+@pytest.mark.parametrize("world,n", [(1, 5), (2, 1), (3, 441), (8, 3000)])
+def test_rank_sum_matches_host_order(world, n):
+    """gnk_rank_sum == the host's left-to-right sum over ranks (slab.Comm), bit for bit."""
+    prob, dev, ref = make(24)
+    be = dev.backend
+    parts = np.random.default_rng(world * n).standard_normal((world, n)) * 10.0 ** np.arange(world)[:, None]
+    out = be.zeros(n)
+    be.rank_sum(be.to_device(parts.reshape(-1)), world, out)
+    s = parts[0].copy()
+    for p in range(1, world):
+        s = s + parts[p]
+    np.testing.assert_array_equal(out.cpu().numpy(), s)
