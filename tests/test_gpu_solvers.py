@@ -216,3 +216,24 @@ def test_gnk_deterministic_and_restart_large():
     # is below what any re-ordering of the arithmetic can hold here; 5e-9 is.
     np.testing.assert_allclose(np.linalg.norm(outs[0].x), np.linalg.norm(ref.x), rtol=5e-9)
     np.testing.assert_allclose(outs[0].x, ref.x, rtol=0, atol=1e-7 * np.abs(ref.x).max())
+
+
+@pytest.mark.parametrize("restart,version", [(3, "res_old"), (7, "res_old"), (5, "res_new")])
+def test_gnk_short_restart_cycles_vs_oracle(restart, version):
+    """Short restart cycles at N = 256 exercise the speculative next-step solve across
+    many restarts and loop ends: bookkeeping equal to the oracle, ||x|| within 5e-9 (the post-restart
+    least-squares steps are cancellation-limited, see test_gnk_deterministic_and_restart_large)."""
+    N = 256
+    prob_o, y, u0 = O.bratu_workload(N)
+    prob = gnk.BratuPdeProblem(N + 1, 5, 10)
+    rec_d, rec_o = [], []
+    with contextlib.redirect_stdout(io.StringIO()):
+        out = gnk.gauss_newton_krylow(prob.make_res(y), u0, prob.make_jac(), krylow_restart=restart, max_iter=40,
+                                      version=version,
+                                      callback=lambda x, nfev, cg_iter: rec_d.append((np.linalg.norm(x), nfev)))
+        ref = O.gauss_newton_krylow(prob_o.make_res(y), u0, prob_o.make_jac(), krylow_restart=restart, max_iter=40,
+                                    version=version,
+                                    callback=lambda x, nfev, cg_iter: rec_o.append((np.linalg.norm(x), nfev)))
+    assert (out.nit, out.nrev, out.njev, out.success) == (ref.nit, ref.nrev, ref.njev, ref.success)
+    assert [n for _, n in rec_d] == [n for _, n in rec_o]
+    np.testing.assert_allclose([a for a, _ in rec_d], [a for a, _ in rec_o], rtol=5e-9)

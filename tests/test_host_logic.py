@@ -115,3 +115,24 @@ def test_gn_single_reduction_cg(golden, name, kw):
     out, rec, so, exc = run(gnk.gauss_newton, dict(grid_nodes=25, ALPHA=5, LAMBDA=10), arr["bratu24_u0"],
                             arr["bratu24_y"], cg_variant="single_reduction", **kw)
     check(meta["cases"][name], out, rec, so, exc, rtol=1e-9)
+
+
+@pytest.mark.parametrize("restart,version", [(3, "res_old"), (5, "res_new")])
+def test_gnk_short_restart_cycles_vs_oracle(restart, version):
+    """N = 256, short restart cycles: the speculative next-step solve across many restarts (DESIGN.md
+    §5b) keeps the oracle's bookkeeping; ||x_k|| within 5e-9 (post-restart LS steps are
+    cancellation-limited)."""
+    N = 256
+    prob_o, y, u0 = O.bratu_workload(N)
+    prob = gnk.BratuPdeProblem(N + 1, 5, 10)
+    rd, ro = [], []
+    with contextlib.redirect_stdout(io.StringIO()):
+        out = gnk.gauss_newton_krylow(prob.make_res(y), u0, prob.make_jac(), krylow_restart=restart, max_iter=40,
+                                      version=version, _backend=NumpyBackend(),
+                                      callback=lambda x, nfev, cg_iter: rd.append((np.linalg.norm(x), nfev)))
+        ref = O.gauss_newton_krylow(prob_o.make_res(y), u0, prob_o.make_jac(), krylow_restart=restart, max_iter=40,
+                                    version=version,
+                                    callback=lambda x, nfev, cg_iter: ro.append((np.linalg.norm(x), nfev)))
+    assert (out.nit, out.nrev, out.njev, out.success) == (ref.nit, ref.nrev, ref.njev, ref.success)
+    assert [n for _, n in rd] == [n for _, n in ro]
+    np.testing.assert_allclose([a for a, _ in rd], [a for a, _ in ro], rtol=5e-9)
