@@ -278,14 +278,14 @@ def main():
     g_avg_bytes = float(np.mean(g_by)) if g_by else float("nan")
     g_gbs = g_avg_bytes / (g_avg_ms * 1e-3) / 1e9 if g_ms else float("nan")
     gram_share = sum(g_ms) * 1e-3 / elapsed if g_ms else float("nan")
-    # per basis size: columns = bytes / (8 n_rank) - 2 (V, u, r); kernel = VALU for k <= 8, staged above
+    # per basis size: columns = bytes / (8 n_rank) - 2 (V, u, r); kernel = VALU for k <= 9, staged above
     n_rank = solver.dev.slab.nrows * N
     by_k = {}
     for m, b in launches:
         kk = int(round(b / (8.0 * n_rank))) - 2
         by_k.setdefault(kk, []).append(m)
     gram_by_k = {str(kk): {"ms": float(np.mean(v)), "GBs": 8.0 * n_rank * (kk + 2) / (np.mean(v) * 1e-3) / 1e9,
-                           "kernel": "k_gram_v" if kk <= 8 else "k_gram_s"} for kk, v in sorted(by_k.items())}
+                           "kernel": "k_gram_v" if kk <= 9 else "k_gram_s"} for kk, v in sorted(by_k.items())}
 
     # JVP microbenchmark (single vector, 24 n bytes per launch)
     sl = solver.dev.slab
@@ -328,8 +328,8 @@ def main():
                    "basis_k_range": [min(s["k"] for s in tr), max(s["k"] for s in tr)] if tr else None,
                    "armijo_trials": int(sum(s["trials"] for s in tr)),
                    "parallelism": f"slab{world}"},
-        "roofline": {"kernel": "Gram pass of the CholeskyQR solve, J V T on the fly (k_gram_v: VALU, k <= 8; "
-                               "k_gram_s: staged fp64 MFMA, k > 8)", "bound": "hbm",
+        "roofline": {"kernel": "Gram pass of the CholeskyQR solve, J V T on the fly (k_gram_v: VALU, k <= 9; "
+                               "k_gram_s: staged fp64 MFMA, k > 9)", "bound": "hbm",
                      "achieved": g_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": g_gbs / HBM_PEAK_GBS,
                      "traffic": traffic, "traffic_source": traffic_src,
                      "avg_launch_ms": g_avg_ms, "algorithmic_bytes_per_launch": g_avg_bytes,

@@ -1870,7 +1870,10 @@ __device__ __forceinline__ void gram_v_point(const double (&a)[K], double rv, co
     for (int j = i; j <= K; ++j, ++q) acc[q] = fma(y[i], y[j], acc[q]);
 }
 
-constexpr int GV_KMAX = 8;
+constexpr int GV_KMAX = 9;      // VALU Gram pass for k <= GV_KMAX (with r); k = 10 measured slower
+                                // than the staged kernel (2.20 vs 2.08 ms, 256 VGPRs)
+constexpr int GV1_KMIN = 9;     // one point per lane from here (register budget; k = 7, 8 measured
+                                // faster with two points per lane, 16-byte loads)
 constexpr int GV_SW = 128;           // strip width: 64 lanes x 2 points
 
 template <int K>
@@ -1942,6 +1945,80 @@ __global__ __launch_bounds__(BLOCK) void k_gram_v(const double* __restrict__ u, 
         vc[j] = vs[j];
       }
       gram_v_point<K>(a, rr.y, T, ldt, acc);
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < NT; ++q) {
+    const double sq = wave_sum(acc[q]);
+    if (lane == 0) red[wave][q] = sq;
+  }
+  __syncthreads();
+  for (int q = threadIdx.x; q < NT; q += BLOCK) {
+    double sq = red[0][q];
+    for (int w = 1; w < BLOCK / 64; ++w) sq += red[w][q];
+    partial[size_t(blockIdx.x) * NT + q] = sq;
+  }
+}
+
+// One-point-per-lane form of k_gram_v (64-point strips, 8-byte loads): half the marching-row registers,
+// so K = 9 still runs at two waves per SIMD (1.54 ms vs 2.05 ms for the staged kernel at 8192^2).
+template <int K>
+__global__ __launch_bounds__(BLOCK) void k_gram_v1(const double* __restrict__ u, const double* __restrict__ V,
+                                                   int64_t ldv, const double* __restrict__ T, int ldt,
+                                                   const double* __restrict__ r, Geo geo, Coef c, int64_t rpr,
+                                                   double* __restrict__ partial) {
+  constexpr int NT = (K + 1) * (K + 2) / 2;
+  __shared__ double red[BLOCK / 64][NT];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int64_t N = geo.N;
+  const int64_t nstrips = N / 64;
+  const int64_t gw = int64_t(blockIdx.x) * (BLOCK / 64) + wave;
+  const int64_t x0 = (gw / nstrips) * rpr;
+  const int64_t x1 = min(geo.nrows, x0 + rpr);
+  const int64_t iy = (gw % nstrips) * 64 + lane;
+  const double cw = iy > 0 ? c.hm2 : 0.0, ce = iy + 1 < N ? c.hm2 : 0.0;
+  const double up = -c.j_lin_up;
+  const bool edge_w = lane == 0, edge_e = lane == 63;
+  const int eoff = edge_w ? -1 : 1;                 // the edge lanes' outer neighbour (others: unused)
+  double acc[NT];
+#pragma unroll
+  for (int q = 0; q < NT; ++q) acc[q] = 0.0;
+  if (x0 < x1) {
+    double vn[K], vc[K];
+    int64_t i = (G + x0) * N + iy;
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+      vn[j] = V[j * ldv + i - N];
+      vc[j] = V[j * ldv + i];
+    }
+    for (int64_t x = x0; x < x1; ++x, i += N) {
+      double vs[K], eo[K];
+#pragma unroll
+      for (int j = 0; j < K; ++j) {
+        const double* cp = V + j * ldv + i;
+        vs[j] = cp[N];
+        eo[j] = cp[eoff];
+      }
+      const double dn = -jdiag(c, u[i]);
+      const double rv = r[i];
+      double a[K];
+#pragma unroll
+      for (int j = 0; j < K; ++j) {
+        double w = __shfl_up(vc[j], 1);
+        double e = __shfl_down(vc[j], 1);
+        if (edge_w) w = eo[j];
+        if (edge_e) e = eo[j];
+        double sv = c.hm2 * vn[j];
+        sv = fma(cw, w, sv);
+        sv = fma(dn, vc[j], sv);
+        sv = fma(ce, e, sv);
+        sv = fma(up, vs[j], sv);
+        a[j] = sv;
+        vn[j] = vc[j];
+        vc[j] = vs[j];
+      }
+      gram_v_point<K>(a, rv, T, ldt, acc);
     }
   }
 #pragma unroll
@@ -2820,10 +2897,13 @@ int gnk_gram(gnk_ctx* ctx, const double* u, const double* V, int64_t ldv, int k,
   // GNK_GRAM_STAGED=2 (tests) forces the staged kernel instead
   const char* valu_s = getenv("GNK_GRAM_VALU");
   const char* staged_f = getenv("GNK_GRAM_STAGED");
-  if (r && k <= GV_KMAX && ctx->geo.N % GV_SW == 0 && !(valu_s && atoi(valu_s) == 0) &&
+  const char* v1_s = getenv("GNK_GRAM_V1");        // 0: no one-point form (then k <= 8 only)
+  const int gv_kmax = (v1_s && atoi(v1_s) == 0) ? GV1_KMIN - 1 : GV_KMAX;
+  if (r && k <= gv_kmax && ctx->geo.N % GV_SW == 0 && !(valu_s && atoi(valu_s) == 0) &&
       !(staged_f && atoi(staged_f) == 2) && !getenv("GNK_DEBUG_GRAM")) {
     const double* tv = rinv ? rinv : ctx->ident + ident_offset(KP / 16);
-    const int64_t nstrips = ctx->geo.N / GV_SW;
+    const bool one_pt = k >= GV1_KMIN && !(v1_s && atoi(v1_s) == 0);
+    const int64_t nstrips = ctx->geo.N / (one_pt ? 64 : GV_SW);
     const int64_t nrows = ctx->geo.nrows;
     // about 8 waves per CU, whole row ranges per strip
     int64_t nranges = std::max<int64_t>(1, std::min<int64_t>(nrows, int64_t(ctx->num_cus) * 8 / nstrips));
@@ -2839,16 +2919,25 @@ int gnk_gram(gnk_ctx* ctx, const double* u, const double* V, int64_t ldv, int k,
 #define GRAMV(KV)                                                                                            \
   hipLaunchKernelGGL((k_gram_v<KV>), dim3(unsigned(nblk)), dim3(BLOCK), 0, ctx->stream, u, V, ldv, tv, KP, r, \
                      ctx->geo, ctx->coef, rpr, ctx->scratch)
-    switch (k) {
-      case 1: GRAMV(1); break;
-      case 2: GRAMV(2); break;
-      case 3: GRAMV(3); break;
-      case 4: GRAMV(4); break;
-      case 5: GRAMV(5); break;
-      case 6: GRAMV(6); break;
-      case 7: GRAMV(7); break;
-      default: GRAMV(8); break;
+#define GRAMV1(KV)                                                                                            \
+  hipLaunchKernelGGL((k_gram_v1<KV>), dim3(unsigned(nblk)), dim3(BLOCK), 0, ctx->stream, u, V, ldv, tv, KP, r, \
+                     ctx->geo, ctx->coef, rpr, ctx->scratch)
+    if (one_pt) {
+      GRAMV1(9);
+    } else {
+      switch (k) {
+        case 1: GRAMV(1); break;
+        case 2: GRAMV(2); break;
+        case 3: GRAMV(3); break;
+        case 4: GRAMV(4); break;
+        case 5: GRAMV(5); break;
+        case 6: GRAMV(6); break;
+        case 7: GRAMV(7); break;
+        case 8: GRAMV(8); break;
+        default: return fail(ctx, "gram: VALU pass beyond k = 8 needs the one-point kernel");
+      }
     }
+#undef GRAMV1
 #undef GRAMV
     tlv.done();
     int rcv = check_launch(ctx, "gram_v");

@@ -254,7 +254,8 @@ def test_cgs_max_propagates_nan():
                                                   # VALU kernel (N % 128 == 0, k <= 8 with r)
                                                   (128, 1, True, False), (256, 2, True, True), (384, 3, True, True),
                                                   (256, 5, True, True), (1024, 6, True, True), (640, 7, True, False),
-                                                  (1024, 8, True, True)])
+                                                  (1024, 8, True, True), (256, 9, True, True), (128, 9, True, False),
+                                                  (640, 7, True, True), (512, 10, True, True)])
 @pytest.mark.parametrize("staged", ["default", "forced", "ring4"])
 def test_gram_mfma(N, k, with_r, with_rinv, staged, monkeypatch):
     """W = [J V | r] @ RinvAug on fp64 MFMA vs an fp64 NumPy Gram (host BLAS).  "forced" runs
