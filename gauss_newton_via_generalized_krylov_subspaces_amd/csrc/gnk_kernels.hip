@@ -1913,7 +1913,7 @@ __global__ __launch_bounds__(BLOCK) void k_gram_v(const double* __restrict__ u, 
       for (int j = 0; j < K; ++j) {
         const double* cp = V + j * ldv + i;
         vs[j] = *reinterpret_cast<const d2*>(cp + N);
-        eo[j] = cp[eoff];
+        eo[j] = (edge_w || edge_e) ? cp[eoff] : 0.0;     // only the strip's edge lanes load
       }
       const d2 uu = *reinterpret_cast<const d2*>(u + i);
       const d2 rr = *reinterpret_cast<const d2*>(r + i);
@@ -1998,7 +1998,7 @@ __global__ __launch_bounds__(BLOCK) void k_gram_v1(const double* __restrict__ u,
       for (int j = 0; j < K; ++j) {
         const double* cp = V + j * ldv + i;
         vs[j] = cp[N];
-        eo[j] = cp[eoff];
+        eo[j] = (edge_w || edge_e) ? cp[eoff] : 0.0;     // only the strip's edge lanes load
       }
       const double dn = -jdiag(c, u[i]);
       const double rv = r[i];

@@ -22,7 +22,7 @@ def load(d, counter):
     return vals
 
 
-GRAM = re.compile(r"k_gram_[smwv]<")    # every Gram-pass kernel (staged / marching / chunked / VALU)
+GRAM = re.compile(r"k_gram_(?:[smw]|v1?)<")    # every Gram-pass kernel (staged / marching / chunked / VALU)
 
 
 def main(d, config=None):
