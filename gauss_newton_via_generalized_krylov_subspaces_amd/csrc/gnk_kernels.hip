@@ -2902,7 +2902,9 @@ int gnk_gram(gnk_ctx* ctx, const double* u, const double* V, int64_t ldv, int k,
   if (r && k <= gv_kmax && ctx->geo.N % GV_SW == 0 && !(valu_s && atoi(valu_s) == 0) &&
       !(staged_f && atoi(staged_f) == 2) && !getenv("GNK_DEBUG_GRAM")) {
     const double* tv = rinv ? rinv : ctx->ident + ident_offset(KP / 16);
-    const bool one_pt = k >= GV1_KMIN && !(v1_s && atoi(v1_s) == 0);
+    const char* v1min_s = getenv("GNK_GRAM_V1MIN");       // tooling A/B: first k of the one-point form
+    const int v1min = v1min_s ? std::max(7, atoi(v1min_s)) : GV1_KMIN;
+    const bool one_pt = k >= v1min && !(v1_s && atoi(v1_s) == 0);
     const int64_t nstrips = ctx->geo.N / (one_pt ? 64 : GV_SW);
     const int64_t nrows = ctx->geo.nrows;
     // about 8 waves per CU, whole row ranges per strip
@@ -2923,7 +2925,7 @@ int gnk_gram(gnk_ctx* ctx, const double* u, const double* V, int64_t ldv, int k,
   hipLaunchKernelGGL((k_gram_v1<KV>), dim3(unsigned(nblk)), dim3(BLOCK), 0, ctx->stream, u, V, ldv, tv, KP, r, \
                      ctx->geo, ctx->coef, rpr, ctx->scratch)
     if (one_pt) {
-      GRAMV1(9);
+      if (k == 7) GRAMV1(7); else if (k == 8) GRAMV1(8); else GRAMV1(9);
     } else {
       switch (k) {
         case 1: GRAMV(1); break;
