@@ -384,11 +384,21 @@ class GNKSolver:
         restart = it % self.restart == 0
         if it >= self.max_iter - 1:
             self.done = True
-        if basis.pending and (restart or self.done):
+        if basis.pending and self.done and not restart:
             self._settle_explicit()
         if restart:                                                       # :135-136
             xr = self._free_x(self.uJ)
-            basis.x(self.e, self.xb[xr])
+            if basis.pending and hasattr(basis, "x_settle"):
+                # the pending column's breakdown test rides on the restart point's GEMV
+                it_p = basis.pend["it"]
+                if basis.x_settle(self.e, self.xb[xr]):
+                    self._breakdown_message(it_p)
+                else:
+                    self._append_coordinate()
+            else:
+                if basis.pending:
+                    self._settle_explicit()
+                basis.x(self.e, self.xb[xr])
             self.c = basis.start(self.xb[xr])
             self.e = self.c.copy()
             self.lls.on_restart()

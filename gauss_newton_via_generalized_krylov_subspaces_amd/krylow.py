@@ -21,7 +21,9 @@ column is settled by the next pass that reads V anyway:
     column k (the arithmetic of the CGS kernel) and returns sum w^2 and max |w|
     with the trial's residual, so the norm (:71) and the breakdown test (:66)
     come back with a host read the trial makes anyway (``resolve``);
-  * a restart or the end of the loop settles it explicitly (``resolve_explicit``).
+  * a restart settles it inside the GEMV of the restart point (``x_settle``: the same
+    materialisation kernel with coefficient 0 for the column), the end of the loop
+    explicitly (``resolve_explicit``).
 Column j of the reference basis is ``sc[j] * V[j]`` (sc = 1 / ||w||: the
 division of :71 is folded into the coefficients of every product with V).  The
 solver keeps the iterate's coordinates twice: ``c`` in the reference's units (the
@@ -211,6 +213,23 @@ class DeviceKrylovBasis:
         g = self._slot(self.pend["slot"])
         self.be.upload(self._hh, self.pend["hh"])
         self.be.cgs_update(self.V, self.k, self._hh, g, self._stats)
+        sumsq, maxabs = self.dev.comm.sum_max(self._stats)
+        return self.resolve(sumsq, maxabs)
+
+    def x_settle(self, e: np.ndarray, out) -> bool:
+        """Restart point out = V @ e (e over the k settled columns, the reference's V @ c) with the
+        pending column settled in the same pass: k_gemv_p materialises w = g - V hh and returns
+        sum w^2, max |w| for its breakdown test (ref:krylow.py:66) -- the column itself enters out with
+        coefficient 0, as the reference's appended coordinate.  Replaces cgs_update + gemv (one read
+        of V instead of two).  Returns True on breakdown (then the column is dropped)."""
+        k = self.k
+        if self.pend is None or self.pend["slot"] != k:
+            raise RuntimeError("x_settle: no pending column in slot k")
+        if len(e) != k:
+            raise RuntimeError("x_settle: coefficient vector must cover the settled columns")
+        self.be.upload(self._c, np.append(e, 0.0))
+        self.be.upload(self._hh, self.pend["hh"])
+        self.be.gemv_pending(self.V, k, self._c, self._hh, out, self._stats)
         sumsq, maxabs = self.dev.comm.sum_max(self._stats)
         return self.resolve(sumsq, maxabs)
 
