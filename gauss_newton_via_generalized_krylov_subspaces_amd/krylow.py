@@ -73,11 +73,11 @@ class DeviceKrylovBasis:
         self._hh = self.be.zeros(self.kmax)
         self._h = self.be.zeros(self.kmax + 1)
         self._stats = self.be.zeros(2)
-        # [sum r^2, sum w^2, max |w|, h_0 .. h_k] of a first trial: one collective / host read;
-        # two (a speculatively enqueued next step has its own)
-        self.packs = [self.be.zeros(3 + self.kmax + 1) for _ in range(2)]
-        self.pack = self.packs[0]
-        self._sc_dev = [self.be.zeros(self.kmax) for _ in range(2)]
+        # [sum r^2, sum w^2, max |w|, h_0 .. h_k] of a first trial: one collective / host read (the
+        # speculative next step reads it on the device before the next trial overwrites it, in
+        # stream order)
+        self.pack = self.be.zeros(3 + self.kmax + 1)
+        self._sc_dev = [self.be.zeros(self.kmax) for _ in range(2)]      # k_lls_next inputs, per buffer set
         self._g = dev.vec()              # raw g when V has no free slot (never pending in a Gram)
 
     @property
@@ -167,12 +167,6 @@ class DeviceKrylovBasis:
         """The folded column scales sc[:k] uploaded into device buffer ``par`` (k_lls_next input)."""
         self.be.upload(self._sc_dev[par], self.sc[:k])
         return self._sc_dev[par]
-
-    def enqueue_products(self, u_jac, r, k, pack):
-        """The basis-update products of ref:krylow.py:62,64 for a basis of k settled columns:
-        g = -J(u_jac)^T r into slot k, pack[3:3+k] = V^T g (this rank).  Returns the slot."""
-        self.be.vjp_gemv_t(u_jac, r, self.V, k, self._slot(k), pack[3:3 + k])
-        return k
 
     def trial_first(self, e_ext, out, r_products=None, coef_dev=None, pack=None):
         """``enqueue_trial`` on the host's current basis (settled k, pending column if any; its hh
