@@ -278,14 +278,23 @@ def main():
     g_avg_bytes = float(np.mean(g_by)) if g_by else float("nan")
     g_gbs = g_avg_bytes / (g_avg_ms * 1e-3) / 1e9 if g_ms else float("nan")
     gram_share = sum(g_ms) * 1e-3 / elapsed if g_ms else float("nan")
-    # per basis size: columns = bytes / (8 n_rank) - 2 (V, u, r); kernel = VALU for k <= 9, staged above
+    # per basis size: columns = bytes / (8 n_rank) - 2 (V, u, r); kernel as gnk_gram dispatches a pass
+    # with P^-1 and r: VALU k <= 9, staged k <= 20 (N % 128 == 0), chunked k_gram_w up to 47 columns
+    # (+ r), the prefetching k_gram_wp up to 63, the pair-split k_gram beyond
+    def gram_kernel(kk):
+        if kk <= 9:
+            return "k_gram_v"
+        if kk <= 20 and N % 128 == 0:
+            return "k_gram_s"
+        return "k_gram_w" if kk + 1 <= 48 else "k_gram_wp" if kk + 1 <= 64 else "k_gram"
+
     n_rank = solver.dev.slab.nrows * N
     by_k = {}
     for m, b in launches:
         kk = int(round(b / (8.0 * n_rank))) - 2
         by_k.setdefault(kk, []).append(m)
     gram_by_k = {str(kk): {"ms": float(np.mean(v)), "GBs": 8.0 * n_rank * (kk + 2) / (np.mean(v) * 1e-3) / 1e9,
-                           "kernel": "k_gram_v" if kk <= 9 else "k_gram_s"} for kk, v in sorted(by_k.items())}
+                           "kernel": gram_kernel(kk)} for kk, v in sorted(by_k.items())}
 
     # JVP microbenchmark (single vector, 24 n bytes per launch)
     sl = solver.dev.slab

@@ -1381,6 +1381,186 @@ __global__ __launch_bounds__(BLOCK) void k_gram_w(const double* __restrict__ u, 
   for (int idx = tid; idx < P * 256; idx += blockDim.x) out[idx] = red[idx];
 }
 
+// Prefetching chunked Gram pass (KP <= 64; the wide-basis pass, k > 20 on the GNK path).  Same
+// 32-row chunks, LDS transpose tile, in-place W <- W RinvAug and Gram MFMAs as k_gram_w, but every
+// basis column of the NEXT chunk is loaded while the MFMAs of the current one run: a lane keeps
+// all its columns' north / centre / south pairs in registers (3 loads per column instead of 5;
+// the in-row neighbours come from the adjacent lanes of the 16-lane DPP row, only the chunk's two
+// edge lanes load their outer neighbour), and the loads of chunk c + 1 are issued between the
+// stencil of chunk c and its MFMAs.  k_gram_w waits for each column group's loads in turn (SQ
+// counters at k = 51: waves waiting 51 % of the time, MFMA busy 27 %).  Same FMA order as
+// k_gram_w, so the two kernels give bit-identical Grams.
+__device__ __forceinline__ double dpp_row_shr1(double v) {     // lane l <- lane l-1 of its 16-lane row
+  const u2v b = __builtin_bit_cast(u2v, v);
+  u2v o;
+  o.x = unsigned(__builtin_amdgcn_update_dpp(0, int(b.x), 0x111, 0xf, 0xf, false));
+  o.y = unsigned(__builtin_amdgcn_update_dpp(0, int(b.y), 0x111, 0xf, 0xf, false));
+  return __builtin_bit_cast(double, o);
+}
+__device__ __forceinline__ double dpp_row_shl1(double v) {     // lane l <- lane l+1 of its 16-lane row
+  const u2v b = __builtin_bit_cast(u2v, v);
+  u2v o;
+  o.x = unsigned(__builtin_amdgcn_update_dpp(0, int(b.x), 0x101, 0xf, 0xf, false));
+  o.y = unsigned(__builtin_amdgcn_update_dpp(0, int(b.y), 0x101, 0xf, 0xf, false));
+  return __builtin_bit_cast(double, o);
+}
+
+template <int NB, int CHT>
+__global__ __launch_bounds__(BLOCK) void k_gram_wp(
+    const double* __restrict__ u, const double* __restrict__ V, int64_t ldv, int k, const double* __restrict__ rinv,
+    const double* __restrict__ r, Geo geo, Coef c, int64_t nchunks, double* __restrict__ partial) {
+  // a lane holds 2 consecutive rows; LPC lanes per column (a 16-lane DPP row holds one column at
+  // CHT = 32, two at CHT = 16: the lanes where a shift would cross a column are the edge lanes)
+  constexpr int LPC = CHT / 2, CG = 64 / LPC;
+  static_assert(CHT == 16 || CHT == 32, "k_gram_wp: 16- or 32-row chunks");
+  constexpr int KP = 16 * NB, S = KP + 1, P = NB * (NB + 1) / 2, NS = KP / CG;   // NS column slots per lane
+  extern __shared__ __attribute__((aligned(16))) double lds[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int nwave = blockDim.x >> 6;
+  double* Wt = lds + wave * (CHT * S);
+  double* rinv_lds = rinv ? lds + nwave * CHT * S : nullptr;
+  const int64_t N = geo.N;
+  const int64_t nown = geo.nrows * N;
+  const int64_t base = int64_t(G) * N;
+  const int K1 = k + (r ? 1 : 0);
+  __builtin_assume(K1 > 16 * (NB - 1));             // KP = gnk_gram_padded_dim(k, r)
+
+  d4 acc[P];
+#pragma unroll
+  for (int q = 0; q < P; ++q) acc[q] = d4{0.0, 0.0, 0.0, 0.0};
+  for (int idx = lane; idx < CHT * S; idx += 64) Wt[idx] = 0.0;     // padding columns stay 0
+  if (rinv_lds)
+    for (int idx = tid; idx < KP * KP; idx += blockDim.x) rinv_lds[idx] = rinv[idx];
+  __syncthreads();
+
+  const int64_t nw = int64_t(gridDim.x) * nwave;
+  const double up = -c.j_lin_up;
+  const int pl = lane % LPC, p2 = pl * 2, cg = lane / LPC;
+  const bool edge_w = pl == 0, edge_e = pl == LPC - 1;
+  const int eoff = edge_w ? -1 : 2;                 // the edge lane's outer neighbour, relative to its row i
+
+  d2 vn[NS], vc[NS], vs[NS], uu, rv = d2{0.0, 0.0};
+  double eo[NS];
+  auto issue = [&](int64_t ch) {
+    const int64_t e0 = ch * CHT;
+    const int64_t i = base + (e0 + p2 < nown ? e0 + p2 : nown - 2);
+    uu = *reinterpret_cast<const d2*>(u + i);
+    if (r) rv = *reinterpret_cast<const d2*>(r + i);
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      if (s * CG < k) {                             // wave-uniform: slot holds at least one column
+        const double* cp = V + int64_t(min(s * CG + cg, k - 1)) * ldv + i;
+        vn[s] = *reinterpret_cast<const d2*>(cp - N);
+        vc[s] = *reinterpret_cast<const d2*>(cp);
+        vs[s] = *reinterpret_cast<const d2*>(cp + N);
+        eo[s] = (edge_w || edge_e) ? cp[eoff] : 0.0;
+      }
+    }
+  };
+
+  const int64_t ch0 = int64_t(blockIdx.x) * nwave + wave;
+  const int64_t step = (nw * CHT) % N;
+  int64_t iyb = (ch0 * CHT) % N;
+  if (ch0 < nchunks) issue(ch0);
+  for (int64_t ch = ch0; ch < nchunks; ch += nw) {
+    const int64_t e0 = ch * CHT;
+    int64_t iy0 = iyb + p2;
+    if (N >= 64) {
+      if (iy0 >= N) iy0 -= N;
+    } else {
+      while (iy0 >= N) iy0 -= N;
+    }
+    int64_t iy1 = iy0 + 1;
+    if (iy1 >= N) iy1 -= N;
+    iyb += step;
+    if (iyb >= N) iyb -= N;
+    const bool val0 = e0 + p2 < nown, val1 = e0 + p2 + 1 < nown;
+    const double cw0 = iy0 > 0 ? c.hm2 : 0.0, ce0 = iy0 + 1 < N ? c.hm2 : 0.0;   // s + 0*v == s
+    const double cw1 = iy1 > 0 ? c.hm2 : 0.0, ce1 = iy1 + 1 < N ? c.hm2 : 0.0;
+    const double dn0 = -jdiag(c, uu.x), dn1 = -jdiag(c, uu.y);
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      if (s * CG < k) {
+        const double w0 = dpp_row_shr1(vc[s].y), e1 = dpp_row_shl1(vc[s].x);
+        const double vw0 = edge_w ? eo[s] : w0, ve1 = edge_e ? eo[s] : e1;
+        double s0 = c.hm2 * vn[s].x;
+        s0 = fma(cw0, vw0, s0);
+        s0 = fma(dn0, vc[s].x, s0);
+        s0 = fma(ce0, vc[s].y, s0);
+        s0 = fma(up, vs[s].x, s0);
+        double s1 = c.hm2 * vn[s].y;
+        s1 = fma(cw1, vc[s].x, s1);
+        s1 = fma(dn1, vc[s].y, s1);
+        s1 = fma(ce1, ve1, s1);
+        s1 = fma(up, vs[s].y, s1);
+        const int j = s * CG + cg;
+        if (j < k) {
+          Wt[p2 * S + j] = val0 ? s0 : 0.0;
+          Wt[(p2 + 1) * S + j] = val1 ? s1 : 0.0;
+        }
+      }
+    }
+    if (r && cg == 0) {
+      Wt[p2 * S + k] = val0 ? rv.x : 0.0;
+      Wt[(p2 + 1) * S + k] = val1 ? rv.y : 0.0;
+    }
+    // the next chunk's loads fly while this chunk's MFMAs run
+    if (ch + nw < nchunks) issue(ch + nw);
+    __builtin_amdgcn_sched_barrier(0);
+    if (rinv_lds) {
+      // in place W <- W @ RinvAug, column blocks descending (block cb reads blocks a <= cb only)
+#pragma unroll
+      for (int c16 = 0; c16 < CHT; c16 += 16) {
+#pragma unroll
+        for (int cb = NB - 1; cb >= 0; --cb) {
+          d4 qv = d4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+          for (int ab = 0; ab <= cb; ++ab) {
+#pragma unroll
+            for (int ks = 0; ks < 4; ++ks) {
+              if (ab < NB - 1 || ab * 16 + ks * 4 < K1) {   // RinvAug rows >= K1 are zero
+                const int kk = ab * 16 + ks * 4 + (lane >> 4);
+                qv = mfma64(Wt[(c16 + (lane & 15)) * S + kk], rinv_lds[kk * KP + cb * 16 + (lane & 15)], qv);
+              }
+            }
+          }
+#pragma unroll
+          for (int ii = 0; ii < 4; ++ii) Wt[(c16 + (lane >> 4) + 4 * ii) * S + cb * 16 + (lane & 15)] = qv[ii];
+        }
+      }
+    }
+    const double* rowbase = Wt + (lane >> 4) * S + (lane & 15);
+#pragma unroll
+    for (int r4 = 0; r4 < CHT; r4 += 4) {
+      const double* row = rowbase + r4 * S;
+      double a[NB];
+#pragma unroll
+      for (int bb = 0; bb < NB; ++bb) a[bb] = row[bb * 16];
+#pragma unroll
+      for (int q = 0; q < P; ++q) acc[q] = mfma64(a[pair_a(q, NB)], a[pair_b(q, NB)], acc[q]);
+    }
+  }
+
+  // block partial = ((w0 + w1) + w2) + ... through LDS, layout [block][pair][lane*4 + i]
+  __syncthreads();
+  double* red = lds;
+  for (int w = 0; w < nwave; ++w) {
+    if (wave == w) {
+#pragma unroll
+      for (int q = 0; q < P; ++q)
+#pragma unroll
+        for (int ii = 0; ii < 4; ++ii) {
+          double* dst = red + q * 256 + lane * 4 + ii;
+          *dst = (w == 0) ? acc[q][ii] : *dst + acc[q][ii];
+        }
+    }
+    __syncthreads();
+  }
+  double* out = partial + size_t(blockIdx.x) * size_t(P) * 256;
+  for (int idx = tid; idx < P * 256; idx += blockDim.x) out[idx] = red[idx];
+}
+
 // Marching Gram pass (N % CHT == 0, k <= 8 CG).  Wave gw owns the vertical strip
 // s = gw % nstrips (CHT consecutive grid columns) and walks a contiguous range of grid rows.
 // Each lane keeps, for each of its <= 8 basis columns, the values of the current row and the
@@ -3094,6 +3274,41 @@ int gnk_gram(gnk_ctx* ctx, const double* u, const double* V, int64_t ldv, int k,
           return check_launch(ctx, "gram scatter");
         }
       }
+    }
+    // prefetching kernel for NB = 4 (k_gram_w keeps one wave per SIMD there: 98.5 KB of LDS per
+    // block; at 8192^2, k = 51 / 61 with P^-1 and r: 23.0 / 24.5 ms vs 31.4 / 33.4 ms).  For NB <= 3
+    // k_gram_w runs two waves per SIMD and stays ahead (k = 33: 12.4 vs 16.7 ms), so it keeps those.
+    // 16-row chunks (less LDS and fewer registers per wave) and two waves per SIMD measured slower
+    // for every NB (k = 51: 24.4 ms).  GNK_GRAM_WP=0 / 2: tooling A/B (never / also for NB = 2, 3)
+    static const int wp_env = getenv("GNK_GRAM_WP") ? atoi(getenv("GNK_GRAM_WP")) : 1;
+    if (wp_env && !dbg && !ch_env && !bc_env && (nb == 4 || (wp_env == 2 && nb >= 2))) {
+      constexpr int chp = 32;
+      size_t ldsp = size_t(nwave) * chp * (KP + 1) * 8 + (rinv ? size_t(KP) * KP * 8 : 0);
+      ldsp = std::max(ldsp, size_t(P) * 256 * 8);
+      ldsp = (ldsp + 15) & ~size_t(15);
+      const int64_t nchp = (nown + chp - 1) / chp;
+      const int wgp = std::max<int>(1, std::min<int>(8, int((160 * 1024) / ldsp)));
+      int64_t nbp = std::min<int64_t>((nchp + nwave - 1) / nwave, int64_t(ctx->num_cus) * wgp);
+      nbp = std::max<int64_t>(nbp, 1);
+      if (size_t(nbp) * P * 256 > SCRATCH_DOUBLES) return fail(ctx, "gram: scratch too small");
+      TimedLaunch tlp(ctx, GNK_TIMER_GRAM, 8.0 * double(nown) * double(k + 1 + (r ? 1 : 0)));
+#define GRAMWP(NBV)                                                                                    \
+  hipLaunchKernelGGL((k_gram_wp<NBV, chp>), dim3(unsigned(nbp)), dim3(64 * nwave), ldsp, ctx->stream, u, V, ldv, \
+                     k, rinv, r, ctx->geo, ctx->coef, nchp, ctx->scratch)
+      if (nb == 2) GRAMWP(2);
+      else if (nb == 3) GRAMWP(3);
+      else GRAMWP(4);
+#undef GRAMWP
+      tlp.done();
+      int rcp = check_launch(ctx, "gram_wp");
+      if (rcp) return rcp;
+      (void)hipMemsetAsync(G_out, 0, size_t(KP) * KP * sizeof(double), ctx->stream);
+      double* red = ctx->scratch + (SCRATCH_DOUBLES - size_t(P) * 256);
+      rcp = wreduce(ctx, ctx->scratch, int(nbp), P * 256, int64_t(P) * 256, P * 256, 0, nullptr, red);
+      if (rcp) return rcp;
+      hipLaunchKernelGGL(k_gram_scatter, dim3((P * 256 + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, ctx->stream, red, P, KP,
+                         G_out);
+      return check_launch(ctx, "gram scatter");
     }
     TimedLaunch tl(ctx, GNK_TIMER_GRAM, 8.0 * double(nown) * double(k + 1 + (r ? 1 : 0)));
 #define GRAMW1(NBV, BCV, CHV) hipLaunchKernelGGL((k_gram_w<NBV, BCV, CHV>), dim3(unsigned(nblk)), dim3(64 * nwave), \

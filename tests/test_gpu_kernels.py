@@ -255,7 +255,10 @@ def test_cgs_max_propagates_nan():
                                                   (128, 1, True, False), (256, 2, True, True), (384, 3, True, True),
                                                   (256, 5, True, True), (1024, 6, True, True), (640, 7, True, False),
                                                   (1024, 8, True, True), (256, 9, True, True), (128, 9, True, False),
-                                                  (640, 7, True, True), (512, 10, True, True)])
+                                                  (640, 7, True, True), (512, 10, True, True),
+                                                  # prefetching wide-basis kernel (KP 32..64; partial tail chunks)
+                                                  (64, 51, True, True), (64, 40, False, True), (96, 22, True, True),
+                                                  (130, 33, True, True), (48, 60, True, True), (24, 30, True, False)])
 @pytest.mark.parametrize("staged", ["default", "forced", "ring4"])
 def test_gram_mfma(N, k, with_r, with_rinv, staged, monkeypatch):
     """W = [J V | r] @ RinvAug on fp64 MFMA vs an fp64 NumPy Gram (host BLAS).  "forced" runs
