@@ -258,7 +258,9 @@ def test_cgs_max_propagates_nan():
                                                   (640, 7, True, True), (512, 10, True, True),
                                                   # prefetching wide-basis kernel (KP 32..64; partial tail chunks)
                                                   (64, 51, True, True), (64, 40, False, True), (96, 22, True, True),
-                                                  (130, 33, True, True), (48, 60, True, True), (24, 30, True, False)])
+                                                  (130, 33, True, True), (48, 60, True, True), (24, 30, True, False),
+                                                  # NB = 4: flattened order (N % 32 != 0) / down-strip walks crossing strips
+                                                  (100, 55, True, True), (96, 50, True, False), (416, 49, True, True)])
 @pytest.mark.parametrize("staged", ["default", "forced", "ring4"])
 def test_gram_mfma(N, k, with_r, with_rinv, staged, monkeypatch):
     """W = [J V | r] @ RinvAug on fp64 MFMA vs an fp64 NumPy Gram (host BLAS).  "forced" runs
