@@ -218,8 +218,15 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
         os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        # GNK_BENCH_BACKEND=gloo: rehearsal of the multi-rank bench on fewer GPUs than ranks (ranks
+        # share cards, collectives staged through the host); the measured runs use RCCL, one GPU each
+        backend = os.environ.get("GNK_BENCH_BACKEND", "nccl")
+        if backend == "gloo":
+            torch.cuda.set_device(local % torch.cuda.device_count())
+            dist.init_process_group("gloo")
+        else:
+            torch.cuda.set_device(local)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     else:
         torch.cuda.set_device(0)
     device = torch.device("cuda", torch.cuda.current_device())
@@ -336,7 +343,8 @@ def main():
                    "krylow_restart": args.restart, "version": args.version, "ALPHA": 5, "LAMBDA": 10,
                    "basis_k_range": [min(s["k"] for s in tr), max(s["k"] for s in tr)] if tr else None,
                    "armijo_trials": int(sum(s["trials"] for s in tr)),
-                   "parallelism": f"slab{world}"},
+                   "parallelism": f"slab{world}",
+                   "transport": (dist.get_backend() if world > 1 else "none")},
         "roofline": {"kernel": "Gram pass of the CholeskyQR solve, J V T on the fly (k_gram_v: VALU, k <= 9; "
                                "k_gram_s: staged fp64 MFMA, k > 9)", "bound": "hbm",
                      "achieved": g_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": g_gbs / HBM_PEAK_GBS,
