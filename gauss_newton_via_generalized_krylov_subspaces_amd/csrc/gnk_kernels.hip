@@ -3214,7 +3214,7 @@ int gnk_gram(gnk_ctx* ctx, const double* u, const double* V, int64_t ldv, int k,
     static const int bc_env = getenv("GNK_GRAM_BC") ? atoi(getenv("GNK_GRAM_BC")) : 0;   // tooling A/B switch
     static const int ch_env = getenv("GNK_GRAM_CH") ? atoi(getenv("GNK_GRAM_CH")) : 0;
     // chunk height: 64 rows for one column block, 32 rows above (LDS tile 32 x (KP+1) per wave)
-    const int chv = ch_env ? ch_env : (KP <= 32 ? 64 : 32);
+    const int chv = (ch_env == 32 || ch_env == 64) ? ch_env : (KP <= 32 ? 64 : 32);   // instantiated heights
     const int nwave = 4;
     size_t ldsw = size_t(nwave) * chv * (KP + 1) * 8 + (rinv ? size_t(KP) * KP * 8 : 0);
     ldsw = std::max(ldsw, size_t(P) * 256 * 8);
