@@ -260,6 +260,7 @@ class HostCallableOps:
         if self._lsq is None:
             self._lsq = CholQR2Solver(self, self.n, gram=self.gram, n_global=self.n, device_solve=False)
             self._lsq.quiet = True
+            self._lsq.min_norm_if_singular = True
             self._eye = _IdentityBasis(self.be, self.n)
         dh, _, _ = self._lsq.solve(u, self._eye, r)
         d.copy_(self.be.to_device(dh))

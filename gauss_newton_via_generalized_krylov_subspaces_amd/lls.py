@@ -112,6 +112,7 @@ class CholQR2Solver:
         self._G = self.be.zeros(kp * kp)
         self._rinv = self.be.zeros(kp * kp)
         self.quiet = False          # True: no rank-deficiency messages (GN's lstsq branch prints none)
+        self.min_norm_if_singular = False   # True: a singular Gram -> minimum-norm solution (lstsq branch)
         self.passes = 0
         self.solves = 0
         self.fallbacks = 0
@@ -283,6 +284,8 @@ class CholQR2Solver:
         self.solves += 1
         p0 = self.passes - passes_before
         conds = []
+        R = None
+        shifted = False                                  # a Gram was numerically singular
         if P is None:
             # classical CholQR2: first pass without preconditioner (T = M, no r column)
             G1 = self._gram(u, basis, k, M, None)[:k, :k]
@@ -292,6 +295,7 @@ class CholQR2Solver:
                 n = self.n_global
                 shift = 11.0 * (n * k + k * (k + 1)) * EPS * np.trace(G1)
                 P = _chol_upper(G1 + shift * np.eye(k))
+                shifted = True
         for it in range(MAX_PASSES):
             if it == 0 and G0 is not None:
                 Gp = G0
@@ -312,6 +316,7 @@ class CholQR2Solver:
                 shift = 11.0 * (n * k + k * (k + 1)) * EPS * np.trace(Gp[:k, :k])
                 P = _chol_upper(Gp[:k, :k] + shift * np.eye(k)) @ P
                 self.fallbacks += 1
+                shifted = True
                 continue
             conds.append(_cond_upper(Ry))
             if conds[-1] <= COND_ACCEPT or it == MAX_PASSES - 1:
@@ -320,6 +325,30 @@ class CholQR2Solver:
                 break
             P = Ry @ P                                   # one more pass with the improved factor
             self.fallbacks += 1
+        if R is None:
+            # no pass gave a Cholesky factor (the Gram is singular beyond the shift): minimum-norm
+            # solution from the Gram of the plain basis (below)
+            d, jdd, R = self._min_norm(u, basis, k, M, r)
+            self.history.append((k, self.passes - p0, conds + [np.inf]))
+            if pending:
+                self._tentative = (R, d)
+                return d, jdd, R
+            self._settle(R)
+            self.R_prev = None                           # no usable preconditioner: CholQR2 next time
+            return d, jdd, R
+        if self.min_norm_if_singular:
+            # the dense lstsq branch: scipy.linalg.lstsq (gelsd, cond = eps) returns the minimum-norm
+            # solution when J is rank-deficient; J = Q R, so that is R's truncated-SVD solution of
+            # R d' = z with the same cut-off (singular values <= eps sigma_max are zero)
+            U, S, Wt = np.linalg.svd(R)
+            keep = S > EPS * S[0]
+            if not np.all(keep):
+                d = -(Wt[keep].T @ ((U[:, keep].T @ z) / S[keep]))
+                jdd = float(np.sum((R @ d) ** 2))
+                self.history.append((k, self.passes - p0, conds))
+                self._settle(R)
+                self.R_prev = None                       # a singular factor does not precondition
+                return d, jdd, R
         d = -scipy.linalg.solve_triangular(R, z, lower=False)
         jdd = float(np.sum((R @ d) ** 2))
         self.history.append((k, self.passes - p0, conds))
@@ -327,6 +356,22 @@ class CholQR2Solver:
             self._tentative = (R, d)
             return d, jdd, R
         self._settle(R)
+        return d, jdd, R
+
+    def _min_norm(self, u, basis, k, M, r):
+        """No Cholesky factor at all: d = -w with w the minimum-norm solution of G w = Y^T r, G the
+        Gram of Y = J V M (one pass; M maps the stored columns to the reference basis), truncated where
+        an eigenvalue of G is below the Gram's rounding bound (the sCholQR3 shift, 11 (n k + k (k+1))
+        eps tr G).  R (rank messages, ref:gauss_newton_krylow.py:32-34) is the triangular factor of
+        diag(sqrt(lambda)) Q^T, zero on the truncated directions."""
+        G = self._gram(u, basis, k, M, r)
+        Gk, b = G[:k, :k], G[:k, k]
+        lam, Q = np.linalg.eigh(0.5 * (Gk + Gk.T))
+        keep = lam > 11.0 * (self.n_global * k + k * (k + 1)) * EPS * max(np.trace(Gk), 0.0)
+        w = Q[:, keep] @ ((Q[:, keep].T @ b) / lam[keep])
+        d = -w
+        R = np.linalg.qr(np.sqrt(np.where(keep, lam, 0.0))[:, None] * Q.T, mode="r")
+        jdd = float(w @ (Gk @ w))
         return d, jdd, R
 
     def _settle(self, R):

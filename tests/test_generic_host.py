@@ -77,3 +77,74 @@ def test_generic_args_and_dense_jacobian():
     ref = O.gauss_newton_krylow(res, np.array([2.0, 2.0]), jac)
     assert (out.nit, out.nrev, out.njev, out.success) == (ref.nit, ref.nrev, ref.njev, ref.success)
     np.testing.assert_allclose(out.x, ref.x, rtol=1e-12)
+
+
+# -- rank-deficient Jacobians (the lstsq branch must not fail when no Cholesky factor exists)
+def _rank1_problem():
+    """3 residuals, 2 parameters, J = a(s) b^T of rank 1 everywhere (s = x0 + 2 x1), nonzero residual."""
+    def res(x):
+        s = x[0] + 2 * x[1]
+        return np.array([np.exp(s) - 2.0, s * s - 0.3, 0.5 * s - 0.2])
+
+    def jac(x):
+        s = x[0] + 2 * x[1]
+        return np.outer([np.exp(s), 2 * s, 0.5], [1.0, 2.0])
+    return res, jac
+
+
+def _trace(fn, res, x0, jac, **kw):
+    rec, so = [], io.StringIO()
+    exc = None
+    try:
+        with contextlib.redirect_stdout(so):
+            out = fn(res, x0, jac, callback=lambda x, nfev, cg_iter: rec.append((x.copy(), nfev, cg_iter)), **kw)
+    except Exception as e:            # noqa: BLE001 -- the reference's exception types are compared
+        out, exc = None, e
+    return out, rec, so.getvalue(), exc
+
+
+def check_rank_deficient_gn(backend_kw):
+    """gauss_newton's lstsq branch (ref:gauss_newton.py:115-116) on a rank-1 Jacobian: scipy.linalg.lstsq
+    returns the minimum-norm step; the device CholeskyQR solve takes R's truncated-SVD solution with
+    lstsq's cut-off (lls.CholQR2Solver, min_norm_if_singular).  Bookkeeping exact, iterates 1e-10."""
+    res, jac = _rank1_problem()
+    a = _trace(gnk.gauss_newton, res, np.array([0.1, 0.1]), jac, **backend_kw)
+    b = _trace(O.gauss_newton, res, np.array([0.1, 0.1]), jac)
+    assert a[3] is None and b[3] is None
+    assert (a[0].nit, a[0].nrev, a[0].njev, a[0].success) == (b[0].nit, b[0].nrev, b[0].njev, b[0].success)
+    assert [r[1:] for r in a[1]] == [r[1:] for r in b[1]]
+    np.testing.assert_allclose(np.array([r[0] for r in a[1]]), np.array([r[0] for r in b[1]]), rtol=1e-10, atol=1e-14)
+    assert a[2] == b[2]
+    # a linear rank-1 least-squares problem (the advisor's case): the first step is lstsq's minimum-norm
+    # solution; the second step's direction is rounding noise (reference: ||d|| = 6e-17 and 100 failed
+    # halvings), so only the step and the end state are compared -- either outcome of that tie
+    A = np.array([[1.0, 2.0], [2.0, 4.0], [3.0, 6.0]])
+    y = np.array([1.0, 0.0, 2.0])
+    a = _trace(gnk.gauss_newton, lambda x: y - A @ x, np.array([1.0, 1.0]), lambda x: -A, **backend_kw)
+    b = _trace(O.gauss_newton, lambda x: y - A @ x, np.array([1.0, 1.0]), lambda x: -A)
+    np.testing.assert_allclose(a[1][0][0], b[1][0][0], rtol=0, atol=1e-14)
+    assert a[1][0][1] == b[1][0][1]
+    assert a[3] is None or type(a[3]).__name__ == type(b[3]).__name__ == "StepLengthConvergenceError"
+    np.testing.assert_allclose(a[1][-1][0], b[1][0][0], rtol=0, atol=1e-14)
+
+
+def check_rank_deficient_gnk(backend_kw):
+    """gauss_newton_krylow on a rank-1 Jacobian: the first step (k = 1) matches; at k = 2, J V has rank 1 and
+    the reference's QR prints 'A is rank deficient' (ref:gauss_newton_krylow.py:32-34) before its
+    rounding-noise step -- the message and the SpansEntireSpace warning must come out the same way."""
+    res, jac = _rank1_problem()
+    a = _trace(gnk.gauss_newton_krylow, res, np.array([0.1, 0.1]), jac, **backend_kw)
+    b = _trace(O.gauss_newton_krylow, res, np.array([0.1, 0.1]), jac)
+    np.testing.assert_allclose(a[1][0][0], b[1][0][0], rtol=1e-12)
+    assert a[1][0][1] == b[1][0][1]
+    head = ("A is rank deficient\nWarning: The genearlized krylow subspace is now identical to the whole "
+            "parameter space at iteration = 2\n")
+    assert a[2].startswith(head) and b[2].startswith(head)
+
+
+def test_rank_deficient_dense_gn():
+    check_rank_deficient_gn(dict(_backend=NumpyBackend()))
+
+
+def test_rank_deficient_gnk():
+    check_rank_deficient_gnk(dict(_backend=NumpyBackend()))

@@ -171,3 +171,13 @@ def test_gpu_gn_dense_jacobian_lstsq_branch(p, x0):
     assert (a.nit, a.nrev, a.njev, a.success) == (b.nit, b.nrev, b.njev, b.success)
     assert [r[1:] for r in ra] == [r[1:] for r in rb]
     np.testing.assert_allclose([r[0] for r in ra], [r[0] for r in rb], rtol=1e-10)
+
+
+def test_rank_deficient_dense_gn_gpu():
+    from tests.test_generic_host import check_rank_deficient_gn
+    check_rank_deficient_gn({})
+
+
+def test_rank_deficient_gnk_gpu():
+    from tests.test_generic_host import check_rank_deficient_gnk
+    check_rank_deficient_gnk({})

@@ -11,7 +11,7 @@ if [[ $STEP == all || $STEP == test ]]; then
   run build && timeout -k 10 300 python -c "import __graft_entry__ as g; g.build()" > gpurun_out/build.log 2>&1 &&
   run probe && timeout -k 10 120 python tools/probe.py > gpurun_out/probe.json 2> gpurun_out/probe.err &&
   run smoke && timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 &&
-  run pytest && timeout -k 10 900 python -m pytest tests -m gpu -x -q > gpurun_out/pytest_gpu.log 2>&1 || exit $?
+  run pytest && timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1 || exit $?
 fi
 if [[ $STEP == all || $STEP == dist ]]; then
   # several ranks on this one GPU (gloo, host-staged collectives) vs the single-rank solve
