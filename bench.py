@@ -44,6 +44,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--repeats", type=int, default=3, help="timed regions of --steps each; value = median")
     ap.add_argument("--grid", type=int, default=8192, help="interior points per side N")
     ap.add_argument("--restart", type=int, default=20)
     ap.add_argument("--version", default="res_old")
@@ -51,16 +52,6 @@ def parse():
     ap.add_argument("--jvp-reps", type=int, default=20)
     ap.add_argument("--cg-iters", type=int, default=200, help="CGLS iterations of the C3 line (0 = skip)")
     return ap.parse_args()
-
-
-def bratu_inputs(N, seed=42):
-    """u_true (Fortran-order flatten == jx*N + iy) and u0 of ref:bratu_pde_test.py:34-36."""
-    from gauss_newton_via_generalized_krylov_subspaces_amd import BratuPdeProblem
-    prob = BratuPdeProblem(N + 1, 5, 10)
-    u_true = prob.u_true
-    np.random.seed(seed)
-    u0 = u_true + 0.1 * np.random.normal(loc=0, scale=1, size=len(u_true))
-    return prob, u_true, u0
 
 
 def step_bytes(n, k, a, passes=1.0, fused=False, pending=True):
@@ -79,67 +70,119 @@ def step_bytes(n, k, a, passes=1.0, fused=False, pending=True):
     return 8.0 * n * (passes * (k + 2) + trials + update)
 
 
-def cpu_baseline(N, seconds, version, restart):
-    """The CPU oracle (NumPy restatement of the reference, oracle/) on this host:
-    setup excluded, GNK outer iterations until `seconds` of work (>= 1)."""
+def cpu_baseline(N, seconds, version, restart, c2_steps=20, grid_c2=1024):
+    """The CPU oracle (NumPy restatement of the reference, oracle/) on this host, BASELINE.md's plan:
+      * headline: GNK on the same N^2 workload, outer iterations until ``seconds`` of work (setup
+        excluded; k = 1..it), with the per-component split (J V products, least squares, Armijo
+        trials, basis update);
+      * C2: one whole restart cycle (``c2_steps`` iterations, k = 1..20) at 1024^2;
+      * the single-vector JVP at N^2 (24 n algorithmic bytes) and the CGLS iteration (Jacobi)."""
     from oracle import gnk_oracle as O
     threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
-    prob, y, u0 = O.bratu_workload(N)
-    res, jac = prob.make_res(y), prob.make_jac()
-    times = []
+    comp = {"jv_products": 0.0, "least_squares": 0.0, "armijo_trials": 0.0, "basis_update": 0.0}
+    orig = (O.linear_least_squares, O.armijo_goldstein, O.KrylovBasis.update, O.BratuJacobian.__matmul__)
+
+    def timed(key, fn, pred=None):
+        def w(*a, **k):
+            t = time.perf_counter()
+            try:
+                return fn(*a, **k)
+            finally:
+                if pred is None or pred(*a):
+                    comp[key] += time.perf_counter() - t
+        return w
 
     class Stop(Exception):
         pass
 
-    t_last = [None]
+    def run(prob, y, u0, budget_s, max_steps):
+        times, t_last = [], [time.perf_counter()]
 
-    def cb(x, nfev, cg_iter):
-        now = time.perf_counter()
-        times.append(now - t_last[0])
-        t_last[0] = now
-        if sum(times) >= seconds:
-            raise Stop
+        def cb(x, nfev, cg_iter):
+            now = time.perf_counter()
+            times.append(now - t_last[0])
+            t_last[0] = now
+            if sum(times) >= budget_s or len(times) >= max_steps:
+                raise Stop
+        t_last[0] = time.perf_counter()
+        with contextlib.redirect_stdout(io.StringIO()):
+            try:
+                O.gauss_newton_krylow(prob.make_res(y), u0, prob.make_jac(), krylow_restart=restart,
+                                      max_iter=10 ** 6, callback=cb, version=version)
+            except Stop:
+                pass
+        return times
 
-    t_last[0] = time.perf_counter()
-    with contextlib.redirect_stdout(io.StringIO()):
-        try:
-            O.gauss_newton_krylow(res, u0, jac, krylow_restart=restart, max_iter=10 ** 6, callback=cb, version=version)
-        except Stop:
-            pass
-    it = len(times)
-    total = sum(times)
-    return {"value": it / total, "unit": "outer_iters/s", "cores": threads, "kind": "port",
-            "sample": f"oracle/gnk_oracle.py GNK on the same {N}^2 workload, first {it} outer iterations "
-                      f"(basis k=1..{it}; {total:.1f} s, setup excluded), OPENBLAS threads={threads}"}
+    prob, y, u0 = O.bratu_workload(N)
+    O.linear_least_squares = timed("least_squares", orig[0])
+    O.armijo_goldstein = timed("armijo_trials", orig[1])
+    O.KrylovBasis.update = timed("basis_update", orig[2])
+    O.BratuJacobian.__matmul__ = timed("jv_products", orig[3], lambda self, V: np.ndim(V) == 2)
+    try:
+        times = run(prob, y, u0, seconds, 10 ** 6)
+    finally:
+        O.linear_least_squares, O.armijo_goldstein, O.KrylovBasis.update, O.BratuJacobian.__matmul__ = orig
+    it, total = len(times), sum(times)
+    comp["other"] = max(total - sum(comp.values()), 0.0)
+    out = {"value": it / total, "unit": "outer_iters/s", "cores": threads, "kind": "port",
+           "sample": f"oracle/gnk_oracle.py GNK on the same {N}^2 workload, first {it} outer iterations "
+                     f"(basis k=1..{it}; {total:.1f} s, setup excluded), OPENBLAS threads={threads}",
+           "components_s": {k: round(v, 3) for k, v in comp.items()}}
+    # single-vector JVP and one CGLS iteration at N^2 (oracle stencils; A = -J(u0), Jacobi)
+    J = prob.make_jac()(u0)
+    v = np.random.default_rng(1).standard_normal(N * N)
+    jt = []
+    for _ in range(3):
+        t = time.perf_counter()
+        J @ v
+        jt.append(time.perf_counter() - t)
+    jms = float(np.median(jt))
+    out["jvp"] = {"ms": 1e3 * jms, "GBs": 24.0 * N * N / jms / 1e9, "note": "oracle stencil J @ v, 24 n bytes"}
+    A = -1 * J
+    b = A.T @ prob.make_res(y)(u0)
+    dinv = 1 / A.diag_ata()
+    ct = []
+    O.scipy_cg(lambda p: A.T @ (A @ p), b, psolve=lambda r: dinv * r, rtol=1e-8, maxiter=3,
+               callback=lambda x: ct.append(time.perf_counter()))
+    out["cg"] = {"ms_per_iter": 1e3 * float(np.mean(np.diff(ct))) if len(ct) > 1 else None,
+                 "note": f"oracle scipy-cg recurrence on A^T A at {N}^2, Jacobi, rtol 1e-8"}
+    del prob, y, u0, J, v, A, b, dinv
+    # C2: one restart cycle at 1024^2, k = 1..20
+    p2, y2, u2 = O.bratu_workload(grid_c2)
+    t2 = run(p2, y2, u2, 10 ** 9, c2_steps)
+    out["c2"] = {"value": len(t2) / sum(t2), "unit": "outer_iters/s", "grid": grid_c2, "steps": len(t2),
+                 "sample": f"GNK restart {restart}, the first restart cycle (k = 1..{len(t2)}), setup excluded"}
+    return out
 
 
 CG_BYTES_PER_ITER = 112     # SURVEY §8d model, bytes per unknown: p update 24, J^T J p 24, x/r/z update 64
                             # (the fused iteration moves 96: step matvec 56 + r/z update 40)
 
 
-def gn_cg_line(args, prob, u_true, u0, comm, device, world):
-    """CGLS of the first Gauss-Newton step at cg_rtol = 1e-8 (Jacobi preconditioner,
-    ref:gauss_newton.py:50-58), capped at --cg-iters iterations (a full solve at 8192^2 takes far
-    more).  Reports CG iterations/s of the whole job and the fused J^T J p kernel's per-launch rate."""
+def gn_cg_line(args, prob, u0, y, comm, device, world, backend):
+    """CGLS of the first Gauss-Newton step (A = -J(u0), right-hand side res(u0),
+    ref:gauss_newton.py:112-114) at cg_rtol = 1e-8 (Jacobi preconditioner, :50-58), capped at
+    --cg-iters iterations (a full solve at 8192^2 takes far more).  Reports CG iterations/s of the
+    whole job and the fused J^T J p kernel's per-launch rate."""
     from gauss_newton_via_generalized_krylov_subspaces_amd import _native
-    from gauss_newton_via_generalized_krylov_subspaces_amd._device import SingleRankOperator
     from gauss_newton_via_generalized_krylov_subspaces_amd.gauss_newton import BratuGNOps, DeviceCG
     N = args.grid
     n = N * N
-    y = SingleRankOperator(prob, device).forward(u_true)
-    ops = BratuGNOps(prob, y, comm, device)
-    del y
+    ops = BratuGNOps(prob, y, comm, device, backend)
     cg = DeviceCG(ops)
     u = ops.load(u0)
+    r0 = ops.vec()
+    ops.residual(u, r0)                                                        # res(u0)
+    comm.halo(r0, N, ops.dev.slab.nrows)
     be = ops.be
-    cg.solve(u, ops.y, cg_rtol=1e-8, preconditioner=True, maxiter=5)          # warm-up
-    cg.solve(u, ops.y, cg_rtol=1e-8, preconditioner=True, maxiter=5, variant="single_reduction")
+    cg.solve(u, r0, cg_rtol=1e-8, preconditioner=True, maxiter=5)             # warm-up
+    cg.solve(u, r0, cg_rtol=1e-8, preconditioner=True, maxiter=5, variant="single_reduction")
     cap = args.cg_iters + 8
     be.timer_start(_native.TIMER_CG_MATVEC, cap)
     comm.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    _, iters = cg.solve(u, ops.y, cg_rtol=1e-8, preconditioner=True, maxiter=args.cg_iters)
+    _, iters = cg.solve(u, r0, cg_rtol=1e-8, preconditioner=True, maxiter=args.cg_iters)
     torch.cuda.synchronize()
     comm.barrier()
     elapsed = time.perf_counter() - t0
@@ -152,7 +195,7 @@ def gn_cg_line(args, prob, u_true, u0, comm, device, world):
     comm.barrier()
     torch.cuda.synchronize()
     t1 = time.perf_counter()
-    _, iters_sr = cg.solve(u, ops.y, cg_rtol=1e-8, preconditioner=True, maxiter=args.cg_iters,
+    _, iters_sr = cg.solve(u, r0, cg_rtol=1e-8, preconditioner=True, maxiter=args.cg_iters,
                            variant="single_reduction")
     torch.cuda.synchronize()
     comm.barrier()
@@ -185,11 +228,13 @@ def prewarm(args, comm, device):
     256^2 grid (same dispatch: N % 128 == 0, same k range and version) makes every kernel variant
     of the timed steps resident before the clock starts."""
     import gauss_newton_via_generalized_krylov_subspaces_amd as gnk
-    from gauss_newton_via_generalized_krylov_subspaces_amd._device import SingleRankOperator
-    prob, u_true, u0 = bratu_inputs(256)
-    y = SingleRankOperator(prob, device).forward(u_true)
+    from gauss_newton_via_generalized_krylov_subspaces_amd._device import BratuDevice
+    from gauss_newton_via_generalized_krylov_subspaces_amd.inputs import slab_inputs
+    prob = gnk.BratuPdeProblem(256 + 1, 5, 10)
+    stage = BratuDevice(prob, comm, device)
+    u0, y, _ = slab_inputs(stage)
     s = gnk.GNKSolver(prob, y, krylow_restart=args.restart, tol=1e-8, max_iter=10 ** 9, version=args.version,
-                      comm=comm, device=device)
+                      comm=comm, device=device, backend=stage.backend)
     s.setup(u0)
     with contextlib.redirect_stdout(io.StringIO()):
         for _ in range(args.restart + 2):
@@ -198,16 +243,47 @@ def prewarm(args, comm, device):
     torch.cuda.synchronize()
 
 
-def pmc_traffic(config_key):
-    """HBM bytes per Gram launch from the committed rocprofv3 PMC summary, if one matches."""
-    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "pmc_summary.json")), reverse=True):
+def c2_gpu(args, comm, device, grid=1024):
+    """GPU outer iterations/s on C2 (1024^2, restart 20): the second restart cycle after setup (the
+    first warms the kernels), for the like-for-like comparison with the CPU's C2 cycle."""
+    import gauss_newton_via_generalized_krylov_subspaces_amd as gnk
+    from gauss_newton_via_generalized_krylov_subspaces_amd._device import BratuDevice
+    from gauss_newton_via_generalized_krylov_subspaces_amd.inputs import slab_inputs
+    prob = gnk.BratuPdeProblem(grid + 1, 5, 10)
+    stage = BratuDevice(prob, comm, device)
+    u0, y, _ = slab_inputs(stage)
+    s = gnk.GNKSolver(prob, y, krylow_restart=args.restart, tol=1e-8, max_iter=10 ** 9, version=args.version,
+                      comm=comm, device=device, backend=stage.backend)
+    s.setup(u0)
+    with contextlib.redirect_stdout(io.StringIO()):
+        for _ in range(args.restart):
+            s.step()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.restart):
+            s.step()
+        torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    return {"value": args.restart / el, "unit": "outer_iters/s", "steps": args.restart,
+            "note": "GPU, second restart cycle (k = 1..20) of the same C2 run"}
+
+
+def pmc_traffic(config_key, window):
+    """HBM bytes per Gram launch from a committed rocprofv3 PMC summary (tools/pmc_summary.py) of this
+    configuration AND this timed window: same warmup / steps / repeats and the same algorithmic bytes
+    per launch (so the same basis sizes).  Otherwise (None, None): the line reports traffic null."""
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "pmc_summary*.json")), reverse=True):
         try:
             with open(path) as f:
                 d = json.load(f)
-            if d.get("config") == config_key and d.get("traffic_bytes_per_launch"):
-                return d["traffic_bytes_per_launch"], os.path.relpath(path, ROOT)
         except (OSError, ValueError):
             continue
+        w = d.get("window") or {}
+        if (d.get("config") == config_key and d.get("traffic_bytes_per_launch")
+                and all(w.get(k) == window[k] for k in ("warmup", "steps", "repeats", "gram_launches"))
+                and abs(w.get("algorithmic_bytes_per_launch", 0.0) - window["algorithmic_bytes_per_launch"])
+                <= 1e-9 * window["algorithmic_bytes_per_launch"]):
+            return d["traffic_bytes_per_launch"], os.path.relpath(path, ROOT)
     return None, None
 
 
@@ -233,45 +309,63 @@ def main():
 
     import gauss_newton_via_generalized_krylov_subspaces_amd as gnk
     from gauss_newton_via_generalized_krylov_subspaces_amd import _native
-    from gauss_newton_via_generalized_krylov_subspaces_amd._device import SingleRankOperator
+    from gauss_newton_via_generalized_krylov_subspaces_amd._device import BratuDevice
+    from gauss_newton_via_generalized_krylov_subspaces_amd.inputs import slab_inputs
     from gauss_newton_via_generalized_krylov_subspaces_amd.slab import Comm
 
     N = args.grid
     n = N * N
     comm = Comm()
     prewarm(args, comm, device)
-    prob, u_true, u0 = bratu_inputs(N)
-    y = SingleRankOperator(prob, device).forward(u_true)            # y = F(u_true) (ref:bratu_pde_test.py:29)
+    prob = gnk.BratuPdeProblem(N + 1, 5, 10)
+    # this rank's slabs of u0 and y = F(u_true) (ref:bratu_pde_test.py:22-36), built per rank: no
+    # whole-grid vector on any host or GPU (inputs.py)
+    stage = BratuDevice(prob, comm, device)
+    u0, y, _ = slab_inputs(stage)
     solver = gnk.GNKSolver(prob, y, krylow_restart=args.restart, tol=1e-8, max_iter=10 ** 9,
-                           version=args.version, comm=comm, device=device)
-    del y
+                           version=args.version, comm=comm, device=device, backend=stage.backend)
     solver.setup(u0)
     be = solver.be
+    warm_s = []                 # per-step times of the warm-up steps (k = 1..warmup), synchronised each
     with contextlib.redirect_stdout(io.StringIO()):
         for _ in range(args.warmup):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
             solver.step()
+            torch.cuda.synchronize()
+            warm_s.append(time.perf_counter() - t0)
+    # --repeats timed regions of exactly --steps outer iterations each (with the default 20 steps one
+    # region is one whole restart cycle, k = 1..20); value = the median region's rate
     cap = 4 * (args.steps + 1)
-    be.timer_start(_native.TIMER_GRAM, cap)
     k_trace0 = len(solver.trace)
     passes0 = solver.lls.passes
-    comm.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    with contextlib.redirect_stdout(io.StringIO()):
-        for _ in range(args.steps):
-            if solver.step():
-                break
-    torch.cuda.synchronize()
-    comm.barrier()
-    elapsed = time.perf_counter() - t0
-    steps_done = len(solver.trace) - k_trace0
-    launches = be.timer_collect(cap)
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=device)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = t.item()
+    gram_offset = solver.lls.passes            # bench-grid Gram launches before the first timed region
+    regions, launches = [], []
+    for _ in range(args.repeats):
+        be.timer_start(_native.TIMER_GRAM, cap)
+        tr0 = len(solver.trace)
+        comm.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        with contextlib.redirect_stdout(io.StringIO()):
+            for _ in range(args.steps):
+                if solver.step():
+                    break
+        torch.cuda.synchronize()
+        comm.barrier()
+        el = time.perf_counter() - t0
+        launches += be.timer_collect(cap)
+        if world > 1:
+            t = torch.tensor([el], dtype=torch.float64, device=device)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            el = t.item()
+        regions.append((len(solver.trace) - tr0, el))
+    rates = [st / el for st, el in regions]
+    imed = int(np.argsort(rates)[len(rates) // 2])
+    steps_done, elapsed = regions[imed]
+    elapsed_all = sum(el for _, el in regions)
 
-    # whole-step algorithmic bytes (global grid) over the timed steps
+    # whole-step algorithmic bytes (global grid) over all timed steps
     tr = solver.trace[k_trace0:]
     passes = solver.lls.passes - passes0
     ppi = passes / max(len(tr), 1)
@@ -284,7 +378,14 @@ def main():
     g_avg_ms = float(np.mean(g_ms)) if g_ms else float("nan")
     g_avg_bytes = float(np.mean(g_by)) if g_by else float("nan")
     g_gbs = g_avg_bytes / (g_avg_ms * 1e-3) / 1e9 if g_ms else float("nan")
-    gram_share = sum(g_ms) * 1e-3 / elapsed if g_ms else float("nan")
+    window = {"warmup": args.warmup, "steps": args.steps, "repeats": args.repeats, "gram_launch_offset": gram_offset,
+              "gram_launches": len(g_ms), "algorithmic_bytes_per_launch": g_avg_bytes}
+    if os.environ.get("GNK_BENCH_WINDOW_OUT") and rank == 0:
+        # the Gram launches of the timed regions, for tools/pmc_summary.py (the PMC pass runs this same
+        # command under rocprofv3 and keeps exactly these launches)
+        with open(os.environ["GNK_BENCH_WINDOW_OUT"], "w") as f:
+            json.dump({**window, "grid": N, "launch_bytes": g_by}, f)
+    gram_share = sum(g_ms) * 1e-3 / elapsed_all if g_ms else float("nan")
     # per basis size: columns = bytes / (8 n_rank) - 2 (V, u, r); kernel as gnk_gram dispatches a pass
     # with P^-1 and r: VALU k <= 9, staged k <= 20 (N % 128 == 0), chunked k_gram_w up to 47 columns
     # (+ r), the prefetching k_gram_wp up to 63, the pair-split k_gram beyond
@@ -322,10 +423,10 @@ def main():
     spec_stats = dict(solver.spec_stats)
     del solver, v, out, uu                      # free the GNK state (the basis) before the CG line
     torch.cuda.empty_cache()
-    cg_line = gn_cg_line(args, prob, u_true, u0, comm, device, world) if args.cg_iters > 0 else None
+    cg_line = gn_cg_line(args, prob, u0, y, comm, device, world, stage.backend) if args.cg_iters > 0 else None
 
     config_key = f"bratu{N}_gnk_restart{args.restart}_{args.version}_ranks{world}"
-    traffic, traffic_src = pmc_traffic(config_key)
+    traffic, traffic_src = pmc_traffic(config_key, window)
     result = {
         "metric": "GN-Krylov outer iters/sec + JVP HBM GB/s, Bratu 8192² fp64, 1/2/4/8 GPUs",
         "value": steps_done / elapsed,
@@ -349,11 +450,13 @@ def main():
                                "k_gram_s: staged fp64 MFMA, k > 9)", "bound": "hbm",
                      "achieved": g_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": g_gbs / HBM_PEAK_GBS,
                      "traffic": traffic, "traffic_source": traffic_src,
+                     "traffic_over_algorithmic": (traffic / g_avg_bytes) if traffic else None, "window": window,
                      "avg_launch_ms": g_avg_ms, "algorithmic_bytes_per_launch": g_avg_bytes,
                      "launches": len(g_ms), "share_of_step_time": gram_share, "by_k": gram_by_k},
         "jvp": {"kernel": "k_jvp (J(u) v, 5-point stencil)", "grid": N, "median_ms": j_ms, "GBs": j_gbs,
                 "frac_of_peak": j_gbs / HBM_PEAK_GBS, "algorithmic_bytes": jl[0][1]},
-        "step_algorithmic_GBs": total_bytes / elapsed / 1e9,
+        "repeats": [{"steps": st, "seconds": el, "outer_iters_per_s": st / el} for st, el in regions],
+        "step_algorithmic_GBs": total_bytes / elapsed_all / 1e9,
         "gram_passes_per_step": ppi,
         "speculated_solves": spec_stats,
     }
@@ -361,7 +464,15 @@ def main():
         result["gn_cg"] = cg_line
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
         try:
-            result["cpu_baseline"] = cpu_baseline(N, args.cpu_seconds, args.version, args.restart)
+            cb_ = cpu_baseline(N, args.cpu_seconds, args.version, args.restart)
+            # the GPU on the CPU sample's own windows: the first outer iterations of this workload
+            # (the warm-up steps, k = 1..) and the C2 restart cycle at 1024^2
+            kk = min(len(warm_s), int(cb_["sample"].split("first ")[1].split(" ")[0]))
+            if kk:
+                cb_["gpu_same_window"] = {"value": kk / sum(warm_s[:kk]), "unit": "outer_iters/s", "steps": kk,
+                                          "note": "GPU, first steps of the same workload, each synchronised"}
+            cb_["c2"]["gpu"] = c2_gpu(args, comm, device)
+            result["cpu_baseline"] = cb_
         except Exception as e:  # report, never hide
             result["cpu_baseline"] = {"value": None, "error": repr(e)}
     if rank == 0:

@@ -14,7 +14,7 @@ from .gauss_newton import GNSolver, cg_least_squares, gauss_newton
 from .gauss_newton_krylow import GNKSolver, gauss_newton_krylow
 from .krylow import GeneralizedKrylowSubspaceBreakdown, GeneralizedKrylowSubspaceSpansEntireSpace
 from .regression_result import RegressionResult
-from .slab import Comm, row_partition
+from .slab import Comm, SlabVector, row_partition
 
 __all__ = [
     "gauss_newton_krylow", "gauss_newton", "cg_least_squares", "BratuPdeProblem", "BratuJacobian",

@@ -227,13 +227,31 @@ class Comm:
                 vec[own_end:own_end + g].copy_(host[own_end:own_end + g])
 
     def gather_rows(self, owned: torch.Tensor, N: int) -> np.ndarray:
-        """All ranks' owned rows -> the full host vector (variable slab sizes)."""
-        host = owned.detach().to("cpu").numpy()
+        """All ranks' owned rows -> the full host vector (variable slab sizes): one tensor
+        all-gather of the owned rows, each rank's part padded to the largest slab."""
         if self.world == 1:
-            return host.copy()
-        parts = [None] * self.world
-        dist.all_gather_object(parts, host, group=self.group)
-        return np.concatenate(parts)
+            return owned.detach().to("cpu").numpy().copy()
+        sizes = [row_partition(N, self.world, p)[1] * N for p in range(self.world)]
+        big = max(sizes)
+        dev = torch.device("cpu") if self.stage else owned.device
+        pad = torch.zeros(big, dtype=torch.float64, device=dev)
+        pad[:owned.numel()] = owned.detach().reshape(-1)
+        buf = torch.empty(self.world * big, dtype=torch.float64, device=dev)
+        dist.all_gather_into_tensor(buf, pad, group=self.group)
+        del pad
+        parts = buf.view(self.world, big)
+        return torch.cat([parts[p, :sizes[p]] for p in range(self.world)]).to("cpu").numpy()
+
+
+class SlabVector:
+    """A vector already distributed as this rank's slab (owned rows + GHOST rows each side, ghost
+    rows valid): accepted wherever a full-grid host vector is, without any whole-grid copy
+    (``inputs.slab_inputs`` builds the bench workload this way)."""
+
+    __slots__ = ("data",)
+
+    def __init__(self, data: torch.Tensor):
+        self.data = data
 
 
 class _ReadHandle:
@@ -258,7 +276,14 @@ class Slab:
         self.n_global = self.N * self.N
 
     def from_host(self, full, backend) -> torch.Tensor:
-        """Slab vector (owned + up to GHOST rows each side) from a full-grid vector."""
+        """Slab vector (owned + up to GHOST rows each side) from a full-grid vector (or a copy of a
+        SlabVector of this geometry)."""
+        if isinstance(full, SlabVector):
+            if full.data.numel() != self.length:
+                raise ValueError(f"SlabVector of length {full.data.numel()}, this rank's slab has {self.length}")
+            out = backend.zeros(self.length)
+            out.copy_(full.data.reshape(-1))
+            return out
         full = torch.as_tensor(np.asarray(full, dtype=np.float64) if not torch.is_tensor(full) else full)
         out = backend.zeros(self.length)
         lo = max(self.row0 - GHOST, 0)

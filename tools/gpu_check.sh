@@ -15,8 +15,8 @@ if [[ $STEP == all || $STEP == test ]]; then
 fi
 if [[ $STEP == all || $STEP == dist ]]; then
   # several ranks on this one GPU (gloo, host-staged collectives) vs the single-rank solve
-  run dist && timeout -k 10 600 torchrun --standalone --local-addr 127.0.0.1 --nproc-per-node 2 tools/dist_rehearsal.py --grid 256 > gpurun_out/dist2.json 2> gpurun_out/dist2.err &&
-  timeout -k 10 600 torchrun --standalone --local-addr 127.0.0.1 --nproc-per-node 3 tools/dist_rehearsal.py --grid 384 > gpurun_out/dist3.json 2> gpurun_out/dist3.err || exit $?
+  run dist && timeout -k 10 600 torchrun --standalone --local-addr 127.0.0.1 --nproc-per-node 2 tests/multislab_worker.py --grid 256 --out gpurun_out/dist2.json > gpurun_out/dist2.log 2>&1 &&
+  timeout -k 10 600 torchrun --standalone --local-addr 127.0.0.1 --nproc-per-node 3 tests/multislab_worker.py --grid 384 --out gpurun_out/dist3.json > gpurun_out/dist3.log 2>&1 || exit $?
 fi
 if [[ $STEP == all || $STEP == bench ]]; then
   run bench && timeout -k 10 600 python bench.py > gpurun_out/bench.json 2> gpurun_out/bench.err || exit $?
