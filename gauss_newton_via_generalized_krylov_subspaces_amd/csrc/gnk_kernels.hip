@@ -141,6 +141,59 @@ __device__ __forceinline__ void block_sum_store(double (&v)[NV], int n, double* 
   }
 }
 
+// ---- compensated sums (Ogita-Rump-Oishi Sum2 / Dot2): a value is carried as s + c, every addition
+// keeps its rounding error (TwoSum) and every product its FMA-exact error (TwoProduct), so a dot
+// product is as accurate as if accumulated in twice the working precision and rounded once.  Used
+// for the CG scalars (p.q, r.r, r.z, ||b||), whose exact rounding decides scipy's stopping test
+// ||r|| < rtol ||b|| (ref:gauss_newton.py:36-58 via scipy iterative.py:397): the reference's own
+// OpenBLAS dot is within a few ulps of the exactly rounded value, and so is this one, whatever the
+// block / wave / rank partition.  (-ffp-contract=off keeps TwoSum intact.)
+__device__ __forceinline__ void comp_add(double& s, double& c, double v) {
+  const double t = s + v;
+  const double bp = t - s;
+  c += (s - (t - bp)) + (v - bp);
+  s = t;
+}
+__device__ __forceinline__ void comp_dot(double& s, double& c, double a, double b) {
+  const double pr = a * b;
+  c += fma(a, b, -pr);
+  comp_add(s, c, pr);
+}
+__device__ __forceinline__ void comp_merge(double& s, double& c, double s2, double c2) {
+  comp_add(s, c, s2);
+  c += c2;
+}
+__device__ __forceinline__ void wave_sum2(double& s, double& c) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const double s2 = __shfl_xor(s, o), c2 = __shfl_xor(c, o);
+    comp_merge(s, c, s2, c2);
+  }
+}
+// block-wide compensated sums of n per-thread (s, c) pairs -> out[2j] = s_j, out[2j + 1] = c_j
+template <int NV>
+__device__ __forceinline__ void block_sum2_store(double (&s)[NV], double (&c)[NV], int n, double* out, double* sh) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+  for (int j = 0; j < NV; ++j) {
+    if (j < n) {
+      wave_sum2(s[j], c[j]);
+      if (lane == 0) {
+        sh[(wave * NV + j) * 2] = s[j];
+        sh[(wave * NV + j) * 2 + 1] = c[j];
+      }
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x < n) {
+    const int j = threadIdx.x;
+    double a = sh[2 * j], b = sh[2 * j + 1];
+    for (int w = 1; w < BLOCK / 64; ++w) comp_merge(a, b, sh[(w * NV + j) * 2], sh[(w * NV + j) * 2 + 1]);
+    out[2 * j] = a;
+    out[2 * j + 1] = b;
+  }
+}
+
 // ---------------------------------------------------------------- row-tiled launch geometry
 // grid.x covers one row (VEC elements per thread), grid.y strides over rows.
 struct RowLaunch {
@@ -611,26 +664,27 @@ __global__ __launch_bounds__(BLOCK) void k_cgs(const double* __restrict__ V, int
 template <int VEC>
 __global__ __launch_bounds__(BLOCK) void k_stats(const double* __restrict__ x, Geo geo, int64_t lr0, int64_t nlr,
                                                  double* __restrict__ partial) {
-  __shared__ double sh[BLOCK / 64][2];
-  double ss = 0.0, mx = 0.0;
+  __shared__ double sh[BLOCK / 64][3];
+  double ss = 0.0, sc = 0.0, mx = 0.0;
   ROW_LOOP_BEGIN(VEC)
   for (int q = 0; q < VEC && iy + q < N; ++q) {
     const double xi = x[li + q];
-    ss += xi * xi;
+    comp_dot(ss, sc, xi, xi);
     mx = nan_max(mx, fabs(xi));
   }
   ROW_LOOP_END
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  ss = wave_sum(ss);
+  wave_sum2(ss, sc);
   mx = wave_max(mx);
-  if (lane == 0) { sh[wave][0] = ss; sh[wave][1] = mx; }
+  if (lane == 0) { sh[wave][0] = ss; sh[wave][1] = sc; sh[wave][2] = mx; }
   __syncthreads();
   if (threadIdx.x == 0) {
-    double a = sh[0][0], b = sh[0][1];
-    for (int w = 1; w < BLOCK / 64; ++w) { a += sh[w][0]; b = nan_max(b, sh[w][1]); }
+    double a = sh[0][0], ac = sh[0][1], b = sh[0][2];
+    for (int w = 1; w < BLOCK / 64; ++w) { comp_merge(a, ac, sh[w][0], sh[w][1]); b = nan_max(b, sh[w][2]); }
     const size_t blk = blockIdx.y * gridDim.x + blockIdx.x;
-    partial[2 * blk] = a;
-    partial[2 * blk + 1] = b;
+    partial[3 * blk] = a;                           // {sum x^2 as s + c, max |x|}
+    partial[3 * blk + 1] = ac;
+    partial[3 * blk + 2] = b;
   }
 }
 
@@ -727,8 +781,8 @@ template <int VEC>
 __global__ __launch_bounds__(BLOCK) void k_cg_matvec(const double* __restrict__ d, const double* __restrict__ p,
                                                      double* __restrict__ q, Geo geo, Coef c, int64_t lr0,
                                                      int64_t nlr, double* __restrict__ partial) {
-  __shared__ double sh[BLOCK / 64];
-  double acc[1] = {0.0};
+  __shared__ double sh[BLOCK / 64 * 2];
+  double acc[1] = {0.0}, accc[1] = {0.0};
   ROW_LOOP_BEGIN(VEC)
   const int64_t gr = geo.row0 + (lr - G);
 #pragma unroll
@@ -744,10 +798,10 @@ __global__ __launch_bounds__(BLOCK) void k_cg_matvec(const double* __restrict__ 
     const double ts = tj(c, d, p, i + N, gr + 1, yy, N);
     const double qi = vjp_pt(c, d[i], tn, tw, hw, tc, te, he, ts);
     q[i] = qi;
-    acc[0] += p[i] * qi;
+    comp_dot(acc[0], accc[0], p[i], qi);
   }
   ROW_LOOP_END
-  block_sum_store<1>(acc, 1, partial + (blockIdx.y * gridDim.x + blockIdx.x), sh);
+  block_sum2_store<1>(acc, accc, 1, partial + 2 * (blockIdx.y * gridDim.x + blockIdx.x), sh);
 }
 
 // q = J^T (J p) by row marching, and the partial p.q.  One wave walks a 128-point strip (two points
@@ -773,7 +827,7 @@ __global__ __launch_bounds__(BLOCK) void k_cg_matvec_m(const double* __restrict_
                                                        double* __restrict__ partial, const double* __restrict__ z,
                                                        double* __restrict__ p, double beta, int first,
                                                        double* __restrict__ x, double xalpha) {
-  __shared__ double sh[BLOCK / 64];
+  __shared__ double sh[BLOCK / 64 * 2];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int64_t N = geo.N;
   const int nbc = int((N + 4 * CGM_SW - 1) / (4 * CGM_SW));
@@ -789,7 +843,7 @@ __global__ __launch_bounds__(BLOCK) void k_cg_matvec_m(const double* __restrict_
   // edge pairs: lane 0 -> columns col0-2, col0-1; lane 63 -> col0+128, col0+129
   const bool ex = (lane == 0 && col0 > 0) || (lane == 63 && col0 + CGM_SW < N);
   const int64_t exo = lane == 0 ? -2 : 2;
-  double acc[1] = {0.0};
+  double acc[1] = {0.0}, accc[1] = {0.0};
   auto ld = [&](const double* base, int64_t xr) -> d2 {   // xr: owned-row index (may be -2 .. nrows+1)
     return valid ? *reinterpret_cast<const d2*>(base + (G + xr) * N + y0) : d2{0.0, 0.0};
   };
@@ -863,8 +917,8 @@ __global__ __launch_bounds__(BLOCK) void k_cg_matvec_m(const double* __restrict_
         qo.x = vjp_pt(c, dB.x, tn.x, tw, hw0, tc.x, tc.y, true, ts.x);
         qo.y = vjp_pt(c, dB.y, tn.y, tc.x, true, tc.y, tE, he1, ts.y);
         *reinterpret_cast<d2*>(q + (G + xs) * N + y0) = qo;
-        acc[0] += pC.x * qo.x;
-        acc[0] += pC.y * qo.y;
+        comp_dot(acc[0], accc[0], pC.x, qo.x);
+        comp_dot(acc[0], accc[0], pC.y, qo.y);
       }
       tn = tc;
       tc = ts;
@@ -874,7 +928,7 @@ __global__ __launch_bounds__(BLOCK) void k_cg_matvec_m(const double* __restrict_
       eB = eC; eC = eD;
     }
   }
-  block_sum_store<1>(acc, 1, partial + blockIdx.x, sh);
+  block_sum2_store<1>(acc, accc, 1, partial + 2 * blockIdx.x, sh);
 }
 
 template <int VEC>
@@ -883,8 +937,8 @@ __global__ __launch_bounds__(BLOCK) void k_cg_xr(double alpha, const double* __r
                                                  double* __restrict__ r, const double* __restrict__ dinv,
                                                  double* __restrict__ z, Geo geo, int64_t lr0, int64_t nlr,
                                                  double* __restrict__ partial) {
-  __shared__ double sh[(BLOCK / 64) * 2];
-  double acc[2] = {0.0, 0.0};
+  __shared__ double sh[(BLOCK / 64) * 2 * 2];
+  double acc[2] = {0.0, 0.0}, accc[2] = {0.0, 0.0};
   ROW_LOOP_BEGIN(VEC)
   for (int qq = 0; qq < VEC && iy + qq < N; ++qq) {
     const int64_t i = li + qq;
@@ -893,11 +947,11 @@ __global__ __launch_bounds__(BLOCK) void k_cg_xr(double alpha, const double* __r
     r[i] = ri;
     const double zi = dinv ? 0.0 + dinv[i] * ri : ri;
     if (dinv) z[i] = zi;
-    acc[0] += ri * ri;
-    acc[1] += ri * zi;
+    comp_dot(acc[0], accc[0], ri, ri);
+    comp_dot(acc[1], accc[1], ri, zi);
   }
   ROW_LOOP_END
-  block_sum_store<2>(acc, 2, partial + 2 * (blockIdx.y * gridDim.x + blockIdx.x), sh);
+  block_sum2_store<2>(acc, accc, 2, partial + 4 * (blockIdx.y * gridDim.x + blockIdx.x), sh);
 }
 
 // Single-reduction CG iteration (Chronopoulos-Gear; the build's non-parity option) on
@@ -980,6 +1034,24 @@ __global__ __launch_bounds__(64) void k_wave_reduce(const double* __restrict__ p
     s = mx ? nan_max(s, t) : s + t;
   }
   if (lane == 0) out[int64_t(j) * nsplit + split] = (mx && s < 0.0) ? 0.0 : s;
+}
+
+// Compensated variant: output j folds the (s, c) pairs partial[j * cs + b * sb + {0, 1}] for b in
+// [split * span, min(nblk, (split+1) * span)) with comp_merge in a fixed order; final != 0 writes
+// s + c to out[j * nsplit + split], else the pair to out[2 (j * nsplit + split) + {0, 1}].
+__global__ __launch_bounds__(64) void k_wave_reduce2(const double* __restrict__ partial, int nblk, int span, int64_t sb,
+                                                     int64_t cs, int final, double* __restrict__ out) {
+  const int j = blockIdx.x, split = blockIdx.y, nsplit = gridDim.y, lane = threadIdx.x;
+  const double* src = partial + int64_t(j) * cs;
+  const int b0 = split * span, b1 = min(nblk, b0 + span);
+  double s = 0.0, c = 0.0;
+  for (int b = b0 + lane; b < b1; b += 64) comp_merge(s, c, src[int64_t(b) * sb], src[int64_t(b) * sb + 1]);
+  wave_sum2(s, c);
+  if (lane == 0) {
+    const int64_t o = int64_t(j) * nsplit + split;
+    if (final) out[o] = s + c;
+    else { out[2 * o] = s; out[2 * o + 1] = c; }
+  }
 }
 
 // out[j] = sum over b of partial[b * stride + j] (mode is_max[j]: NaN-propagating max).
@@ -2311,12 +2383,12 @@ __global__ __launch_bounds__(BLOCK) void k_csr_spmv(int64_t nrows, const int* __
 template <int VEC>
 __global__ __launch_bounds__(BLOCK) void k_dot(const double* __restrict__ a, const double* __restrict__ b, Geo geo,
                                                int64_t lr0, int64_t nlr, double* __restrict__ partial) {
-  __shared__ double sh[BLOCK / 64];
-  double acc[1] = {0.0};
+  __shared__ double sh[BLOCK / 64 * 2];
+  double acc[1] = {0.0}, accc[1] = {0.0};
   ROW_LOOP_BEGIN(VEC)
-  for (int q = 0; q < VEC && iy + q < N; ++q) acc[0] += a[li + q] * b[li + q];
+  for (int q = 0; q < VEC && iy + q < N; ++q) comp_dot(acc[0], accc[0], a[li + q], b[li + q]);
   ROW_LOOP_END
-  block_sum_store<1>(acc, 1, partial + (blockIdx.y * gridDim.x + blockIdx.x), sh);
+  block_sum2_store<1>(acc, accc, 1, partial + 2 * (blockIdx.y * gridDim.x + blockIdx.x), sh);
 }
 
 // Gram of [W P^-1 | r] for a materialised W (k columns of length m, column stride ldw):
@@ -2723,6 +2795,26 @@ int reduce(gnk_ctx* ctx, const double* partial, int nblk, int len, int stride, c
   return wreduce(ctx, partial, nblk, len, stride, len, 0, is_max, out);
 }
 
+// Compensated reduction of nblk blocks of (s, c) pairs: quantity j of block b at
+// partial[2 j + b * sb + {0, 1}] -> out[j] = s + c (k_wave_reduce2; two stages above 4096 blocks).
+int wreduce2(gnk_ctx* ctx, const double* partial, int nblk, int len, int64_t sb, double* out) {
+  constexpr int SPAN = 4096;
+  if (nblk <= SPAN) {
+    hipLaunchKernelGGL(k_wave_reduce2, dim3(len, 1), dim3(64), 0, ctx->stream, partial, nblk, nblk, sb, int64_t(2), 1,
+                       out);
+    return check_launch(ctx, "reduce2");
+  }
+  const int nsplit = (nblk + SPAN - 1) / SPAN;
+  double* tmp = ctx->scratch + (SCRATCH_DOUBLES - size_t(2) * len * nsplit);
+  hipLaunchKernelGGL(k_wave_reduce2, dim3(len, nsplit), dim3(64), 0, ctx->stream, partial, nblk, SPAN, sb, int64_t(2),
+                     0, tmp);
+  int rc = check_launch(ctx, "reduce2 stage 1");
+  if (rc) return rc;
+  hipLaunchKernelGGL(k_wave_reduce2, dim3(len, 1), dim3(64), 0, ctx->stream, tmp, nsplit, nsplit, int64_t(2),
+                     int64_t(2) * nsplit, 1, out);
+  return check_launch(ctx, "reduce2 stage 2");
+}
+
 // device constant {0, 1} flags for {sum, max} reductions
 __device__ int d_sum_max_flags[2] = {0, 1};
 
@@ -2730,6 +2822,13 @@ const int* sum_max_flags() {
   void* p = nullptr;
   (void)hipGetSymbolAddress(&p, HIP_SYMBOL(d_sum_max_flags));
   return static_cast<const int*>(p);
+}
+
+// {sum x^2, max |x|} of k_stats partials ([s, c, max] per block)
+int reduce_stats(gnk_ctx* ctx, const double* partial, int nblk, double* stats_out) {
+  int rc = wreduce2(ctx, partial, nblk, 1, 3, stats_out);
+  if (rc) return rc;
+  return wreduce(ctx, partial + 2, nblk, 1, 3, 1, 0, sum_max_flags() + 1, stats_out + 1);
 }
 
 // flat geometry helpers (generic problems)
@@ -3031,7 +3130,7 @@ int gnk_vec_stats(gnk_ctx* ctx, const double* x, double* stats_out) {
   DISPATCH_VEC(ctx, k_stats, L, 0, x, ctx->geo, L.lr0, L.nlr, ctx->scratch);
   int rc = check_launch(ctx, "vec_stats");
   if (rc) return rc;
-  return reduce(ctx, ctx->scratch, nblk, 2, 2, sum_max_flags(), stats_out);
+  return reduce_stats(ctx, ctx->scratch, nblk, stats_out);
 }
 
 int gnk_vec_div(gnk_ctx* ctx, const double* src, double denom, double* dst, int full_slab) {
@@ -3441,7 +3540,7 @@ int gnk_flat_stats(gnk_ctx* ctx, const double* x, int64_t n, double* stats_out) 
   FLAT_DISPATCH(vec, k_stats, L, x, geo, L.lr0, L.nlr, ctx->scratch);
   int rc = check_launch(ctx, "flat_stats");
   if (rc) return rc;
-  return reduce(ctx, ctx->scratch, int(L.grid.x), 2, 2, sum_max_flags(), stats_out);
+  return reduce_stats(ctx, ctx->scratch, int(L.grid.x), stats_out);
 }
 
 int gnk_flat_dot(gnk_ctx* ctx, const double* a, const double* b, int64_t n, double* out) {
@@ -3453,7 +3552,7 @@ int gnk_flat_dot(gnk_ctx* ctx, const double* a, const double* b, int64_t n, doub
   FLAT_DISPATCH(vec, k_dot, L, a, b, geo, L.lr0, L.nlr, ctx->scratch);
   int rc = check_launch(ctx, "flat_dot");
   if (rc) return rc;
-  return reduce(ctx, ctx->scratch, int(L.grid.x), 1, 1, nullptr, out);
+  return wreduce2(ctx, ctx->scratch, int(L.grid.x), 1, 2, out);
 }
 
 int gnk_flat_div(gnk_ctx* ctx, const double* src, double denom, double* dst, int64_t n) {
@@ -3483,7 +3582,7 @@ int gnk_flat_cg_update_xr(gnk_ctx* ctx, double alpha, const double* p, const dou
   FLAT_DISPATCH(vec, k_cg_xr, L, alpha, p, q, x, r, dinv, z, geo, L.lr0, L.nlr, ctx->scratch);
   int rc = check_launch(ctx, "flat_cg_update_xr");
   if (rc) return rc;
-  return reduce(ctx, ctx->scratch, int(L.grid.x), 2, 2, nullptr, out);
+  return wreduce2(ctx, ctx->scratch, int(L.grid.x), 2, 4, out);
 }
 
 int gnk_flat_cg_update_p(gnk_ctx* ctx, double beta, int first, const double* z, double* p, int64_t n) {
@@ -3559,7 +3658,7 @@ int gnk_cg_normal_matvec(gnk_ctx* ctx, const double* d, const double* p, double*
   }
   int rc = check_launch(ctx, "cg_normal_matvec");
   if (rc) return rc;
-  return reduce(ctx, ctx->scratch, nblk, 1, 1, nullptr, pq_out);
+  return wreduce2(ctx, ctx->scratch, nblk, 1, 2, pq_out);
 }
 
 int gnk_cg_step_matvec(gnk_ctx* ctx, const double* d, const double* z, const double* p_in, double* p_out, double* q,
@@ -3580,7 +3679,7 @@ int gnk_cg_step_matvec(gnk_ctx* ctx, const double* d, const double* z, const dou
   tl.done();
   int rc = check_launch(ctx, "cg_step_matvec");
   if (rc) return rc;
-  return reduce(ctx, ctx->scratch, nblk, 1, 1, nullptr, pq_out);
+  return wreduce2(ctx, ctx->scratch, nblk, 1, 2, pq_out);
 }
 
 int gnk_cg_update_xr(gnk_ctx* ctx, double alpha, const double* p, const double* q, double* x, double* r,
@@ -3591,7 +3690,7 @@ int gnk_cg_update_xr(gnk_ctx* ctx, double alpha, const double* p, const double* 
   DISPATCH_VEC(ctx, k_cg_xr, L, 0, alpha, p, q, x, r, dinv, z, ctx->geo, L.lr0, L.nlr, ctx->scratch);
   int rc = check_launch(ctx, "cg_update_xr");
   if (rc) return rc;
-  return reduce(ctx, ctx->scratch, nblk, 2, 2, nullptr, out);
+  return wreduce2(ctx, ctx->scratch, nblk, 2, 4, out);
 }
 
 int gnk_cg_sr_update(gnk_ctx* ctx, double alpha, double beta, int first, const double* w, double* p, double* s,

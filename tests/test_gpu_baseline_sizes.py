@@ -7,15 +7,14 @@ written by tests/golden/make_golden_large.py, which ran the reference in the bui
 * C3 (configs[2]): N = 8192, the first Gauss-Newton step's CGLS (Jacobi, rtol 1e-8,
   ref:gauss_newton.py:50-58) capped at 30 CG iterations.
 
-Tolerances (per-iteration ||x_k|| and ||r_k||, relative), each backed by a sensitivity test of the
-oracle that shows an algebraically equivalent reordering of the reference's own arithmetic moves
-the reference trajectory at least that much (tests/test_oracle_sensitivity.py):
-  * iteration 1 (k = 1): the step d = (J v)^T r / ||J v||^2 is a cancellation-heavy dot product:
-    K1_TOL (test_c2_sensitivity: row-permuted QR moves it by >= K1_TOL);
-  * otherwise 1e-10 -- north_star's bar -- except res_old after its first restart (iteration > 21),
-    whose trajectory is chaotic: RESTART_TOL (test_c2_sensitivity: >= RESTART_TOL), and the final
-    converged step's Armijo trial count, a rounding tie (the permuted-QR oracle takes 83 instead of
-    82 evaluations there).
+Tolerances (per-iteration ||x_k|| and ||r_k||, relative): max(1e-10, envelope_i), envelope_i = the
+largest move of the reference's own trajectory at iteration i under algebraically equivalent
+reorderings of its arithmetic (tests/tolerances.py, tests/golden/sensitivity.json).  At these sizes
+the envelope is large in two places: iteration 1 (k = 1), where ||x_1|| = |c + d| cancels to 1e-5 of
+||x_0|| and the reference's own dot products are 4e-10 (N = 1024) / 6e-8 (N = 8192) away from the
+exactly rounded step, and res_old after its first restart (iteration > 21), whose trajectory is
+chaotic (1e-7 under a row permutation of the QR).  The converged last step of the res_old run is an
+Armijo rounding tie (its trial count moves with the reorderings too).
 """
 import contextlib
 import io
@@ -30,11 +29,10 @@ pytestmark = pytest.mark.gpu
 
 import gauss_newton_via_generalized_krylov_subspaces_amd as gnk  # noqa: E402
 from oracle import gnk_oracle as O  # noqa: E402
+from tests import tolerances as T  # noqa: E402
 
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
-K1_TOL = 3e-10
-TOL = 1e-10
-RESTART_TOL = 3e-7
+TOL = T.NORTH_STAR
 
 
 def _load(name):
@@ -62,14 +60,6 @@ def _run_gnk(N, max_iter, version):
     return out, rec, buf.getvalue().splitlines()
 
 
-def _tolerances(n, version):
-    tol = np.full(n, TOL)
-    tol[0] = K1_TOL
-    if version == "res_old":
-        tol[21:] = RESTART_TOL
-    return tol
-
-
 @pytest.mark.parametrize("version", ["res_old", "res_new"])
 def test_c2_full_run_vs_reference(version):
     meta, arr = _load("c2")
@@ -87,13 +77,14 @@ def test_c2_full_run_vs_reference(version):
         assert abs(rec["nfev"][-1] - ref["nfev"][-1]) <= 2 and out.nrev - rec["nfev"][-1] == case["nrev"] - ref["nfev"][-1]
     else:
         assert out.nrev == case["nrev"]
-    tol = _tolerances(n, version)
+    tol = T.per_iteration(f"c2_{version}", n)
+    tol_r = T.per_iteration(f"c2_{version}", n, "r")
     ex = np.abs(np.array(rec["xnorm"]) - ref["xnorm"]) / np.abs(ref["xnorm"])
     er = np.abs(np.array(rec["rnorm"]) - ref["rnorm"]) / np.abs(ref["rnorm"])
     print(f"C2 {version}: max rel ||x_k|| {ex.max():.3g} (it {ex.argmax() + 1}), k=1 {ex[0]:.3g}, "
           f"before restart {ex[1:21].max():.3g}; ||r_k|| {er.max():.3g}")
     assert np.all(ex <= tol), np.nonzero(ex > tol)
-    assert np.all(er <= tol), np.nonzero(er > tol)
+    assert np.all(er <= tol_r), np.nonzero(er > tol_r)
     xs = out.x[::meta["subsample_stride"]]
     np.testing.assert_allclose(xs, arr[f"{version}__x_sub"], rtol=0, atol=tol[-1] * 10 * np.abs(xs).max())
 
@@ -106,11 +97,12 @@ def test_headline_8192_first_iterations_vs_reference():
     ref = case["per_iter"]
     assert (out.nit, out.nrev, out.njev, out.success) == (case["nit"], case["nrev"], case["njev"], case["success"])
     assert rec["nfev"] == ref["nfev"] and so == case["stdout"]
-    tol = _tolerances(len(ref["nfev"]), "res_old")
+    tol = T.per_iteration("head8192", len(ref["nfev"]))
+    tol_r = T.per_iteration("head8192", len(ref["nfev"]), "r")
     ex = np.abs(np.array(rec["xnorm"]) - ref["xnorm"]) / np.abs(ref["xnorm"])
     er = np.abs(np.array(rec["rnorm"]) - ref["rnorm"]) / np.abs(ref["rnorm"])
     print(f"8192^2 first 4 iterations: rel ||x_k|| {ex}, ||r_k|| {er}")
-    assert np.all(ex <= tol) and np.all(er <= tol)
+    assert np.all(ex <= tol) and np.all(er <= tol_r)
 
 
 def test_c3_cgls_8192_capped_vs_reference():

@@ -112,14 +112,13 @@ def test_gpu_generic_gnk_rosenbrock(golden, p, x0name, version):
         out, rec, so, exc = _run(gnk.gauss_newton_krylow, res, x0, jac, version=version)
     name = f"rosen{p}_{x0name}_{version}"
     case = meta["cases"][name]
-    if version == "gn":
-        # scipy's cg stops on ||r|| < rtol ||b|| (strict): near convergence that is a rounding tie,
-        # and the GPU reductions round differently from OpenBLAS ddot / dnrm2 -- a CG solve may take
-        # one iteration more or less (as for the long Bratu CG solves); the outer
-        # bookkeeping and trajectory stay exact
+    if version == "gn" and p == 2:
+        # the CG dot products are compensated (as exactly rounded sums), which reproduces every cg_iter
+        # of the reference except the converged last outer step of the p = 2 runs: a CG stopping test
+        # on a 2-element residual that is a rounding tie (an exactly rounded dot flips one of them:
+        # tests/test_oracle_sensitivity.py::test_rosen2_last_cg_count_is_a_tie)
         ref_cg = case["per_iter"]["cg_iter"]
-        assert len(rec["cg_iter"]) == len(ref_cg)
-        assert all(abs(a - b) <= 1 for a, b in zip(rec["cg_iter"], ref_cg))
+        assert rec["cg_iter"][:-1] == ref_cg[:-1] and abs(rec["cg_iter"][-1] - ref_cg[-1]) <= 1
         rec = dict(rec, cg_iter=ref_cg)
     _check(case, out, rec, so, exc, rtol=1e-10 if p == 2 else 1e-9)
     if p == 2:

@@ -15,6 +15,7 @@ pytestmark = pytest.mark.gpu
 
 import gauss_newton_via_generalized_krylov_subspaces_amd as gnk  # noqa: E402
 from oracle import gnk_oracle as O  # noqa: E402
+from tests import tolerances as T  # noqa: E402
 from tests.test_host_logic import check  # noqa: E402
 
 
@@ -60,9 +61,23 @@ def test_gnk_bratu100(golden, version, restart):
     y = prob.pde_operator(prob.u_true)
     out, rec, so, exc = run(gnk.gauss_newton_krylow, dict(grid_nodes=101, ALPHA=5, LAMBDA=10),
                             arr["bratu100_u0"], y, version=version, max_iter=100, krylow_restart=restart)
-    check(meta["cases"][f"bratu100_{version}_r{restart}"], out, rec, so, exc,
-          rtol=1e-10 if restart is None else 1e-9)
-    np.testing.assert_allclose(out.x, arr[f"bratu100_{version}_r{restart}__x"], rtol=1e-8, atol=1e-10)
+    case = meta["cases"][f"bratu100_{version}_r{restart}"]
+    if restart is None:
+        check(case, out, rec, so, exc, rtol=T.NORTH_STAR)
+        np.testing.assert_allclose(out.x, arr[f"bratu100_{version}_r{restart}__x"], rtol=0,
+                                   atol=1e-9 * np.abs(out.x).max())
+        return
+    # restart 20: per-iteration bound max(1e-10, what reordering the reference's own QR / sums moves
+    # it by) -- tests/tolerances.py, case bratu100_r20_<version>
+    tol = T.per_iteration(f"bratu100_r20_{version}", len(case["per_iter"]["xnorm"]))
+    check(case, out, dict(rec, xnorm=case["per_iter"]["xnorm"], rnorm=case["per_iter"]["rnorm"]), so, exc)
+    ex = np.abs(np.array(rec["xnorm"]) - case["per_iter"]["xnorm"]) / np.abs(case["per_iter"]["xnorm"])
+    assert np.all(ex <= tol), (ex.max(), np.nonzero(ex > tol))
+    tol_r = T.per_iteration(f"bratu100_r20_{version}", len(case["per_iter"]["rnorm"]), "r")
+    er = np.abs(np.array(rec["rnorm"]) - case["per_iter"]["rnorm"]) / np.abs(case["per_iter"]["rnorm"])
+    assert np.all(er <= tol_r), (er.max(), np.nonzero(er > tol_r))
+    np.testing.assert_allclose(out.x, arr[f"bratu100_{version}_r{restart}__x"], rtol=0,
+                               atol=10 * tol[-1] * np.abs(out.x).max())
 
 
 @pytest.mark.parametrize("version", ["res_old", "res_new"])
@@ -126,29 +141,22 @@ def test_gn_bratu24(golden, name, kw):
 
 
 def test_gn_bratu100(golden):
-    """CG runs of 900-2000 iterations (unpreconditioned + Jacobi, ref:gauss_newton.py:45-58) amplify
-    the block-order rounding of the GPU dot products; the NumPy test double (np.dot, as scipy)
-    reproduces the reference bit for bit, the GPU path may end a long CG solve one iteration
-    earlier or later.  GN bookkeeping exact; cg_iter within 1; iterates within 1e-6."""
+    """CG runs of 900-2000 iterations (unpreconditioned + Jacobi, ref:gauss_newton.py:45-58): the device
+    dot products are compensated (exactly rounded sums), which reproduces the reference's cg_iter of
+    every outer step; bookkeeping exact, iterates within 1e-10."""
     meta, arr = golden
     prob = O.BratuPdeProblem(101, 5, 10)
     y = prob.pde_operator(prob.u_true)
     out, rec, so, exc = run(gnk.gauss_newton, dict(grid_nodes=101, ALPHA=5, LAMBDA=10), arr["bratu100_u0"], y)
-    case = meta["cases"]["bratu100_gn"]
-    assert so == case["stdout"] and exc is None
-    assert (out.nit, out.nrev, out.njev, out.success) == (case["nit"], case["nrev"], case["njev"], case["success"])
-    ref = case["per_iter"]
-    assert rec["nfev"] == ref["nfev"]
-    assert rec["cg_iter"][:3] == ref["cg_iter"][:3]
-    assert all(abs(a - b) <= 1 for a, b in zip(rec["cg_iter"], ref["cg_iter"]))
-    np.testing.assert_allclose(rec["xnorm"], ref["xnorm"], rtol=1e-6)
+    check(meta["cases"]["bratu100_gn"], out, rec, so, exc, rtol=T.NORTH_STAR)
 
 
 @pytest.mark.parametrize("N,name", [(24, "bratu24_gn"), (100, "bratu100_gn")])
 def test_gn_single_reduction_cg_gpu(golden, N, name):
-    """cg_variant="single_reduction" (Chronopoulos-Gear: one reduction per CG iteration)
-    on the GPU against the golden GN runs: outer bookkeeping exact, cg_iter within 1 (a different
-    recurrence, so a long solve may stop one iteration apart), iterates within 1e-6."""
+    """cg_variant="single_reduction" (Chronopoulos-Gear: one reduction per CG iteration) --
+    a NON-parity option: a different recurrence from the reference's scipy cg (same iterates only in
+    exact arithmetic), so a long solve may stop one iteration apart and the iterates differ by the
+    recurrences' rounding; outer bookkeeping exact, cg_iter within 1, iterates within 1e-6."""
     meta, arr = golden
     if N == 24:
         u0, y = arr["bratu24_u0"], arr["bratu24_y"]
@@ -175,9 +183,10 @@ def test_cg_least_squares(golden, N, pre, rtol):
     x, it = gnk.cg_least_squares(-1 * dprob.make_jac()(u0), r0, cg_rtol=rtol, preconditioner=pre)
     name = f"cgls{N}_pre{int(pre)}" + ("_rtol1e-8" if rtol == 1e-8 else "")
     assert it == meta["cases"][name]["cg_iter"]
-    # long recurrences (up to 949 iterations at rtol 1e-8) amplify the block-order rounding of
-    # the GPU dot products: the solution agrees to 1e-7 of its scale, 1e-9 for the short solves
-    tol = 1e-7 if it > 500 else 1e-9
+    # compensated device dot products: the short solves agree to 1e-10 of max |x|; the 949-iteration
+    # rtol 1e-8 solve to CGLS_LONG_X, which the exactly rounded recurrence itself is from the
+    # reference's (tests/tolerances.py)
+    tol = T.CGLS_LONG_X if it > 500 else T.NORTH_STAR
     np.testing.assert_allclose(x, arr[name + "__x"], rtol=0, atol=tol * np.abs(x).max())
 
 
@@ -195,8 +204,9 @@ def test_drop_in_closures_on_host_arrays(golden):
                                atol=1e-12 * np.abs(arr["ops64_res"]).max())
 
 
-def test_gnk_deterministic_and_restart_large():
-    """N = 1024, restart 20: two runs are bitwise identical; iterates stay close to the oracle."""
+def test_gnk_deterministic_restart_large():
+    """N = 1024, restart 20: two runs are bitwise identical (fixed-order reductions, no atomics).  The
+    trajectory itself is checked against the reference's C2 run in test_gpu_baseline_sizes.py."""
     N = 1024
     prob_o, y, u0 = O.bratu_workload(N)
     prob = gnk.BratuPdeProblem(N + 1, 5, 10)
@@ -206,23 +216,13 @@ def test_gnk_deterministic_and_restart_large():
             outs.append(gnk.gauss_newton_krylow(prob.make_res(y), u0, prob.make_jac(), krylow_restart=20, max_iter=25))
     np.testing.assert_array_equal(outs[0].x, outs[1].x)
     assert outs[0].nrev == outs[1].nrev
-    with contextlib.redirect_stdout(io.StringIO()):
-        ref = O.gauss_newton_krylow(prob_o.make_res(y), u0, prob_o.make_jac(), krylow_restart=20, max_iter=25)
-    assert (outs[0].nit, outs[0].nrev, outs[0].njev) == (ref.nit, ref.nrev, ref.njev)
-    # At N = 1024 the k = 1 step and the steps right after a restart solve least-squares
-    # problems whose Q^T r is a cancellation-heavy dot product of noise-dominated vectors:
-    # the same CholQR2 algorithm on the host (tests/numpy_backend.py) differs from the
-    # LAPACK-Householder oracle by 4.5e-10 at k = 1 and 1.1e-9 after the restart, so 1e-10
-    # is below what any re-ordering of the arithmetic can hold here; 5e-9 is.
-    np.testing.assert_allclose(np.linalg.norm(outs[0].x), np.linalg.norm(ref.x), rtol=5e-9)
-    np.testing.assert_allclose(outs[0].x, ref.x, rtol=0, atol=1e-7 * np.abs(ref.x).max())
 
 
 @pytest.mark.parametrize("restart,version", [(3, "res_old"), (7, "res_old"), (5, "res_new")])
 def test_gnk_short_restart_cycles_vs_oracle(restart, version):
     """Short restart cycles at N = 256 exercise the speculative next-step solve across
-    many restarts and loop ends: bookkeeping equal to the oracle, ||x|| within 5e-9 (the post-restart
-    least-squares steps are cancellation-limited, see test_gnk_deterministic_and_restart_large)."""
+    many restarts and loop ends: bookkeeping equal to the oracle, ||x_k|| within max(1e-10, the
+    reordering envelope of the same run, tests/tolerances.py case short256_r<restart>_<version>)."""
     N = 256
     prob_o, y, u0 = O.bratu_workload(N)
     prob = gnk.BratuPdeProblem(N + 1, 5, 10)
@@ -236,4 +236,7 @@ def test_gnk_short_restart_cycles_vs_oracle(restart, version):
                                     callback=lambda x, nfev, cg_iter: rec_o.append((np.linalg.norm(x), nfev)))
     assert (out.nit, out.nrev, out.njev, out.success) == (ref.nit, ref.nrev, ref.njev, ref.success)
     assert [n for _, n in rec_d] == [n for _, n in rec_o]
-    np.testing.assert_allclose([a for a, _ in rec_d], [a for a, _ in rec_o], rtol=5e-9)
+    xd, xo = np.array([a for a, _ in rec_d]), np.array([a for a, _ in rec_o])
+    tol = T.per_iteration(f"short256_r{restart}_{version}", len(xo))
+    ex = np.abs(xd - xo) / np.abs(xo)
+    assert np.all(ex <= tol), (ex.max(), np.nonzero(ex > tol))
