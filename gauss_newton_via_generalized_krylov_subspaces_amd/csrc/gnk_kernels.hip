@@ -1465,15 +1465,15 @@ __global__ __launch_bounds__(BLOCK) void k_gram_w(const double* __restrict__ u, 
 __device__ __forceinline__ double dpp_row_shr1(double v) {     // lane l <- lane l-1 of its 16-lane row
   const u2v b = __builtin_bit_cast(u2v, v);
   u2v o;
-  o.x = unsigned(__builtin_amdgcn_update_dpp(0, int(b.x), 0x111, 0xf, 0xf, false));
-  o.y = unsigned(__builtin_amdgcn_update_dpp(0, int(b.y), 0x111, 0xf, 0xf, false));
+  o.x = unsigned(__builtin_amdgcn_mov_dpp(int(b.x), 0x111, 0xf, 0xf, true));   // bound_ctrl: row edge -> 0
+  o.y = unsigned(__builtin_amdgcn_mov_dpp(int(b.y), 0x111, 0xf, 0xf, true));   // bound_ctrl: row edge -> 0
   return __builtin_bit_cast(double, o);
 }
 __device__ __forceinline__ double dpp_row_shl1(double v) {     // lane l <- lane l+1 of its 16-lane row
   const u2v b = __builtin_bit_cast(u2v, v);
   u2v o;
-  o.x = unsigned(__builtin_amdgcn_update_dpp(0, int(b.x), 0x101, 0xf, 0xf, false));
-  o.y = unsigned(__builtin_amdgcn_update_dpp(0, int(b.y), 0x101, 0xf, 0xf, false));
+  o.x = unsigned(__builtin_amdgcn_mov_dpp(int(b.x), 0x101, 0xf, 0xf, true));   // bound_ctrl: row edge -> 0
+  o.y = unsigned(__builtin_amdgcn_mov_dpp(int(b.y), 0x101, 0xf, 0xf, true));   // bound_ctrl: row edge -> 0
   return __builtin_bit_cast(double, o);
 }
 
@@ -1823,8 +1823,9 @@ constexpr unsigned waitcnt_vm_lgkm0(int n) { return unsigned((n & 0xF) | ((n >> 
 template <int J>
 __device__ __forceinline__ double bcast_row(double v) {
   const int2 b = __builtin_bit_cast(int2, v);
-  const int lo = __builtin_amdgcn_update_dpp(0, b.x, 0x150 + J, 0xF, 0xF, false);
-  const int hi = __builtin_amdgcn_update_dpp(0, b.y, 0x150 + J, 0xF, 0xF, false);
+  // mov_dpp: every lane has a valid source, so no "old" value (update_dpp's costs a v_mov per half)
+  const int lo = __builtin_amdgcn_mov_dpp(b.x, 0x150 + J, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_mov_dpp(b.y, 0x150 + J, 0xF, 0xF, false);
   return __builtin_bit_cast(double, int2{lo, hi});
 }
 
