@@ -2461,6 +2461,48 @@ __global__ __launch_bounds__(BLOCK) void k_flat_gram(const double* __restrict__ 
   for (int t = tid; t < P * 256; t += BLOCK) out[t] = red[t];
 }
 
+// Flat Gram for bases wider than k_flat_gram's four 16-column blocks (generic problems, SURVEY f1:
+// the reference grows the basis to max_iter - 1 columns without restart, ref:krylow.py:72-73).  Two
+// plain passes, both deterministic:
+//   Y[j][i] = sum_{l <= j} W[l][i] RinvAug[l][j]   (l ascending; Y[k] = r, padding columns 0)
+//   Gout[a][b] = Gout[b][a] = sum_i Y[a][i] Y[b][i]   (one block per pair a <= b, compensated sums)
+// The generic path's sizes are small (m residuals of a user problem): these run once per pass.
+__global__ __launch_bounds__(BLOCK) void k_flat_ytrans(const double* __restrict__ W, int64_t ldw, int k,
+                                                       const double* __restrict__ rinv, int ldr,
+                                                       const double* __restrict__ r, int64_t m, int kp,
+                                                       double* __restrict__ Y) {
+  const int j = blockIdx.y;
+  for (int64_t i = int64_t(blockIdx.x) * BLOCK + threadIdx.x; i < m; i += int64_t(gridDim.x) * BLOCK) {
+    double y = 0.0;
+    if (j < k) {
+      for (int l = 0; l <= j; ++l) y = fma(W[int64_t(l) * ldw + i], rinv ? rinv[int64_t(l) * ldr + j] : (l == j), y);
+    } else if (j == k && r) {
+      y = r[i];
+    }
+    Y[int64_t(j) * m + i] = y;
+  }
+}
+
+__global__ __launch_bounds__(BLOCK) void k_flat_syrk(const double* __restrict__ Y, int64_t m, int kp,
+                                                     double* __restrict__ Gout) {
+  __shared__ double sh[BLOCK / 64 * 2];
+  // pair index -> (a, b), a <= b, row-major over the upper triangle
+  int p = blockIdx.x, a = 0;
+  while (p >= kp - a) { p -= kp - a; ++a; }
+  const int b = a + p;
+  double s[1] = {0.0}, c[1] = {0.0};
+  const double* ya = Y + int64_t(a) * m;
+  const double* yb = Y + int64_t(b) * m;
+  for (int64_t i = threadIdx.x; i < m; i += BLOCK) comp_dot(s[0], c[0], ya[i], yb[i]);
+  double out[2];
+  block_sum2_store<1>(s, c, 1, out, sh);
+  if (threadIdx.x == 0) {
+    const double v = out[0] + out[1];
+    Gout[a * kp + b] = v;
+    Gout[b * kp + a] = v;
+  }
+}
+
 // Sum Gram partials over blocks (block order) and scatter into G[KP][KP] (symmetric).
 // scatter the reduced pair tiles (red[pair * 256 + lane * 4 + i]) into symmetric G[KP][KP]
 __global__ __launch_bounds__(BLOCK) void k_gram_scatter(const double* __restrict__ red, int P, int KP,
@@ -3612,8 +3654,18 @@ int gnk_flat_gram(gnk_ctx* ctx, const double* W, int64_t ldw, int k, const doubl
   if (k < 1 || m < 1) return fail(ctx, "flat_gram: k < 1 or m < 1");
   const int KP = gnk_gram_padded_dim(k, r != nullptr);
   const int nb = KP / 16;
-  if (nb > 4) return fail(ctx, "flat_gram: at most 63 basis columns (+ r)");
   if (rinv && ldr != KP) return fail(ctx, "flat_gram: rinv must be the kp x kp augmented inverse (ldr == kp)");
+  if (nb > 4) {
+    // wide basis: Y = W RinvAug materialised in the scratch arena, then the pairwise Gram
+    if (size_t(KP) * size_t(m) > SCRATCH_DOUBLES || KP > 1024) return fail(ctx, "flat_gram: basis too wide for the scratch arena");
+    double* Y = ctx->scratch;
+    const unsigned gx = unsigned(std::min<int64_t>((m + BLOCK - 1) / BLOCK, 1024));
+    hipLaunchKernelGGL(k_flat_ytrans, dim3(gx, KP), dim3(BLOCK), 0, ctx->stream, W, ldw, k, rinv, KP, r, m, KP, Y);
+    int rc = check_launch(ctx, "flat_gram ytrans");
+    if (rc) return rc;
+    hipLaunchKernelGGL(k_flat_syrk, dim3(KP * (KP + 1) / 2), dim3(BLOCK), 0, ctx->stream, Y, m, KP, G_out);
+    return check_launch(ctx, "flat_gram syrk");
+  }
   const double* rv = rinv ? rinv : ctx->ident + ident_offset(nb);
   const int P = nb * (nb + 1) / 2;
   const int64_t nchunk = (m + 15) / 16;

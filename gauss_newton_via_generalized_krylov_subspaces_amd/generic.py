@@ -14,8 +14,11 @@ the results to the GPU:
     (``gnk_flat_gram`` of [J V P^-1 | r] -> lls.CholQR2Solver) and the Armijo trials run in the
     HIP library exactly as for Bratu.
 
-Single GPU (a user callable has no row partition); at most 63 basis columns per least-squares
-solve (the flat Gram kernel's four 16-column MFMA blocks).
+Single GPU (a user callable has no row partition).  The flat Gram runs on MFMA tiles up to 63
+basis columns (+ r) and as a transform pass plus a pairwise compensated Gram beyond (up to 1023
+columns), so the reference's default -- no restart, the basis growing to max_iter - 1 columns
+(ref:gauss_newton_krylow.py:81-82, ref:krylow.py:72-73) -- and dense Jacobians of more than 63
+parameters (ref:gauss_newton.py:115-116) run unchanged.
 """
 from __future__ import annotations
 
@@ -30,7 +33,8 @@ from .krylow import GeneralizedKrylowSubspaceBreakdown, GeneralizedKrylowSubspac
 from .lls import CholQR2Solver
 from .slab import Comm
 
-FLAT_GRAM_KMAX = 63
+FLAT_GRAM_KMAX = 1023          # gnk_flat_gram: MFMA tiles up to 63 columns (+ r), a transform + pairwise
+                               # Gram pass beyond (KP <= 1024, m x KP doubles in the scratch arena)
 
 
 class DeviceCSR:

@@ -148,3 +148,53 @@ def test_rank_deficient_dense_gn():
 
 def test_rank_deficient_gnk():
     check_rank_deficient_gnk(dict(_backend=NumpyBackend()))
+
+
+# -- bases wider than 63 columns (the reference never restarts by default and grows the basis to
+# max_iter - 1 columns, ref:gauss_newton_krylow.py:81-82, ref:krylow.py:72-73) and dense Jacobians with more
+# than 63 parameters (ref:gauss_newton.py:115-116)
+def check_wide_basis(backend_kw):
+    """Rosenbrock p = 1000 from the F5 start, res_old, tol 1e-12, max_iter 71: 70 iterations without restart,
+    the basis grows to 70 columns -- bookkeeping exact, ||x_k|| within 1e-10 of the oracle.  (At tol 0 / longer
+    runs the converged steps are Armijo rounding ties; this window stops before them.)"""
+    meta_arr = dict(np.load(__import__("os").path.join(__import__("os").path.dirname(__file__), "golden", "golden.npz")))
+    res, jac = O.rosenbrock(1000)
+    x0 = meta_arr["rosen1000_x0_i"]
+    runs = []
+    for fn, kw in ((gnk.gauss_newton_krylow, backend_kw), (O.gauss_newton_krylow, {})):
+        rec = []
+        with contextlib.redirect_stdout(io.StringIO()):
+            r = fn(res, x0.copy(), jac, tol=1e-12, max_iter=71, version="res_old",
+                   callback=lambda x, nfev, cg_iter: rec.append((np.linalg.norm(x), nfev)), **kw)
+        runs.append((r, rec))
+    (a, ra), (b, rb) = runs
+    assert (a.nit, a.nrev, a.njev, a.success) == (b.nit, b.nrev, b.njev, b.success) == (70, 71, 71, False)
+    assert [n for _, n in ra] == [n for _, n in rb]
+    np.testing.assert_allclose([x for x, _ in ra], [x for x, _ in rb], rtol=1e-10)
+
+
+def check_dense_100(backend_kw):
+    """gauss_newton's lstsq branch with 100 parameters (ndarray Jacobians of the Rosenbrock chain, three
+    starts) vs scipy.linalg.lstsq in the oracle: bookkeeping exact, ||x_k|| within 1e-10."""
+    res, jac = O.rosenbrock(100)
+    djac = lambda x: jac(x).toarray()  # noqa: E731
+    rng = np.random.default_rng(42)
+    for x0 in (2 * np.ones(100), 1 + 0.1 * rng.standard_normal(100), np.r_[2.0, 2.0, 1.99, 2 * np.ones(97)]):
+        runs = []
+        for fn, kw in ((gnk.gauss_newton, backend_kw), (O.gauss_newton, {})):
+            rec = []
+            with contextlib.redirect_stdout(io.StringIO()):
+                r = fn(res, x0.copy(), djac, callback=lambda x, nfev, cg_iter: rec.append((np.linalg.norm(x), nfev)), **kw)
+            runs.append((r, rec))
+        (a, ra), (b, rb) = runs
+        assert (a.nit, a.nrev, a.njev, a.success) == (b.nit, b.nrev, b.njev, b.success)
+        assert [n for _, n in ra] == [n for _, n in rb]
+        np.testing.assert_allclose([x for x, _ in ra], [x for x, _ in rb], rtol=1e-10)
+
+
+def test_wide_basis_beyond_63_columns():
+    check_wide_basis(dict(_backend=NumpyBackend()))
+
+
+def test_dense_lstsq_100_parameters():
+    check_dense_100(dict(_backend=NumpyBackend()))

@@ -180,3 +180,47 @@ def test_rank_deficient_dense_gn_gpu():
 def test_rank_deficient_gnk_gpu():
     from tests.test_generic_host import check_rank_deficient_gnk
     check_rank_deficient_gnk({})
+
+
+def test_wide_basis_beyond_63_columns_gpu():
+    """70 basis columns: the MFMA flat Gram up to 63, the transform + pairwise Gram pass beyond."""
+    from tests.test_generic_host import check_wide_basis
+    check_wide_basis({})
+
+
+def test_dense_lstsq_100_parameters_gpu():
+    from tests.test_generic_host import check_dense_100
+    check_dense_100({})
+
+
+@pytest.mark.parametrize("m,k,with_r,with_rinv", [(1000, 64, True, True), (2000, 70, True, True), (333, 99, False, True),
+                                                  (4096, 80, True, False), (150, 120, True, True)])
+def test_flat_gram_wide(be, m, k, with_r, with_rinv):
+    """gnk_flat_gram beyond 63 columns (Y = W RinvAug, then the pairwise compensated Gram) vs NumPy."""
+    rng = np.random.default_rng(m + k)
+    Wh = rng.standard_normal((k, m))
+    r = rng.standard_normal(m) if with_r else None
+    kp = be.gram_dim(k, with_r)
+    Rinv = None
+    Wa = np.zeros((m, kp))
+    Wa[:, :k] = Wh.T
+    if with_r:
+        Wa[:, k] = r
+    if with_rinv:
+        A = np.triu(rng.standard_normal((kp, kp))) * 0.1 + np.eye(kp)
+        A[k + (1 if with_r else 0):, :] = 0
+        A[:, k + (1 if with_r else 0):] = 0
+        if with_r:
+            A[k, :] = 0
+            A[:, k] = 0
+            A[k, k] = 1.0
+        Rinv = A
+        Wa = Wa @ A
+    Gref = Wa.T @ Wa
+    G = be.zeros(kp * kp)
+    be.flat_gram(be.to_device(Wh), k, None if Rinv is None else be.to_device(Rinv.reshape(-1)),
+                 None if r is None else be.to_device(r), m, G)
+    Gd = G.cpu().numpy().reshape(kp, kp)
+    scale = np.sqrt(np.outer(np.diag(Gref), np.diag(Gref))) + 1e-300
+    assert np.max(np.abs(Gd - Gref) / scale) < 1e-13
+    np.testing.assert_array_equal(Gd, Gd.T)
