@@ -10,6 +10,9 @@ reference's own result depends on the thread count):
                 dot product at large N) with exactly rounded sums (math.fsum);
   perm<s>       Householder QR of the row-permuted [A | y] (permutation seed s);
   perm<s>+k1    both;
+  cholqr2       the least-squares step by CholeskyQR2 (R from the Cholesky factor of the Gram of A,
+                twice; Q^T y = R^-T A^T y) instead of Householder -- the same factorisation in exact
+                arithmetic, and the family the device solve belongs to;
   slab<P>       every reduction ordered as a P-rank slab run (P = 2..8) orders it: TSQR over P row blocks
                 (Householder QR per block, QR of the stacked R factors) and the Krylov update's V^T g,
                 ||g|| summed block by block in rank order (multi-slab cases only).
@@ -55,6 +58,19 @@ def lls_variant(exact_k1, seed):
     return lls
 
 
+def cholqr2_lls(A, y):
+    """min ||A d - y|| by CholeskyQR2 (prints the reference's rank messages from its R)."""
+    R1 = scipy.linalg.cholesky(A.T @ A, lower=False)
+    Q1 = scipy.linalg.solve_triangular(R1, A.T, trans="T", lower=False).T
+    R2 = scipy.linalg.cholesky(Q1.T @ Q1, lower=False)
+    R = R2 @ R1
+    for r_kk in np.diagonal(R):
+        if np.isclose(r_kk, 0, atol=1e-8):
+            print("A is rank deficient")
+    z = scipy.linalg.solve_triangular(R, A.T @ y, trans="T", lower=False)
+    return scipy.linalg.solve_triangular(R, z)
+
+
 def slab_variant(N, P):
     """(lls, update) with every reduction split into the row slabs of a P-rank run, summed in rank order."""
     from gauss_newton_via_generalized_krylov_subspaces_amd.slab import row_partition
@@ -90,7 +106,8 @@ def slab_variant(N, P):
 
 def variants(N, slabs=False):
     v = {"base": (_LLS, _UPDATE), "exact_k1": (lls_variant(True, None), _UPDATE),
-         "perm7": (lls_variant(False, 7), _UPDATE), "perm8+k1": (lls_variant(True, 8), _UPDATE)}
+         "perm7": (lls_variant(False, 7), _UPDATE), "perm8+k1": (lls_variant(True, 8), _UPDATE),
+         "cholqr2": (cholqr2_lls, _UPDATE)}
     if slabs:
         v.update({f"slab{P}": slab_variant(N, P) for P in range(2, 9)})
     return v
@@ -111,12 +128,17 @@ def trajectory(prob, y, u0, lls, update, threads, **kw):
     return np.array(xs), np.array(rs), nf
 
 
+ONLY = None            # --only v1,v2: recompute these variants (and base) and merge into the stored case
+
+
 def envelope(N, ref=None, slabs=False, threads=THREADS, **kw):
     """Per-variant and maximal per-iteration distances from ``ref`` = (xnorm, rnorm) (None: the
     1-thread base oracle)."""
     prob, y, u0 = O.bratu_workload(N)
     runs = {}
     for name, (lls, upd) in variants(N, slabs).items():
+        if ONLY is not None and name not in ONLY and not (name == "base" and ref is None):
+            continue
         for t in threads:
             runs[f"{name}@{t}"] = trajectory(prob, y, u0, lls, upd, t, **kw)
     if ref is None:
@@ -162,13 +184,24 @@ CASES = {
 
 def store(case, res):
     allc = json.load(open(PATH)) if os.path.exists(PATH) else {}
+    if ONLY is not None and case in allc:                  # merge the recomputed variants
+        old = allc[case]
+        old["variants"].update(res["variants"])
+        n = min(len(v["x"]) for v in old["variants"].values())
+        old["envelope"] = {k: [max(v[k][i] for v in old["variants"].values() if k in v) for i in range(n)]
+                           for k in ("x", "r") if any(k in v for v in old["variants"].values())}
+        res = old
     allc[case] = res
     with open(PATH, "w") as f:
         json.dump(allc, f, indent=1, sort_keys=True)
 
 
 if __name__ == "__main__":
-    names = list(CASES) if sys.argv[1:] == ["all"] else sys.argv[1:]
+    args = sys.argv[1:]
+    if args and args[0] == "--only":
+        ONLY = set(args[1].split(","))
+        args = args[2:]
+    names = list(CASES) if args == ["all"] else args
     for case in names:
         r = CASES[case]()
         store(case, r)
