@@ -1119,7 +1119,7 @@ template <int PPW>
 __global__ __launch_bounds__(BLOCK) void k_gram(const double* __restrict__ u, const double* __restrict__ V,
                                                 int64_t ldv, int k, const double* __restrict__ rinv,
                                                 const double* __restrict__ r, Geo geo, Coef c, int T, int logT,
-                                                int KP, int P, int rowsplit, int64_t ntiles,
+                                                int KP, int P, int rowsplit, int64_t ntiles, int rinv_in_lds,
                                                 double* __restrict__ partial) {
   extern __shared__ __attribute__((aligned(16))) double lds[];
   const int S = KP + 1;
@@ -1148,8 +1148,10 @@ __global__ __launch_bounds__(BLOCK) void k_gram(const double* __restrict__ u, co
   // padding columns [K1, KP) stay zero for the whole launch (the pass-2 transform
   // writes zeros there too: RinvAug is zero outside its k(+1) leading block)
   for (int idx = tid; idx < T * S; idx += BLOCK) Wt[idx] = 0.0;
-  // RinvAug staged once per launch behind the tile when it fits (KP <= 64)
-  double* rinv_lds = (rinv && KP <= 64) ? lds + T * S : nullptr;
+  // RinvAug staged once per launch behind the tile when it fits (the host decides: KP <= 64, and
+  // wider bases as long as tile + RinvAug fit the LDS -- a B operand from L2 inside the transform's
+  // MFMA chain makes the pass latency-bound)
+  double* rinv_lds = (rinv && rinv_in_lds) ? lds + T * S : nullptr;
   if (rinv_lds)
     for (int idx = tid; idx < KP * KP; idx += BLOCK) rinv_lds[idx] = rinv[idx];
   __syncthreads();
@@ -3489,7 +3491,9 @@ int gnk_gram(gnk_ctx* ctx, const double* u, const double* V, int64_t ldv, int k,
   while (T > 64 && size_t(T) * (KP + 1) * 8 > 40 * 1024) T >>= 1;
   int logT = 0;
   while ((1 << logT) < T) ++logT;
-  size_t lds = size_t(T) * (KP + 1) * 8 + ((rinv && KP <= 64) ? size_t(KP) * KP * 8 : 0);
+  const size_t tile_b = size_t(T) * (KP + 1) * 8;
+  const int rinv_in_lds = rinv && tile_b + size_t(KP) * KP * 8 <= 160 * 1024 ? 1 : 0;
+  size_t lds = tile_b + (rinv_in_lds ? size_t(KP) * KP * 8 : 0);
   lds = (lds + 15) & ~size_t(15);
   if (rowsplit && size_t(P) * 256 > size_t(T) * (KP + 1)) return fail(ctx, "gram: reduction staging does not fit");
   if (lds > 160 * 1024) return fail(ctx, "gram: k too large for the LDS tile");
@@ -3504,7 +3508,7 @@ int gnk_gram(gnk_ctx* ctx, const double* u, const double* V, int64_t ldv, int k,
   TimedLaunch tl(ctx, GNK_TIMER_GRAM, 8.0 * double(nown) * double(k + 1 + (r ? 1 : 0)));
 #define GRAM_LAUNCH(PP)                                                                                    \
   hipLaunchKernelGGL(k_gram<PP>, dim3(unsigned(nblk), unsigned(groups)), dim3(BLOCK), lds, ctx->stream, u, V, ldv, \
-                     k, rinv, r, ctx->geo, ctx->coef, T, logT, KP, P, rowsplit, ntiles, ctx->scratch)
+                     k, rinv, r, ctx->geo, ctx->coef, T, logT, KP, P, rowsplit, ntiles, rinv_in_lds, ctx->scratch)
   if (!rowsplit) GRAM_LAUNCH(PPW_MAX);
   else if (P == 1) GRAM_LAUNCH(1);
   else if (P <= 3) GRAM_LAUNCH(3);
