@@ -168,7 +168,7 @@ CASES = {
     # BASELINE sizes vs the reference's own fixtures (make_golden_large.py)
     "c2_res_old": lambda: envelope(1024, _large("c2", "res_old"), krylow_restart=20, max_iter=100, version="res_old"),
     "c2_res_new": lambda: envelope(1024, _large("c2", "res_new"), krylow_restart=20, max_iter=100, version="res_new"),
-    "head8192": lambda: envelope(8192, _large("head8192", "res_old"), threads=(8,), krylow_restart=20, max_iter=5,
+    "head8192": lambda: envelope(8192, _large("head8192", "res_old"), threads=(4, 8), krylow_restart=20, max_iter=5,
                                  version="res_old"),
     # golden N = 100 restart-20 runs (tests/test_gpu_solvers.py)
     **{f"bratu100_r20_{v}": (lambda v=v: envelope(100, _golden(f"bratu100_{v}_r20"), krylow_restart=20, max_iter=100,
