@@ -2524,9 +2524,8 @@ __global__ __launch_bounds__(BLOCK) void k_gram_scatter(const double* __restrict
 }
 
 __global__ __launch_bounds__(BLOCK) void k_gram_reduce(const double* __restrict__ partial, int nblk, int P,
-                                                       int rowsplit, int KP, double* __restrict__ Gout) {
+                                                       int PG, int KP, double* __restrict__ Gout) {
   const int nb = KP / 16;
-  const int PG = rowsplit ? P : 4 * PPW_MAX;
   for (int idx = blockIdx.x * BLOCK + threadIdx.x; idx < P * 256; idx += gridDim.x * BLOCK) {
     const int p = idx >> 8, li = idx & 255, lane = li >> 2, i = li & 3;
     const int grp = p / PG, pl = p % PG;
@@ -3485,7 +3484,14 @@ int gnk_gram(gnk_ctx* ctx, const double* u, const double* V, int64_t ldv, int k,
     return check_launch(ctx, "gram scatter");
   }
   const int rowsplit = P <= PPW_MAX ? 1 : 0;
-  const int groups = rowsplit ? 1 : (P + 4 * PPW_MAX - 1) / (4 * PPW_MAX);
+  // pair-split: the P pair tiles spread evenly over the 4 waves (PPW = ceil(P / 4), instantiated up
+  // to PPW_MAX; was 10 per wave, which left one wave of four idle at P = 28)
+  int ppw = PPW_MAX;
+  if (!rowsplit) {
+    const int want = (P + 3) / 4;
+    ppw = want <= 4 ? 4 : want <= 6 ? 6 : want <= 7 ? 7 : want <= 9 ? 9 : PPW_MAX;
+  }
+  const int groups = rowsplit ? 1 : (P + 4 * ppw - 1) / (4 * ppw);
   // tile rows: LDS tile <= ~40 KB for small KP (several WGs per CU), 64 rows otherwise
   int T = 256;
   while (T > 64 && size_t(T) * (KP + 1) * 8 > 40 * 1024) T >>= 1;
@@ -3502,15 +3508,20 @@ int gnk_gram(gnk_ctx* ctx, const double* u, const double* V, int64_t ldv, int k,
   const int wg_per_cu = std::max<int>(1, std::min<int>(4, int((160 * 1024) / lds)));
   int64_t nblk = std::min<int64_t>(ntiles, int64_t(ctx->num_cus) * wg_per_cu);
   nblk = std::max<int64_t>(nblk, 1);
-  const size_t per_group_pairs = rowsplit ? P : 4 * PPW_MAX;
+  const size_t per_group_pairs = rowsplit ? P : 4 * ppw;
   if (size_t(nblk) * groups * per_group_pairs * 256 > SCRATCH_DOUBLES) return fail(ctx, "gram: scratch too small");
   // algorithmic bytes: k basis columns + u (+ r), each 8 bytes per owned point
   TimedLaunch tl(ctx, GNK_TIMER_GRAM, 8.0 * double(nown) * double(k + 1 + (r ? 1 : 0)));
 #define GRAM_LAUNCH(PP)                                                                                    \
   hipLaunchKernelGGL(k_gram<PP>, dim3(unsigned(nblk), unsigned(groups)), dim3(BLOCK), lds, ctx->stream, u, V, ldv, \
                      k, rinv, r, ctx->geo, ctx->coef, T, logT, KP, P, rowsplit, ntiles, rinv_in_lds, ctx->scratch)
-  if (!rowsplit) GRAM_LAUNCH(PPW_MAX);
-  else if (P == 1) GRAM_LAUNCH(1);
+  if (!rowsplit) {
+    if (ppw == 4) GRAM_LAUNCH(4);
+    else if (ppw == 6) GRAM_LAUNCH(6);
+    else if (ppw == 7) GRAM_LAUNCH(7);
+    else if (ppw == 9) GRAM_LAUNCH(9);
+    else GRAM_LAUNCH(PPW_MAX);
+  } else if (P == 1) GRAM_LAUNCH(1);
   else if (P <= 3) GRAM_LAUNCH(3);
   else if (P <= 6) GRAM_LAUNCH(6);
   else GRAM_LAUNCH(PPW_MAX);
@@ -3520,7 +3531,7 @@ int gnk_gram(gnk_ctx* ctx, const double* u, const double* V, int64_t ldv, int k,
   if (rc) return rc;
   (void)hipMemsetAsync(G_out, 0, size_t(KP) * KP * sizeof(double), ctx->stream);
   hipLaunchKernelGGL(k_gram_reduce, dim3((P * 256 + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, ctx->stream, ctx->scratch,
-                     int(nblk), P, rowsplit, KP, G_out);
+                     int(nblk), P, int(per_group_pairs), KP, G_out);
   return check_launch(ctx, "gram reduce");
 }
 
