@@ -110,7 +110,7 @@ def test_sensitivity_fixture_is_consistent():
     assert not [n for n in need if n not in s]
 
 
-@pytest.mark.parametrize("case", ["bratu100_r20_res_old", "short256_r3_res_old"])
+@pytest.mark.parametrize("case", ["short256_r3_res_old"])
 def test_sensitivity_envelope_recomputed_live(case):
     """The cheap envelopes recomputed here agree with the committed file (same variants)."""
     live = MS.CASES[case]()
