@@ -171,10 +171,10 @@ CASES = {
     "head8192": lambda: envelope(8192, _large("head8192", "res_old"), threads=(4, 8), krylow_restart=20, max_iter=5,
                                  version="res_old"),
     # golden N = 100 restart-20 runs (tests/test_gpu_solvers.py)
-    **{f"bratu100_r20_{v}": (lambda v=v: envelope(100, _golden(f"bratu100_{v}_r20"), krylow_restart=20, max_iter=100,
-                                                  version=v)) for v in ("res_old", "res_new")},
+    **{f"bratu100_r20_{v}": (lambda v=v: envelope(100, _golden(f"bratu100_{v}_r20"), slabs=True, krylow_restart=20,
+                                                  max_iter=100, version=v)) for v in ("res_old", "res_new")},
     # short restart cycles at N = 256 (oracle reference)
-    **{f"short256_r{r}_{v}": (lambda r=r, v=v: envelope(256, None, krylow_restart=r, max_iter=40, version=v))
+    **{f"short256_r{r}_{v}": (lambda r=r, v=v: envelope(256, None, slabs=True, krylow_restart=r, max_iter=40, version=v))
        for r, v in ((3, "res_old"), (7, "res_old"), (5, "res_new"))},
     # multi-slab GPU test cases (tests/multislab_worker.py): single-rank oracle reference
     **{f"multislab{N}_{v}": (lambda N=N, v=v: envelope(N, None, slabs=True, krylow_restart=20, max_iter=45, version=v))
