@@ -13,14 +13,19 @@ reference's own result depends on the thread count):
   cholqr2       the least-squares step by CholeskyQR2 (R from the Cholesky factor of the Gram of A,
                 twice; Q^T y = R^-T A^T y) instead of Householder -- the same factorisation in exact
                 arithmetic, and the family the device solve belongs to;
+  cholqr2b<P>   the same with every Gram summed over P row blocks in order (P = 4, 64, 256: the
+                device's per-block partials; multi-slab / short-restart cases);
   slab<P>       every reduction ordered as a P-rank slab run (P = 2..8) orders it: TSQR over P row blocks
                 (Householder QR per block, QR of the stacked R factors) and the Krylov update's V^T g,
                 ||g|| summed block by block in rank order (multi-slab cases only).
 The per-iteration relative distance of every variant from the reference trajectory (the reference's
 own fixture where one exists -- tests/golden/golden.json, large_*.json -- else the 1-thread oracle)
-is recorded, and ``envelope`` is the per-iteration maximum over all variants.  tests/tolerances.py
-turns it into the bound max(1e-10, envelope); tests/test_oracle_sensitivity.py recomputes the cheap
-cases live and checks them against this file.
+is recorded, and ``envelope`` is the per-iteration maximum over all variants.  Where the signed
+distances are recorded too (``xs`` / ``rs``), ``diameter`` is the per-iteration spread of the whole
+family (the reference included): max - min of the signed distances, i.e. how far two equivalent
+roundings of the reference's arithmetic can land from each other -- this build being one more.
+tests/tolerances.py turns it into the bound max(1e-10, diameter) (else envelope);
+tests/test_oracle_sensitivity.py recomputes the cheap cases live and checks them against this file.
 
 Usage:  python tests/golden/make_sensitivity.py <case> [<case> ...]   (cases: see CASES; "all")
 """
@@ -71,6 +76,30 @@ def cholqr2_lls(A, y):
     return scipy.linalg.solve_triangular(R, z)
 
 
+def cholqr2_blocked(P):
+    """CholeskyQR2 with every Gram (A^T A, A^T y) accumulated over P row blocks in order -- the shape of
+    the device solve's reduction (per-block partials summed in a fixed order)."""
+    def gram(X, Y):
+        n = X.shape[0]
+        edges = np.linspace(0, n, P + 1).astype(int)
+        g = 0.0
+        for a, b in zip(edges[:-1], edges[1:]):
+            g = g + X[a:b].T @ Y[a:b]
+        return g
+
+    def lls(A, y):
+        R1 = scipy.linalg.cholesky(gram(A, A), lower=False)
+        Q1 = scipy.linalg.solve_triangular(R1, A.T, trans="T", lower=False).T
+        R2 = scipy.linalg.cholesky(gram(Q1, Q1), lower=False)
+        R = R2 @ R1
+        for r_kk in np.diagonal(R):
+            if np.isclose(r_kk, 0, atol=1e-8):
+                print("A is rank deficient")
+        z = scipy.linalg.solve_triangular(R, gram(A, y[:, None])[:, 0], trans="T", lower=False)
+        return scipy.linalg.solve_triangular(R, z)
+    return lls
+
+
 def slab_variant(N, P):
     """(lls, update) with every reduction split into the row slabs of a P-rank run, summed in rank order."""
     from gauss_newton_via_generalized_krylov_subspaces_amd.slab import row_partition
@@ -110,6 +139,7 @@ def variants(N, slabs=False):
          "cholqr2": (cholqr2_lls, _UPDATE)}
     if slabs:
         v.update({f"slab{P}": slab_variant(N, P) for P in range(2, 9)})
+        v.update({f"cholqr2b{P}": (cholqr2_blocked(P), _UPDATE) for P in (4, 64, 256)})
     return v
 
 
@@ -147,11 +177,94 @@ def envelope(N, ref=None, slabs=False, threads=THREADS, **kw):
     out = {}
     for name, (xs, rs, nf) in runs.items():
         n = min(len(xs), len(ref_x))
-        out[name] = {"x": (np.abs(xs[:n] - ref_x[:n]) / np.abs(ref_x[:n])).tolist(),
-                     "r": (np.abs(rs[:n] - ref_r[:n]) / np.abs(ref_r[:n])).tolist(), "nfev": nf}
-    n = min(len(v["x"]) for v in out.values())
-    env = {k: [max(v[k][i] for v in out.values()) for i in range(n)] for k in ("x", "r")}
-    return {"N": N, "kwargs": kw, "threads": list(threads), "variants": out, "envelope": env}
+        sx, sr = (xs[:n] - ref_x[:n]) / np.abs(ref_x[:n]), (rs[:n] - ref_r[:n]) / np.abs(ref_r[:n])
+        out[name] = {"x": np.abs(sx).tolist(), "r": np.abs(sr).tolist(), "xs": sx.tolist(), "rs": sr.tolist(),
+                     "nfev": nf}
+    res = {"N": N, "kwargs": kw, "threads": list(threads), "variants": out}
+    _summarise(res)
+    return res
+
+
+def _summarise(case):
+    """envelope (max |distance|) and, over the variants with signed distances, diameter (spread)."""
+    vs = case["variants"].values()
+    n = min(len(v["x"]) for v in vs)
+    case["envelope"] = {k: [max(v[k][i] for v in vs if k in v) for i in range(n)] for k in ("x", "r")}
+    signed = [v for v in vs if "xs" in v]
+    if signed:
+        m = min(len(v["xs"]) for v in signed)
+        case["diameter"] = {k: [max(0.0, max(v[k + "s"][i] for v in signed)) - min(0.0, min(v[k + "s"][i] for v in signed))
+                                for i in range(m)] for k in ("x", "r")}
+
+
+def _cg_with(dot):
+    """O.scipy_cg with every dot product / norm by ``dot`` (an equivalent summation order)."""
+    def cg(matvec, b, psolve=None, rtol=1e-5, maxiter=None, callback=None):
+        norm = lambda a: math.sqrt(dot(a, a))          # noqa: E731
+        bnrm2 = norm(b)
+        atol = max(0.0, float(rtol) * float(bnrm2))
+        if bnrm2 == 0:
+            return b, 0
+        maxiter = len(b) * 10 if maxiter is None else maxiter
+        x, r, rho_prev, p = np.zeros_like(b), b.copy(), None, None
+        for it in range(maxiter):
+            if norm(r) < atol:
+                return x, 0
+            z = r if psolve is None else psolve(r)
+            rho = dot(r, z)
+            if it > 0:
+                p *= rho / rho_prev
+                p += z
+            else:
+                p = z.copy()
+            q = matvec(p)
+            alpha = rho / dot(p, q)
+            x += alpha * p
+            r -= alpha * q
+            rho_prev = rho
+            if callback:
+                callback(x)
+        return x, maxiter
+    return cg
+
+
+def gn_envelope(N, threads=THREADS, **kw):
+    """Gauss-Newton + CGLS (ref:gauss_newton.py): the reference's CG with its dot products summed in
+    other orders -- numpy pairwise, reversed, P-slab blocks in rank order (P = 2..8) -- and at 1 / 8
+    BLAS threads; distances of ||x_k|| from the 1-thread reference."""
+    from gauss_newton_via_generalized_krylov_subspaces_amd.slab import row_partition
+    prob, y, u0 = O.bratu_workload(N)
+
+    def slab_dot(P):
+        sl = [slice(r0 * N, (r0 + nr) * N) for r0, nr in (row_partition(N, P, p) for p in range(P))]
+        return lambda a, b: sum((float(np.dot(a[q], b[q])) for q in sl), 0.0)
+
+    variants = {"base": O.scipy_cg, "pairwise": _cg_with(lambda a, b: float(np.sum(a * b))),
+                "reversed": _cg_with(lambda a, b: float(np.dot(a[::-1], b[::-1])))}
+    variants.update({f"slab{P}": _cg_with(slab_dot(P)) for P in range(2, 9)})
+
+    def traj(cg, t):
+        xs = []
+        orig = O.scipy_cg
+        O.scipy_cg = cg
+        try:
+            with threadpool_limits(limits=t, user_api="blas"), contextlib.redirect_stdout(io.StringIO()):
+                O.gauss_newton(prob.make_res(y), u0, prob.make_jac(),
+                               callback=lambda x, nfev, cg_iter: xs.append(np.linalg.norm(x)), **kw)
+        finally:
+            O.scipy_cg = orig
+        return np.array(xs)
+
+    runs = {f"{name}@{t}": traj(cg, t) for name, cg in variants.items() for t in (threads if name == "base" else (1,))}
+    ref = runs[f"base@{threads[0]}"]
+    out = {}
+    for name, xs in runs.items():
+        n = min(len(xs), len(ref))
+        sx = (xs[:n] - ref[:n]) / np.abs(ref[:n])
+        out[name] = {"x": np.abs(sx).tolist(), "xs": sx.tolist(), "r": [0.0] * n, "rs": [0.0] * n}
+    res = {"N": N, "kwargs": kw, "threads": list(threads), "variants": out}
+    _summarise(res)
+    return res
 
 
 def _golden(name):
@@ -179,6 +292,9 @@ CASES = {
     # multi-slab GPU test cases (tests/multislab_worker.py): single-rank oracle reference
     **{f"multislab{N}_{v}": (lambda N=N, v=v: envelope(N, None, slabs=True, krylow_restart=20, max_iter=45, version=v))
        for N in (256, 384) for v in ("res_old", "res_new", "jac_old_res_old", "jac_old_res_new")},
+    # multi-slab GN + CGLS cases (tests/multislab_worker.py)
+    **{f"gn{N}": (lambda N=N: gn_envelope(N, max_iter=4, cg_rtol=1e-4)) for N in (256, 384)},
+    **{f"gn{N}_pre": (lambda N=N: gn_envelope(N, max_iter=3, cg_rtol=1e-4, cg_preconditioner=True)) for N in (256, 384)},
 }
 
 
@@ -187,9 +303,7 @@ def store(case, res):
     if ONLY is not None and case in allc:                  # merge the recomputed variants
         old = allc[case]
         old["variants"].update(res["variants"])
-        n = min(len(v["x"]) for v in old["variants"].values())
-        old["envelope"] = {k: [max(v[k][i] for v in old["variants"].values() if k in v) for i in range(n)]
-                           for k in ("x", "r") if any(k in v for v in old["variants"].values())}
+        _summarise(old)
         res = old
     allc[case] = res
     with open(PATH, "w") as f:

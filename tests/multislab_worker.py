@@ -33,12 +33,15 @@ from gauss_newton_via_generalized_krylov_subspaces_amd.inputs import slab_inputs
 from gauss_newton_via_generalized_krylov_subspaces_amd.slab import Comm  # noqa: E402
 
 # ||x_k|| bound, multi-rank vs single-rank (every reduction summed in a different order): GNK at
-# max(1e-10, the envelope of the reference's own arithmetic reordered as 2 / 3 / 8 slabs order it,
-# permuted QR, exact k = 1 sums, 1 vs 8 BLAS threads -- tests/tolerances.py, cases
-# multislab<grid>_<version>); GN at 1e-10 (compensated CG dot products).
-def bound(kind, version, grid):
+# max(1e-10, the spread of the reference's own arithmetic reordered as 2 .. 8 slabs order it, permuted
+# QR, exact k = 1 sums, 1 vs 8 BLAS threads -- tests/tolerances.py, cases multislab<grid>_<version>);
+# GN + CGLS at max(1e-10, the spread of the reference's GN with its CG dot products summed in other
+# orders -- pairwise, reversed, 2 .. 8 slab blocks, 8 BLAS threads: cases gn<grid>[_pre]).
+def bound(kind, kw, grid):
     from tests import tolerances as T
-    return T.trajectory_bound(f"multislab{grid}_{version}") if kind == "gnk" else T.NORTH_STAR
+    if kind == "gnk":
+        return T.trajectory_bound(f"multislab{grid}_{kw['version']}")
+    return T.trajectory_bound(f"gn{grid}" + ("_pre" if kw.get("cg_preconditioner") else ""))
 
 
 BACKEND = None          # --numpy: the NumPy test double of the C-ABI (CPU rehearsal of this script)
@@ -130,7 +133,7 @@ def main():
         same = all(d[f] == s[f] for f in ("nit", "nrev", "njev", "success", "nfev", "stdout"))
         rel = float(np.max(np.abs(np.array(d["norms"]) - np.array(s["norms"])) / np.abs(s["norms"]))) \
             if len(d["norms"]) == len(s["norms"]) and s["norms"] else float("inf")
-        tol = bound(kind, kw.get("version"), N)
+        tol = bound(kind, kw, N)
         case_ok = same and ranks_equal and rel <= tol
         ok &= case_ok
         report.append({"case": kind, **kw, "world": world, "grid": N, "ranks_identical": ranks_equal,

