@@ -137,16 +137,18 @@ def variants(N, slabs=False):
     v = {"base": (_LLS, _UPDATE), "exact_k1": (lls_variant(True, None), _UPDATE),
          "perm7": (lls_variant(False, 7), _UPDATE), "perm8+k1": (lls_variant(True, 8), _UPDATE),
          "cholqr2": (cholqr2_lls, _UPDATE)}
+    v.update({f"cholqr2b{P}": (cholqr2_blocked(P), _UPDATE) for P in (4, 64, 256)})
     if slabs:
         v.update({f"slab{P}": slab_variant(N, P) for P in range(2, 9)})
-        v.update({f"cholqr2b{P}": (cholqr2_blocked(P), _UPDATE) for P in (4, 64, 256)})
     return v
 
 
 def trajectory(prob, y, u0, lls, update, threads, **kw):
     res = prob.make_res(y)
     xs, rs, nf = [], [], []
-    O.linear_least_squares, O.KrylovBasis.update = lls, update
+    O.linear_least_squares = lls
+    if update is not _UPDATE:
+        O.KrylovBasis.update = update
     try:
         with threadpool_limits(limits=threads, user_api="blas"), contextlib.redirect_stdout(io.StringIO()):
             O.gauss_newton_krylow(res, u0, prob.make_jac(), callback=lambda x, nfev, cg_iter: (
@@ -154,7 +156,9 @@ def trajectory(prob, y, u0, lls, update, threads, **kw):
     except O.StepLengthConvergenceError:
         pass
     finally:
-        O.linear_least_squares, O.KrylovBasis.update = _LLS, _UPDATE
+        O.linear_least_squares = _LLS
+        if update is not _UPDATE:
+            O.KrylovBasis.update = _UPDATE
     return np.array(xs), np.array(rs), nf
 
 
@@ -267,6 +271,29 @@ def gn_envelope(N, threads=THREADS, **kw):
     return res
 
 
+def mispredict_envelope(N):
+    """tests/test_mispredict.py's injected run (a rejected first trial at iteration 12, a breakdown at
+    15, ref:armijo_goldstein.py:53-62, ref:krylow.py:66-69) under the non-slab reorderings."""
+    from tests.test_mispredict import injected
+    prob, y, u0 = O.bratu_workload(N)
+    kw = dict(krylow_restart=20, max_iter=22, version="res_old")
+    runs = {}
+    for name, (lls, upd) in variants(N).items():
+        for t in THREADS:
+            with injected():
+                runs[f"{name}@{t}"] = trajectory(prob, y, u0, lls, upd, t, **kw)
+    ref_x, ref_r = runs[f"base@{THREADS[0]}"][:2]
+    out = {}
+    for name, (xs, rs, nf) in runs.items():
+        n = min(len(xs), len(ref_x))
+        sx, sr = (xs[:n] - ref_x[:n]) / np.abs(ref_x[:n]), (rs[:n] - ref_r[:n]) / np.abs(ref_r[:n])
+        out[name] = {"x": np.abs(sx).tolist(), "r": np.abs(sr).tolist(), "xs": sx.tolist(), "rs": sr.tolist(),
+                     "nfev": nf}
+    res = {"N": N, "kwargs": kw, "threads": list(THREADS), "variants": out}
+    _summarise(res)
+    return res
+
+
 def _golden(name):
     c = json.load(open(os.path.join(OUT, "golden.json")))["cases"][name]["per_iter"]
     return c["xnorm"], c["rnorm"]
@@ -292,6 +319,8 @@ CASES = {
     # multi-slab GPU test cases (tests/multislab_worker.py): single-rank oracle reference
     **{f"multislab{N}_{v}": (lambda N=N, v=v: envelope(N, None, slabs=True, krylow_restart=20, max_iter=45, version=v))
        for N in (256, 384) for v in ("res_old", "res_new", "jac_old_res_old", "jac_old_res_new")},
+    # the injected misprediction run of tests/test_mispredict.py
+    "mispredict1024": lambda: mispredict_envelope(1024),
     # multi-slab GN + CGLS cases (tests/multislab_worker.py)
     **{f"gn{N}": (lambda N=N: gn_envelope(N, max_iter=4, cg_rtol=1e-4)) for N in (256, 384)},
     **{f"gn{N}_pre": (lambda N=N: gn_envelope(N, max_iter=3, cg_rtol=1e-4, cg_preconditioner=True)) for N in (256, 384)},
