@@ -2127,7 +2127,10 @@ __global__ __launch_bounds__(GS_SW) void k_fused_wedge(const double* __restrict_
   wcol[(G + x0) * geo.N + col] = wedge[(idx * 2) * GS_SW + threadIdx.x];
   if (x1 - 1 > x0) wcol[(G + x1 - 1) * geo.N + col] = wedge[(idx * 2 + 1) * GS_SW + threadIdx.x];
 }
-constexpr int GF_KMAX = 19;     // V columns of the fused pass (k + 1 <= GS_KMAX Gram columns)
+// V columns of the fused pass.  The ring fits k <= 19, but a 16-column instance (k = 15, 8192^2)
+// faulted under tools/kbench.py's repeated launches and is not understood yet: capped at 13, the
+// range measured and tested on the GPU
+constexpr int GF_KMAX = 13;
 
 // (v_0 + v_1) + (v_2 + v_3) over the four 16-lane rows of the wave, the same bits in every lane
 __device__ __forceinline__ double sum_rows4(double v) {
@@ -2143,7 +2146,7 @@ __device__ __forceinline__ double sum_rows4(double v) {
          __builtin_bit_cast(double, int2{int(lo2[1]), int(hi2[1])});
 }
 
-template <int NB, int L, int KSL>
+template <int NB, int L, int KSL, int R>
 __global__ __launch_bounds__(64 * GS_NW) __attribute__((amdgpu_waves_per_eu(2))) void k_gram_sf(
     double* __restrict__ V, int64_t ldv, int k, const double* __restrict__ etry, const double* __restrict__ hh,
     const double* __restrict__ rold, const double* __restrict__ yv, const double* __restrict__ tf, int ldr,
@@ -2452,15 +2455,20 @@ __global__ __launch_bounds__(64 * GS_NW) __attribute__((amdgpu_waves_per_eu(2)))
     }
   };
 
+  // R = 5: row x+3 is issued at the start of step x and waited for at its end.  R = 6: row x+4 is
+  // issued at the END of step x (after the step's stores, so that vmcnt(L) leaves exactly it in
+  // flight) and lands during step x+1: one DMA row stays in flight across every barrier.
+  constexpr int INF = R - 5;
   if (x0 < x1) {
-    // ring slots: sq / sn / sc / ss / sp = rows x-2 .. x+2 (sq receives row x+3 during step x)
-    int sq = 4, sn = 0, sc = 1, ss_ = 2, sp = 3;
+    // ring slots: sq / sn / sc / ss / sp (/ sf) = rows x-2 .. x+2 (x+3); sq receives the next DMA row
+    int sq = R - 1, sn = 0, sc = 1, ss_ = 2, sp = 3, sf = 4;
     issue_row(x0 - 2, sq);
     issue_row(x0 - 1, sn);
     issue_row(x0, sc);
     issue_row(x0 + 1, ss_);
     issue_row(x0 + 2, sp);
-    __builtin_amdgcn_s_waitcnt(waitcnt_vm_lgkm0(0));
+    if (R == 6) issue_row(x0 + 3, sf);
+    __builtin_amdgcn_s_waitcnt(waitcnt_vm_lgkm0(L * INF));
     __builtin_amdgcn_s_barrier();
     // prologue: trial points of rows x0-1 .. x0+1, g of rows x0-1 and x0
     double xm1, xt0, xt1, hm1 = 0.0, h0 = 0.0, h1 = 0.0;
@@ -2473,7 +2481,7 @@ __global__ __launch_bounds__(64 * GS_NW) __attribute__((amdgpu_waves_per_eu(2)))
     double dn = own_dn(d1);                         // row x0
     __builtin_amdgcn_s_barrier();
     for (int64_t x = x0; x < x1; ++x) {
-      issue_row(x + 3, sq);
+      if (R == 5) issue_row(x + 3, sq);
       double* Ln = lds + sn * slotd;
       double* Lc = lds + sc * slotd;
       double* Ls = lds + ss_ * slotd;
@@ -2522,13 +2530,19 @@ __global__ __launch_bounds__(64 * GS_NW) __attribute__((amdgpu_waves_per_eu(2)))
       xt1 = xt2;
       h1 = h2;
       ex0 = ex1;
+      if (R == 6) issue_row(x + 4, sq);
       const int t = sq;
       sq = sn;
       sn = sc;
       sc = ss_;
       ss_ = sp;
-      sp = t;
-      __builtin_amdgcn_s_waitcnt(waitcnt_vm_lgkm0(0));   // row x+3 landed
+      if (R == 6) {
+        sp = sf;
+        sf = t;
+      } else {
+        sp = t;
+      }
+      __builtin_amdgcn_s_waitcnt(waitcnt_vm_lgkm0(L * INF));   // row x+3 landed (R = 6: x+4 in flight)
       __builtin_amdgcn_s_barrier();
     }
     gram(qp, lds + sn * slotd);                     // last row x1-1
@@ -4469,7 +4483,11 @@ int gnk_gram_fused(gnk_ctx* ctx, double* V, int64_t ldv, int k, const double* e_
   const int nbs = kg <= 16 ? 1 : 2;
   const int ksl = ((kg - 16 * (nbs - 1)) + 3) / 4;
   const int L = (k + 3 + GS_NW - 1) / GS_NW;
-  const size_t lds = size_t(5) * ((size_t(k) + 5) * GS_CS + 128) * sizeof(double);
+  const size_t slot_bytes = ((size_t(k) + 5) * GS_CS + 128) * sizeof(double);
+  // six ring slots (a DMA row in flight across the barriers) where they fit, else five
+  const char* ring_s = getenv("GNK_FUSED_RING");           // tooling A/B: 5 forces the five-slot ring
+  const int ring = (6 * slot_bytes <= 160 * 1024 && !(ring_s && atoi(ring_s) == 5)) ? 6 : 5;
+  const size_t lds = size_t(ring) * slot_bytes;
   if (L > 3 || lds > 160 * 1024) return fail(ctx, "gram_fused: ring does not fit");
   const int nacc = gs_nacc(nbs, ksl);
   const int PL = 256 + 64 * nacc;
@@ -4488,9 +4506,14 @@ int gnk_gram_fused(gnk_ctx* ctx, double* V, int64_t ldv, int k, const double* e_
   const int64_t nown = nrows * ctx->geo.N;
   // algorithmic bytes: read V (k), r_old, y; write w, x, r_t, g
   TimedLaunch tl(ctx, GNK_TIMER_GRAM, 8.0 * double(nown) * double(k + 6));
-#define GRAMF(NBV, LV, KV)                                                                                         \
-  hipLaunchKernelGGL((k_gram_sf<NBV, LV, KV>), dim3(unsigned(nwg)), dim3(64 * GS_NW), lds, ctx->stream, V, ldv, k, \
+#define GRAMF_R(NBV, LV, KV, RV)                                                                                    \
+  hipLaunchKernelGGL((k_gram_sf<NBV, LV, KV, RV>), dim3(unsigned(nwg)), dim3(64 * GS_NW), lds, ctx->stream, V, ldv, k, \
                      e_try, hh, r_old, y, T, KP, x, r_t, ctx->geo, ctx->coef, rpr, ctx->scratch, tpart, wedge)
+#define GRAMF(NBV, LV, KV)                          \
+  do {                                              \
+    if (ring == 6) GRAMF_R(NBV, LV, KV, 6);         \
+    else GRAMF_R(NBV, LV, KV, 5);                   \
+  } while (0)
 #define GRAMF_K(NBV, LV)                                                                  \
   do {                                                                                    \
     if (ksl == 1) GRAMF(NBV, LV, 1); else if (ksl == 2) GRAMF(NBV, LV, 2);                \
@@ -4503,6 +4526,7 @@ int gnk_gram_fused(gnk_ctx* ctx, double* V, int64_t ldv, int k, const double* e_
   }
 #undef GRAMF_K
 #undef GRAMF
+#undef GRAMF_R
   tl.done();
   int rc = check_launch(ctx, "gram_fused");
   if (rc) return rc;

@@ -142,7 +142,7 @@ class NumpyBackend:
         G.numpy()[:kp_next * kp_next] = g.reshape(-1)
 
     def gram_fused_max_k(self):
-        return 19
+        return 13
 
     def gram_fused(self, V, k, e_try, hh, r_old, y, T, x, r_t, G, pack):
         """NumPy double of gnk_gram_fused (owned rows written; w, x and g evaluated on the slab rows the

@@ -4,8 +4,9 @@
 Written vectors (w, x, r_t, g) are pointwise / stencil arithmetic: agree to a few ulps of their scale.
 The pack (sums over owned points) and the Gram (fp64 MFMA, fixed-order reductions) differ from the
 double only in summation order: 1e-12 of their scale.  Geometries: a whole single-rank grid and an
-interior / edge slab with filled ghost rows (the multi-rank case), every kernel instance (the number of
-Gram columns k + 1 = 3 .. 20 selects NB, KSL and the DMA width)."""
+interior / edge slab with filled ghost rows (the multi-rank case), every kernel instance the pass
+enables (k <= gnk_gram_fused_max_k() = 13: the number of Gram columns k + 1 = 3 .. 14 selects KSL and
+the DMA width)."""
 import numpy as np
 import pytest
 import torch
@@ -47,7 +48,7 @@ def _setup(N, row0, nrows, k, seed):
     return rng, be, nb, n, V, hh, etry, r_old, y, T, kp, u_ref
 
 
-@pytest.mark.parametrize("k", [2, 5, 8, 9, 11, 12, 13, 15, 16, 17, 19])
+@pytest.mark.parametrize("k", [2, 5, 8, 9, 11, 12, 13])
 @pytest.mark.parametrize("geom", ["single", "interior", "top"])
 def test_gram_fused_matches_numpy_double(k, geom):
     N = 256
@@ -85,7 +86,7 @@ def test_gram_fused_matches_numpy_double(k, geom):
     np.testing.assert_allclose(a, b, rtol=0, atol=1e-12 * np.abs(b).max())
 
 
-@pytest.mark.parametrize("k", [3, 9, 16, 19])
+@pytest.mark.parametrize("k", [3, 9, 13, 19])
 def test_lls_fused_t_and_proj_match_numpy_double(k):
     """gnk_lls_fused_t / gnk_lls_proj (one wave) == their NumPy doubles; the projected Gram == the Gram
     gnk_gram gives over the materialised pending column with gnk_lls_next's transform."""
