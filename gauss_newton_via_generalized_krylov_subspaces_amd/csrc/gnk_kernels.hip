@@ -2146,12 +2146,13 @@ __device__ __forceinline__ double sum_rows4(double v) {
          __builtin_bit_cast(double, int2{int(lo2[1]), int(hi2[1])});
 }
 
-template <int NB, int L, int KSL, int R>
+template <int NB, int L, int KSL>
 __global__ __launch_bounds__(64 * GS_NW) __attribute__((amdgpu_waves_per_eu(2))) void k_gram_sf(
     double* __restrict__ V, int64_t ldv, int k, const double* __restrict__ etry, const double* __restrict__ hh,
     const double* __restrict__ rold, const double* __restrict__ yv, const double* __restrict__ tf, int ldr,
     double* __restrict__ xout, double* __restrict__ rout, Geo geo, Coef cf, int64_t rpr,
-    double* __restrict__ partial, double* __restrict__ tpart, double* __restrict__ wedge) {
+    double* __restrict__ partial, double* __restrict__ tpart, double* __restrict__ wedge,
+    double* __restrict__ trash) {
   constexpr int NACC = gs_nacc(NB, KSL);
   constexpr int TMAX = NB == 2 ? 4 * KSL : 0;
   constexpr int ER = NB * TMAX, RR = ER + NB;
@@ -2321,8 +2322,9 @@ __global__ __launch_bounds__(64 * GS_NW) __attribute__((amdgpu_waves_per_eu(2)))
     wv = Lp[oV + (k - 1) * sV] - sw;
     xv = fma(wv, ekp, sx);
   };
-  // B: w and x of grid row xr (ring slot Lp) at point e (and the halo point in waves 0 / 7)
-  auto trial_row = [&](double* Lp, int64_t xr, double& xe, double& xh) {
+  // B: w and x of grid row xr (ring slot Lp) at point e (and the halo point in waves 0 / 7); direct:
+  // store them (the prologue), else the step loop stores them one step later (see st_ptr)
+  auto trial_row = [&](double* Lp, int64_t xr, double& xe, double& xh, double& we, bool direct) {
     double wv, xv;
     trial_pt(Lp, e, GS_CS, wv, xv);
     const bool own = xr >= x0 && xr < x1;
@@ -2332,17 +2334,20 @@ __global__ __launch_bounds__(64 * GS_NW) __attribute__((amdgpu_waves_per_eu(2)))
       if (own) {
         // the range's first and last rows are read as raw g by the neighbouring ranges' blocks:
         // staged in wedge, copied into V after the pass (k_fused_wedge)
-        if (xr == x0 || xr == x1 - 1) wedge[(size_t(idx) * 2 + (xr == x0 ? 0 : 1)) * GS_SW + e] = wv;
-        else wcol[gi] = wv;
+        if (direct) {
+          if (xr == x0 || xr == x1 - 1) wedge[(size_t(idx) * 2 + (xr == x0 ? 0 : 1)) * GS_SW + e] = wv;
+          else wcol[gi] = wv;
+        }
         ss += wv * wv;
         mx = nan_max(mx, fabs(wv));
       }
     }
     if (wr_x) {
       Lp[RX * GS_CS + e] = xv;
-      if (own) xout[gi] = xv;
+      if (own && direct) xout[gi] = xv;
     }
     xe = xv;
+    we = wv;
     if (hwave) {
       double wh, xhv;
       trial_pt(Lp, hb + hs, 4, wh, xhv);
@@ -2360,7 +2365,7 @@ __global__ __launch_bounds__(64 * GS_NW) __attribute__((amdgpu_waves_per_eu(2)))
   // C: g of grid row xr (r_old rows xr-1 / xr / xr+1 in slots Lq / Lr / Ls) from x(xr) at the task point;
   // d1 = jdiag(x), ex1 = LAMBDA exp(x) (the residual's exp term)
   auto g_row = [&](const double* Lq, double* Lr, const double* Ls, int64_t xr, double xt, double& d1,
-                   double& ex1) -> double {
+                   double& ex1, bool direct) -> double {
     ex1 = cf.lam_zero ? 0.0 : cf.lam * exp(xt);
     d1 = cf.lam_zero ? cf.j_lin_diag : cf.j_lin_diag + ex1;
     const int64_t grow = geo.row0 + xr;
@@ -2368,12 +2373,12 @@ __global__ __launch_bounds__(64 * GS_NW) __attribute__((amdgpu_waves_per_eu(2)))
     if (grow < 0 || grow >= N || !cin) gv = 0.0;
     if (wr_g) {
       Lr[oG] = gv;
-      if (!hl && xr >= x0 && xr < x1) gcol[(G + xr) * N + col0 + e] = gv;
+      if (direct && !hl && xr >= x0 && xr < x1) gcol[(G + xr) * N + col0 + e] = gv;
     }
     return gv;
   };
   // D: r_t of grid row xr at point e (pde_operator in fwd_pt's order, with the trial point's exp)
-  auto r_row = [&](const double* Ln_, double* Lc_, double xc, double xs_, double exc, int64_t xr) {
+  auto r_row = [&](const double* Ln_, double* Lc_, double xc, double xs_, double exc) -> double {
     double l = 0.0 + cf.l_off * Ln_[oXc];
     if (fhw) l = l + cf.l_off * Lc_[oXw];
     l = l + cf.l_diag * xc;
@@ -2386,9 +2391,9 @@ __global__ __launch_bounds__(64 * GS_NW) __attribute__((amdgpu_waves_per_eu(2)))
     const double rt = Lc_[RY * GS_CS + e] - f;
     if (wr_r) {
       Lc_[RT * GS_CS + e] = rt;
-      rout[(G + xr) * N + col0 + e] = rt;
       rr += rt * rt;
     }
+    return rt;
   };
   // the fragments' diagonal -jdiag at point e (lanes of the g stencil at a halo point take it from
   // the same point's lane in the next group)
@@ -2399,6 +2404,14 @@ __global__ __launch_bounds__(64 * GS_NW) __attribute__((amdgpu_waves_per_eu(2)))
       if (hl) dn = dno;
     }
     return dn;
+  };
+  // the residual's exp term at point e, the same way
+  auto own_ex = [&](double ex) {
+    if (hwave) {
+      const double o = __shfl_xor(ex, 16);
+      if (hl) ex = o;
+    }
+    return ex;
   };
 
   double a[NB][4];
@@ -2455,42 +2468,62 @@ __global__ __launch_bounds__(64 * GS_NW) __attribute__((amdgpu_waves_per_eu(2)))
     }
   };
 
-  // R = 5: row x+3 is issued at the start of step x and waited for at its end.  R = 6: row x+4 is
-  // issued at the END of step x (after the step's stores, so that vmcnt(L) leaves exactly it in
-  // flight) and lands during step x+1: one DMA row stays in flight across every barrier.
-  constexpr int INF = R - 5;
+  // Row x+3 is issued at the start of step x and waited for at its end.  The step's global stores
+  // (w, x at row x+2, g at row x+1, r_t at row x: one quantity per lane group, so one store
+  // instruction per wave) are issued at the start of the NEXT step, right after its DMA, so that the
+  // end-of-step vmcnt(1) waits for the DMA but not for the stores; lanes with nothing to store write
+  // their own word of `trash` (the count of vector-memory instructions per step stays fixed).
+  const int gw_ = (hg + 1) & 3, gx_ = (hg + 2) & 3, gg_ = (hg + 3) & 3;
+  double* const trash_l = trash + size_t(blockIdx.x) * (64 * GS_NW) + tid;
+  double* st_ptr = trash_l;
+  double st_val = 0.0;
   if (x0 < x1) {
-    // ring slots: sq / sn / sc / ss / sp (/ sf) = rows x-2 .. x+2 (x+3); sq receives the next DMA row
-    int sq = R - 1, sn = 0, sc = 1, ss_ = 2, sp = 3, sf = 4;
+    // ring slots: sq / sn / sc / ss / sp = rows x-2 .. x+2; sq receives row x+3 during step x
+    int sq = 4, sn = 0, sc = 1, ss_ = 2, sp = 3;
     issue_row(x0 - 2, sq);
     issue_row(x0 - 1, sn);
     issue_row(x0, sc);
     issue_row(x0 + 1, ss_);
     issue_row(x0 + 2, sp);
-    if (R == 6) issue_row(x0 + 3, sf);
-    __builtin_amdgcn_s_waitcnt(waitcnt_vm_lgkm0(L * INF));
+    __builtin_amdgcn_s_waitcnt(waitcnt_vm_lgkm0(0));
     __builtin_amdgcn_s_barrier();
-    // prologue: trial points of rows x0-1 .. x0+1, g of rows x0-1 and x0
-    double xm1, xt0, xt1, hm1 = 0.0, h0 = 0.0, h1 = 0.0;
-    trial_row(lds + sn * slotd, x0 - 1, xm1, hm1);
-    trial_row(lds + sc * slotd, x0, xt0, h0);
-    trial_row(lds + ss_ * slotd, x0 + 1, xt1, h1);
+    // prologue: trial points of rows x0-1 .. x0+1, g of rows x0-1 and x0 (stored directly)
+    double xm1, xt0, xt1, hm1 = 0.0, h0 = 0.0, h1 = 0.0, wdum;
+    trial_row(lds + sn * slotd, x0 - 1, xm1, hm1, wdum, true);
+    trial_row(lds + sc * slotd, x0, xt0, h0, wdum, true);
+    trial_row(lds + ss_ * slotd, x0 + 1, xt1, h1, wdum, true);
     double d1, ex0, exm;
-    (void)g_row(lds + sq * slotd, lds + sn * slotd, lds + sc * slotd, x0 - 1, hl ? hm1 : xm1, d1, exm);
-    (void)g_row(lds + sn * slotd, lds + sc * slotd, lds + ss_ * slotd, x0, hl ? h0 : xt0, d1, ex0);
+    (void)g_row(lds + sq * slotd, lds + sn * slotd, lds + sc * slotd, x0 - 1, hl ? hm1 : xm1, d1, exm, true);
+    (void)g_row(lds + sn * slotd, lds + sc * slotd, lds + ss_ * slotd, x0, hl ? h0 : xt0, d1, ex0, true);
+    ex0 = own_ex(ex0);
     double dn = own_dn(d1);                         // row x0
+    __builtin_amdgcn_s_waitcnt(waitcnt_vm_lgkm0(0));
     __builtin_amdgcn_s_barrier();
     for (int64_t x = x0; x < x1; ++x) {
-      if (R == 5) issue_row(x + 3, sq);
+      issue_row(x + 3, sq);
+      asm volatile("" ::: "memory");                // the store stays behind the DMA (vmcnt order)
+      *st_ptr = st_val;                             // the previous step's store (or trash)
       double* Ln = lds + sn * slotd;
       double* Lc = lds + sc * slotd;
       double* Ls = lds + ss_ * slotd;
       double* Lp = lds + sp * slotd;
-      double xt2, h2 = 0.0;
-      trial_row(Lp, x + 2, xt2, h2);                // B: row x+2
+      double xt2, h2 = 0.0, w2;
+      trial_row(Lp, x + 2, xt2, h2, w2, false);     // B: row x+2
       double d1n, ex1;
-      const double gnext = g_row(Lc, Ls, Lp, x + 1, hl ? h1 : xt1, d1n, ex1);   // C: row x+1
-      r_row(Ln, Lc, xt0, xt1, ex0, x);              // D: row x
+      const double gnext = g_row(Lc, Ls, Lp, x + 1, hl ? h1 : xt1, d1n, ex1, false);   // C: row x+1
+      const double rt = r_row(Ln, Lc, xt0, xt1, ex0);  // D: row x
+      {
+        // next step's store: lane group gw_ -> w(x+2), gx_ -> x(x+2), gg_ -> g(x+1), hg -> r_t(x)
+        const int64_t r2 = (G + x + 2) * N + col0 + e, r1 = (G + x + 1) * N + col0 + e;
+        const int64_t r0 = (G + x) * N + col0 + e;
+        const bool own2 = x + 2 < x1, own1 = x + 1 < x1;
+        double* pw = own2 ? (x + 2 == x1 - 1 ? wedge + (size_t(idx) * 2 + 1) * GS_SW + e : wcol + r2) : trash_l;
+        double* px = own2 ? xout + r2 : trash_l;
+        double* pg = own1 ? gcol + r1 : trash_l;
+        double* pr = rout + r0;
+        st_ptr = cq == gw_ ? pw : (cq == gx_ ? px : (cq == gg_ ? pg : pr));
+        st_val = cq == gw_ ? w2 : (cq == gx_ ? xt2 : (cq == gg_ ? gnext : rt));
+      }
       const double gcur = Lc[RG * GS_CS + e];       // g(x) at point e (step x-1)
 #pragma unroll
       for (int ab = 0; ab < NB; ++ab)
@@ -2529,22 +2562,17 @@ __global__ __launch_bounds__(64 * GS_NW) __attribute__((amdgpu_waves_per_eu(2)))
       xt0 = xt1;
       xt1 = xt2;
       h1 = h2;
-      ex0 = ex1;
-      if (R == 6) issue_row(x + 4, sq);
+      ex0 = own_ex(ex1);
       const int t = sq;
       sq = sn;
       sn = sc;
       sc = ss_;
       ss_ = sp;
-      if (R == 6) {
-        sp = sf;
-        sf = t;
-      } else {
-        sp = t;
-      }
-      __builtin_amdgcn_s_waitcnt(waitcnt_vm_lgkm0(L * INF));   // row x+3 landed (R = 6: x+4 in flight)
+      sp = t;
+      __builtin_amdgcn_s_waitcnt(waitcnt_vm_lgkm0(1));   // row x+3 landed (this step's store may fly)
       __builtin_amdgcn_s_barrier();
     }
+    *st_ptr = st_val;                               // the last step's store
     gram(qp, lds + sn * slotd);                     // last row x1-1
   }
   __builtin_amdgcn_s_waitcnt(waitcnt_vm_lgkm0(0));
@@ -4484,10 +4512,7 @@ int gnk_gram_fused(gnk_ctx* ctx, double* V, int64_t ldv, int k, const double* e_
   const int ksl = ((kg - 16 * (nbs - 1)) + 3) / 4;
   const int L = (k + 3 + GS_NW - 1) / GS_NW;
   const size_t slot_bytes = ((size_t(k) + 5) * GS_CS + 128) * sizeof(double);
-  // six ring slots (a DMA row in flight across the barriers) where they fit, else five
-  const char* ring_s = getenv("GNK_FUSED_RING");           // tooling A/B: 5 forces the five-slot ring
-  const int ring = (6 * slot_bytes <= 160 * 1024 && !(ring_s && atoi(ring_s) == 5)) ? 6 : 5;
-  const size_t lds = size_t(ring) * slot_bytes;
+  const size_t lds = size_t(5) * slot_bytes;
   if (L > 3 || lds > 160 * 1024) return fail(ctx, "gram_fused: ring does not fit");
   const int nacc = gs_nacc(nbs, ksl);
   const int PL = 256 + 64 * nacc;
@@ -4499,21 +4524,18 @@ int gnk_gram_fused(gnk_ctx* ctx, double* V, int64_t ldv, int k, const double* e_
   const int64_t nwg = nstrips * nranges;
   const size_t toff = (size_t(nwg) * PL + 1) & ~size_t(1);
   const size_t eoff = toff + size_t(nwg) * GF_TPL;
-  if (nwg > 4096 || eoff + size_t(nwg) * 2 * GS_SW > SCRATCH_DOUBLES - size_t(PL))
+  const size_t xoff = eoff + size_t(nwg) * 2 * GS_SW;
+  if (nwg > 4096 || xoff + size_t(nwg) * 64 * GS_NW > SCRATCH_DOUBLES - size_t(PL))
     return fail(ctx, "gram_fused: scratch too small");
   double* tpart = ctx->scratch + toff;
   double* wedge = ctx->scratch + eoff;
+  double* trash = ctx->scratch + xoff;             // per-thread sink of the deferred stores
   const int64_t nown = nrows * ctx->geo.N;
   // algorithmic bytes: read V (k), r_old, y; write w, x, r_t, g
   TimedLaunch tl(ctx, GNK_TIMER_GRAM, 8.0 * double(nown) * double(k + 6));
-#define GRAMF_R(NBV, LV, KV, RV)                                                                                    \
-  hipLaunchKernelGGL((k_gram_sf<NBV, LV, KV, RV>), dim3(unsigned(nwg)), dim3(64 * GS_NW), lds, ctx->stream, V, ldv, k, \
-                     e_try, hh, r_old, y, T, KP, x, r_t, ctx->geo, ctx->coef, rpr, ctx->scratch, tpart, wedge)
-#define GRAMF(NBV, LV, KV)                          \
-  do {                                              \
-    if (ring == 6) GRAMF_R(NBV, LV, KV, 6);         \
-    else GRAMF_R(NBV, LV, KV, 5);                   \
-  } while (0)
+#define GRAMF(NBV, LV, KV)                                                                                          \
+  hipLaunchKernelGGL((k_gram_sf<NBV, LV, KV>), dim3(unsigned(nwg)), dim3(64 * GS_NW), lds, ctx->stream, V, ldv, k, \
+                     e_try, hh, r_old, y, T, KP, x, r_t, ctx->geo, ctx->coef, rpr, ctx->scratch, tpart, wedge, trash)
 #define GRAMF_K(NBV, LV)                                                                  \
   do {                                                                                    \
     if (ksl == 1) GRAMF(NBV, LV, 1); else if (ksl == 2) GRAMF(NBV, LV, 2);                \
@@ -4526,7 +4548,6 @@ int gnk_gram_fused(gnk_ctx* ctx, double* V, int64_t ldv, int k, const double* e_
   }
 #undef GRAMF_K
 #undef GRAMF
-#undef GRAMF_R
   tl.done();
   int rc = check_launch(ctx, "gram_fused");
   if (rc) return rc;
