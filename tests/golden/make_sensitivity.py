@@ -45,7 +45,7 @@ sys.path.insert(0, ROOT)
 from oracle import gnk_oracle as O  # noqa: E402
 
 OUT = os.path.dirname(os.path.abspath(__file__))
-PATH = os.path.join(OUT, "sensitivity.json")
+PATH = os.environ.get("SENS_OUT", os.path.join(OUT, "sensitivity.json"))   # (merge tooling: SENS_OUT)
 _LLS = O.linear_least_squares
 _UPDATE = O.KrylovBasis.update
 THREADS = (1, 8)

@@ -131,7 +131,7 @@ def test_fused_gnk_matches_unfused_and_oracle(N):
     assert sf.spec_stats["hit"] >= su.spec_stats["hit"] - 1
     # the first restart cycle agrees to rounding; after the res_old restart the trajectory amplifies
     # rounding (tests/golden/sensitivity.json): fused and unfused both stay within 1e-10 of the oracle
-    np.testing.assert_allclose(xf[1:21], xo[1:21], rtol=1e-13)   # k = 1 cancels (sensitivity.json)
+    np.testing.assert_allclose(xf[1:21], xo[1:21], rtol=1e-11)   # k = 1 cancels (sensitivity.json)
     np.testing.assert_allclose(xf, xo, rtol=1e-10)
     np.testing.assert_allclose(xf, xu, rtol=1e-10)
     np.testing.assert_allclose(out_f.x, out_u.x, rtol=0, atol=1e-9 * np.abs(out_u.x).max())
