@@ -2115,6 +2115,9 @@ __global__ __launch_bounds__(64 * GS_NW) __attribute__((amdgpu_waves_per_eu(WPE)
 // neighbours of the computed rows (halo entries of w, x and g) come from a second trial-point round
 // in waves 0 and 7 (points -1 / 128) and from one lane group of those waves in the g stencil.
 constexpr int GF_TPL = 24;      // trial partial per block: [sum r^2, sum w^2, max |w|, h_0 .. h_{k-1}]
+#ifndef GNK_FDBG
+#define GNK_FDBG 0      // tooling-only ablation builds of the fused pass (tools/abl_fused.sh): 1 = no trial-point
+#endif                  // sums, 2 = no g stencil / exp, 4 = no r_t stencil, 8 = no halo round
 
 // the fused pass's pending column on the first / last row of every row range (staged by k_gram_sf)
 __global__ __launch_bounds__(GS_SW) void k_fused_wedge(const double* __restrict__ wedge, double* __restrict__ wcol,
@@ -2310,6 +2313,11 @@ __global__ __launch_bounds__(64 * GS_NW) __attribute__((amdgpu_waves_per_eu(2)))
 
   // trial point at one point (offset oV, column stride sV): w and x from this group's columns
   auto trial_pt = [&](const double* Lp, int oV, int sV, double& wv, double& xv) {
+    if (GNK_FDBG & 1) {
+      wv = Lp[oV + (k - 1) * sV];
+      xv = wv;
+      return;
+    }
     double sw = 0.0, sx = 0.0;
 #pragma unroll
     for (int s = 0; s < JS; ++s) {
@@ -2348,7 +2356,7 @@ __global__ __launch_bounds__(64 * GS_NW) __attribute__((amdgpu_waves_per_eu(2)))
     }
     xe = xv;
     we = wv;
-    if (hwave) {
+    if (hwave && !(GNK_FDBG & 8)) {
       double wh, xhv;
       trial_pt(Lp, hb + hs, 4, wh, xhv);
       if (!hin) {
@@ -2366,10 +2374,10 @@ __global__ __launch_bounds__(64 * GS_NW) __attribute__((amdgpu_waves_per_eu(2)))
   // d1 = jdiag(x), ex1 = LAMBDA exp(x) (the residual's exp term)
   auto g_row = [&](const double* Lq, double* Lr, const double* Ls, int64_t xr, double xt, double& d1,
                    double& ex1, bool direct) -> double {
-    ex1 = cf.lam_zero ? 0.0 : cf.lam * exp(xt);
+    ex1 = (cf.lam_zero || (GNK_FDBG & 2)) ? xt : cf.lam * exp(xt);
     d1 = cf.lam_zero ? cf.j_lin_diag : cf.j_lin_diag + ex1;
     const int64_t grow = geo.row0 + xr;
-    double gv = -vjp_pt(cf, d1, Lq[oRc], Lr[oRw], cw, Lr[oRc], Lr[oRe], ce, Ls[oRc]);
+    double gv = (GNK_FDBG & 2) ? Lr[oRc] : -vjp_pt(cf, d1, Lq[oRc], Lr[oRw], cw, Lr[oRc], Lr[oRe], ce, Ls[oRc]);
     if (grow < 0 || grow >= N || !cin) gv = 0.0;
     if (wr_g) {
       Lr[oG] = gv;
@@ -2379,6 +2387,11 @@ __global__ __launch_bounds__(64 * GS_NW) __attribute__((amdgpu_waves_per_eu(2)))
   };
   // D: r_t of grid row xr at point e (pde_operator in fwd_pt's order, with the trial point's exp)
   auto r_row = [&](const double* Ln_, double* Lc_, double xc, double xs_, double exc) -> double {
+    if (GNK_FDBG & 4) {
+      const double rt = Lc_[RY * GS_CS + e] - xc;
+      if (wr_r) Lc_[RT * GS_CS + e] = rt;
+      return rt;
+    }
     double l = 0.0 + cf.l_off * Ln_[oXc];
     if (fhw) l = l + cf.l_off * Lc_[oXw];
     l = l + cf.l_diag * xc;

@@ -246,6 +246,9 @@ def gn_envelope(N, threads=THREADS, **kw):
     variants = {"base": O.scipy_cg, "pairwise": _cg_with(lambda a, b: float(np.sum(a * b))),
                 "reversed": _cg_with(lambda a, b: float(np.dot(a[::-1], b[::-1])))}
     variants.update({f"slab{P}": _cg_with(slab_dot(P)) for P in range(2, 9)})
+    if os.environ.get("GN_VARIANTS"):                  # (tooling: a subset, e.g. for a quick recompute)
+        keep = set(os.environ["GN_VARIANTS"].split(","))
+        variants = {k: v for k, v in variants.items() if k in keep or k == "base"}
 
     def traj(cg, t):
         xs = []
