@@ -116,7 +116,9 @@ def main():
     del one, F
     cases = [("gnk", dict(krylow_restart=20, max_iter=a.iters, version=v))
              for v in ("res_old", "res_new", "jac_old_res_old", "jac_old_res_new")]
-    cases.append(("gn", dict(max_iter=4, cg_rtol=1e-4)))
+    from tests import tolerances as T
+    if f"gn{N}" in T.sensitivity():               # unpreconditioned GN: evidence recorded at grid 256
+        cases.append(("gn", dict(max_iter=4, cg_rtol=1e-4)))
     cases.append(("gn", dict(max_iter=3, cg_rtol=1e-4, cg_preconditioner=True)))
     mine = [run(kind, prob, y, u0, Comm(), **kw) for kind, kw in cases]
     staging = staged_vs_host(prob, y, u0, Comm(), steps=24)

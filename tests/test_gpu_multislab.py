@@ -3,7 +3,7 @@
 Each case starts fresh child processes (torch.distributed.run, gloo with host-staged collectives:
 RCCL refuses two ranks on one device) that run the HIP kernels on real slabs -- row0 > 0,
 halo-filled ghost rows, rank-ordered reductions -- for GNK (all four versions, restart 20) and GN
-(with and without Jacobi), then compare with the single-rank solve (tests/multislab_worker.py):
+(with Jacobi; without it too at grid 256, where its sensitivity case is recorded), then compare with the single-rank solve (tests/multislab_worker.py):
 bookkeeping and printed messages identical, every rank identical, per-iteration ||x_k|| within the
 bounds the oracle sensitivity tests back; per-rank staged inputs (inputs.py) reproduce the full-grid
 inputs' run bit for bit.  World 8 is the C4 rank count (8 x 32 rows of a 256^2 grid).
