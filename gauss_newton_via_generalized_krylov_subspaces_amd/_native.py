@@ -19,6 +19,9 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("GNK_LIB", os.path.join(_HERE, "libgnk.so"))
 GHOST = 2  # GNK_GHOST_ROWS
 TIMER_GRAM, TIMER_JVP, TIMER_CG_MATVEC = 1, 2, 3  # GNK_TIMER_*
+ABI_VERSION = 2  # GNK_ABI_VERSION
+# GNK_TUNE_* keys of gnk_set_tuning (tests / A/B tooling only; the solver never sets them)
+TUNE = {"gram_path": 0, "gram_ring": 1, "gram_v1min": 2, "cg_matvec": 3, "vjpg_blocks": 4, "gram_wide": 5}
 
 _c_int, _c_i64, _c_dbl, _c_vp = ctypes.c_int, ctypes.c_int64, ctypes.c_double, ctypes.c_void_p
 
@@ -29,6 +32,9 @@ SIGNATURES = {
     "gnk_ctx_destroy": (None, [_c_vp]),
     "gnk_last_error": (ctypes.c_char_p, [_c_vp]),
     "gnk_set_stream": (_c_int, [_c_vp, _c_vp]),
+    "gnk_set_reduce_pairs": (_c_int, [_c_vp, _c_int]),
+    "gnk_set_tuning": (_c_int, [_c_vp, _c_int, _c_int]),
+    "gnk_scratch_doubles": (_c_i64, []),
     "gnk_set_bratu": (_c_int, [_c_vp, _c_i64, _c_i64, _c_i64, _c_dbl, _c_dbl, _c_dbl]),
     "gnk_slab_len": (_c_i64, [_c_vp]),
     "gnk_bratu_jvp": (_c_int, [_c_vp, _c_vp, _c_vp, _c_vp]),
@@ -105,7 +111,7 @@ def load_library(path: str = LIB_PATH):
         fn = getattr(lib, name)  # AttributeError = missing export
         fn.restype = res
         fn.argtypes = args
-    if lib.gnk_abi_version() != 1:
+    if lib.gnk_abi_version() != ABI_VERSION:
         raise NativeLibraryError("libgnk.so ABI version mismatch")
     if path == LIB_PATH:
         _LIB = lib
@@ -133,6 +139,7 @@ class HipBackend:
             raise NativeLibraryError(f"gnk_ctx_create failed ({rc})")
         self.ctx = ctx
         self._stream = None
+        self.pairs = False
 
     def __del__(self):
         try:
@@ -156,6 +163,18 @@ class HipBackend:
     def _call(self, name, *args):
         self._sync_stream()
         self._chk(getattr(self.lib, name)(self.ctx, *args), name)
+
+    def set_reduce_pairs(self, on: bool):
+        """Compensated reductions return unevaluated (s, c) pairs (gnk_set_reduce_pairs)."""
+        self._chk(self.lib.gnk_set_reduce_pairs(self.ctx, int(bool(on))), "set_reduce_pairs")
+        self.pairs = bool(on)
+
+    def set_tuning(self, key: str, value: int):
+        """Kernel-choice override for tests / A/B tooling (gnk_set_tuning; 0 restores the default)."""
+        self._chk(self.lib.gnk_set_tuning(self.ctx, TUNE[key], int(value)), "set_tuning")
+
+    def scratch_doubles(self) -> int:
+        return int(self.lib.gnk_scratch_doubles())
 
     # --- problem ---------------------------------------------------------------
     def set_bratu(self, N, row0, nrows, h, alpha, lam):

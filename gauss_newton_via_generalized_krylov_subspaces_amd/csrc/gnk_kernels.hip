@@ -1300,7 +1300,7 @@ template <int NB, int BC, int CHT>
 __global__ __launch_bounds__(BLOCK) void k_gram_w(const double* __restrict__ u, const double* __restrict__ V,
                                                   int64_t ldv, int k, const double* __restrict__ rinv,
                                                   const double* __restrict__ r, Geo geo, Coef c,
-                                                  int64_t nchunks, double* __restrict__ partial, int dbg) {
+                                                  int64_t nchunks, double* __restrict__ partial) {
   // NB column blocks of 16 (KP = 16 NB), P = NB (NB + 1) / 2 Gram pair tiles; every block / pair
   // loop below is compile-time so the MFMA loops unroll and their LDS reads issue ahead.
   // CHT rows per wave chunk; a lane holds 2 consecutive rows (16-B loads); LPC = CHT/2 lanes
@@ -1357,22 +1357,14 @@ __global__ __launch_bounds__(BLOCK) void k_gram_w(const double* __restrict__ u, 
     const double dn0 = -jdiag(c, uu.x), dn1 = -jdiag(c, uu.y);
     for (int j0 = 0; j0 < k; j0 += CG * BC) {
       d2 vn[BC], vw[BC], vc[BC], ve[BC], vs[BC];
-      if (dbg & 1) {
 #pragma unroll
-        for (int q = 0; q < BC; ++q) {
-          const double t = 1e-3 * (lane + q + j0);
-          vn[q] = vw[q] = vc[q] = ve[q] = vs[q] = d2{t, -t};
-        }
-      } else {
-#pragma unroll
-        for (int q = 0; q < BC; ++q) {
-          const double* cp = V + min(j0 + CG * q + cg, k - 1) * ldv + i;
-          vn[q] = *reinterpret_cast<const d2*>(cp - N);
-          vw[q] = *reinterpret_cast<const d2*>(cp - 1);    // (i-1, i)
-          vc[q] = *reinterpret_cast<const d2*>(cp);
-          ve[q] = *reinterpret_cast<const d2*>(cp + 1);    // (i+1, i+2)
-          vs[q] = *reinterpret_cast<const d2*>(cp + N);
-        }
+      for (int q = 0; q < BC; ++q) {
+        const double* cp = V + min(j0 + CG * q + cg, k - 1) * ldv + i;
+        vn[q] = *reinterpret_cast<const d2*>(cp - N);
+        vw[q] = *reinterpret_cast<const d2*>(cp - 1);    // (i-1, i)
+        vc[q] = *reinterpret_cast<const d2*>(cp);
+        ve[q] = *reinterpret_cast<const d2*>(cp + 1);    // (i+1, i+2)
+        vs[q] = *reinterpret_cast<const d2*>(cp + N);
       }
 #pragma unroll
       for (int q = 0; q < BC; ++q) {
@@ -1422,7 +1414,7 @@ __global__ __launch_bounds__(BLOCK) void k_gram_w(const double* __restrict__ u, 
         }
       }
     }
-    if (!(dbg & 2)) {
+    {
       const double* rowbase = Wt + (lane >> 4) * S + (lane & 15);
 #pragma unroll
       for (int r4 = 0; r4 < CHT; r4 += 4) {
@@ -1806,9 +1798,6 @@ __global__ __launch_bounds__(BLOCK) void k_gram_m(const double* __restrict__ u, 
 // and blocks in a fixed order, like the MFMA tile.
 // GS_CS = 144 == 16 (mod 32): the A-fragment reads of a half-wave (16 points x 2 columns) hit
 // 64 distinct banks.
-#ifndef GNK_SDBG
-#define GNK_SDBG 0      // tooling-only ablation builds (tools/abl_build.sh): 1 = no DMA in the step
-#endif                  // loop, 2 = no stencil fragments, 4 = no MFMAs
 constexpr int GS_SW = 128;
 constexpr int GS_CS = 144;
 constexpr int GS_NW = 8;
@@ -2010,7 +1999,7 @@ __global__ __launch_bounds__(64 * GS_NW) __attribute__((amdgpu_waves_per_eu(WPE)
     __builtin_amdgcn_s_barrier();
     double dn = -jdiag(cf, lds[sc * slotd + ou]);
     for (int64_t x = x0; x < x1; ++x) {
-      if (!(GNK_SDBG & 1)) issue_row(x + R - 2, sd);
+      issue_row(x + R - 2, sd);
       const double* Ln = lds + sn * slotd;
       const double* Lc = lds + sc * slotd;
       const double* Ls = lds + ss * slotd;
@@ -2018,7 +2007,6 @@ __global__ __launch_bounds__(64 * GS_NW) __attribute__((amdgpu_waves_per_eu(WPE)
       for (int ab = 0; ab < NB; ++ab)
 #pragma unroll
         for (int ks = 0; ks < nks(ab); ++ks) {
-          if (GNK_SDBG & 2) { a[ab][ks] = dn; continue; }
           const int o = fo[ab][ks];
           const double vn = Ln[o], vw = Lc[fw[ab][ks]], vc = Lc[o], ve = Lc[fe[ab][ks]], vs = Ls[o];
           // J V with explicit FMAs in CSR term order (as k_gram_w).  Only the last fragment can hold
@@ -2044,13 +2032,8 @@ __global__ __launch_bounds__(64 * GS_NW) __attribute__((amdgpu_waves_per_eu(WPE)
         }
       dn = -jdiag(cf, Ls[ou]);                        // row x+1 (its u is in the ring)
       d4 qv[NB];
-      if (GNK_SDBG & 4) {
-#pragma unroll
-        for (int cb = 0; cb < NB; ++cb) qv[cb] = d4{a[0][0], a[0][0], a[0][0], a[0][0]};
-      } else {
-        transform(qv);
-        if (x > x0) gram(qp, Ln);                     // rows of x-1: r is in slot n
-      }
+      transform(qv);
+      if (x > x0) gram(qp, Ln);                       // rows of x-1: r is in slot n
 #pragma unroll
       for (int cb = 0; cb < NB; ++cb) qp[cb] = qv[cb];
       const int t = sn;
@@ -2066,7 +2049,7 @@ __global__ __launch_bounds__(64 * GS_NW) __attribute__((amdgpu_waves_per_eu(WPE)
       __builtin_amdgcn_s_waitcnt(waitcnt_vm_lgkm0(L * INF));  // row x+2 landed (R = 5: x+3 in flight)
       __builtin_amdgcn_s_barrier();
     }
-    if (!(GNK_SDBG & 4)) gram(qp, lds + sn * slotd);  // last row x1-1 (its slot is now sn)
+    gram(qp, lds + sn * slotd);                       // last row x1-1 (its slot is now sn)
   }
   __builtin_amdgcn_s_waitcnt(waitcnt_vm_lgkm0(0));
   __builtin_amdgcn_s_barrier();
@@ -3365,6 +3348,10 @@ struct gnk_ctx {
   double* ident = nullptr;     // 16², 32², 48², 64² identities (RinvAug of an unpreconditioned pass)
   int num_cus = 256;
   std::string err;
+  // gnk_set_reduce_pairs: compensated reductions written as unevaluated (s, c) pairs
+  int pairs = 0;
+  // gnk_set_tuning (tooling A/B of kernel choices; 0 = the product's choice)
+  int tune[GNK_TUNE_COUNT] = {};
   // per-launch timer (tooling, see gnk_timer_start)
   int timer_kernel = 0;
   int timer_count = 0;
@@ -3467,11 +3454,14 @@ int reduce(gnk_ctx* ctx, const double* partial, int nblk, int len, int stride, c
 
 // Compensated reduction of nblk blocks of (s, c) pairs: quantity j of block b at
 // partial[2 j + b * sb + {0, 1}] -> out[j] = s + c (k_wave_reduce2; two stages above 4096 blocks).
+// With ctx->pairs the result stays the unevaluated pair: out[2 j] = s_j, out[2 j + 1] = c_j (the
+// caller merges ranks' pairs, slab.Comm.sum_pairs).
 int wreduce2(gnk_ctx* ctx, const double* partial, int nblk, int len, int64_t sb, double* out) {
   constexpr int SPAN = 4096;
+  const int final = ctx->pairs ? 0 : 1;
   if (nblk <= SPAN) {
-    hipLaunchKernelGGL(k_wave_reduce2, dim3(len, 1), dim3(64), 0, ctx->stream, partial, nblk, nblk, sb, int64_t(2), 1,
-                       out);
+    hipLaunchKernelGGL(k_wave_reduce2, dim3(len, 1), dim3(64), 0, ctx->stream, partial, nblk, nblk, sb, int64_t(2),
+                       final, out);
     return check_launch(ctx, "reduce2");
   }
   const int nsplit = (nblk + SPAN - 1) / SPAN;
@@ -3481,7 +3471,7 @@ int wreduce2(gnk_ctx* ctx, const double* partial, int nblk, int len, int64_t sb,
   int rc = check_launch(ctx, "reduce2 stage 1");
   if (rc) return rc;
   hipLaunchKernelGGL(k_wave_reduce2, dim3(len, 1), dim3(64), 0, ctx->stream, tmp, nsplit, nsplit, int64_t(2),
-                     int64_t(2) * nsplit, 1, out);
+                     int64_t(2) * nsplit, final, out);
   return check_launch(ctx, "reduce2 stage 2");
 }
 
@@ -3503,12 +3493,14 @@ const int* pack_flags() {
   return static_cast<const int*>(p);
 }
 
-// {sum x^2, max |x|} of k_stats partials ([s, c, max] per block)
+// {sum x^2, max |x|} of k_stats partials ([s, c, max] per block); ctx->pairs: {s, c, max |x|}
 int reduce_stats(gnk_ctx* ctx, const double* partial, int nblk, double* stats_out) {
   int rc = wreduce2(ctx, partial, nblk, 1, 3, stats_out);
   if (rc) return rc;
-  return wreduce(ctx, partial + 2, nblk, 1, 3, 1, 0, sum_max_flags() + 1, stats_out + 1);
+  return wreduce(ctx, partial + 2, nblk, 1, 3, 1, 0, sum_max_flags() + 1, stats_out + (ctx->pairs ? 2 : 1));
 }
+
+int tuning(const gnk_ctx* ctx, int key) { return ctx->tune[key]; }
 
 // flat geometry helpers (generic problems)
 bool ctx_ok(gnk_ctx* ctx) { return ctx != nullptr; }
@@ -3568,6 +3560,21 @@ void gnk_ctx_destroy(gnk_ctx* ctx) {
 }
 
 const char* gnk_last_error(const gnk_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+
+int gnk_set_reduce_pairs(gnk_ctx* ctx, int on) {
+  if (!ctx) return -1;
+  ctx->pairs = on ? 1 : 0;
+  return 0;
+}
+
+int gnk_set_tuning(gnk_ctx* ctx, int key, int value) {
+  if (!ctx) return -1;
+  if (key < 0 || key >= GNK_TUNE_COUNT) return fail(ctx, "gnk_set_tuning: unknown key");
+  ctx->tune[key] = value;
+  return 0;
+}
+
+int64_t gnk_scratch_doubles(void) { return int64_t(SCRATCH_DOUBLES); }
 
 int gnk_set_stream(gnk_ctx* ctx, void* stream) {
   if (!ctx) return -1;
@@ -3682,8 +3689,8 @@ int gnk_vjp_gemv_t(gnk_ctx* ctx, const double* u, const double* r, const double*
   // one chunk of the smallest compiled width >= k up to 24 columns, else 16-column chunks
   const int kct = k <= 24 ? std::max(4, (k + 3) / 4 * 4) : 16;
   const int nchunk = std::max(1, (k + kct - 1) / kct);
-  static const int cap_env = getenv("GNK_VJPG_CAP") ? atoi(getenv("GNK_VJPG_CAP")) : 0;  // tooling A/B switch
-  RowLaunch L = rows(ctx, G, ctx->geo.nrows, vec_of(ctx), cap_env ? cap_env : std::max(64, 2048 / nchunk));
+  const int cap = tuning(ctx, GNK_TUNE_VJPG_BLOCKS);
+  RowLaunch L = rows(ctx, G, ctx->geo.nrows, vec_of(ctx), cap > 0 ? cap : std::max(64, 2048 / nchunk));
   L.grid.z = nchunk;
   const int nblk = L.grid.x * L.grid.y;
   if (size_t(nblk) * nchunk * kct > SCRATCH_DOUBLES) return fail(ctx, "vjp_gemv_t: scratch too small");
@@ -3851,18 +3858,15 @@ int gnk_gram(gnk_ctx* ctx, const double* u, const double* V, int64_t ldv, int k,
   if (rinv && ldr != KP) return fail(ctx, "gram: rinv must be the kp x kp augmented inverse (ldr == kp)");
   const int nb = KP / 16;
   const int P = nb * (nb + 1) / 2;
-  // VALU pass for small k with r (every preconditioned pass at k <= 8); GNK_GRAM_VALU=0 disables it,
-  // GNK_GRAM_STAGED=2 (tests) forces the staged kernel instead
-  const char* valu_s = getenv("GNK_GRAM_VALU");
-  const char* staged_f = getenv("GNK_GRAM_STAGED");
-  const char* v1_s = getenv("GNK_GRAM_V1");        // 0: no one-point form (then k <= 8 only)
-  const int gv_kmax = (v1_s && atoi(v1_s) == 0) ? GV1_KMIN - 1 : GV_KMAX;
-  if (r && k <= gv_kmax && ctx->geo.N % GV_SW == 0 && !(valu_s && atoi(valu_s) == 0) &&
-      !(staged_f && atoi(staged_f) == 2) && !getenv("GNK_DEBUG_GRAM")) {
+  // VALU pass for small k with r (every preconditioned pass at k <= 9); tuning GNK_TUNE_GRAM_PATH
+  // 3 disables it, 1 (tests) forces the staged kernel instead
+  const int path = tuning(ctx, GNK_TUNE_GRAM_PATH);
+  const int v1t = tuning(ctx, GNK_TUNE_GRAM_V1MIN);          // tooling A/B: first k of the one-point form
+  const int gv_kmax = v1t < 0 ? GV1_KMIN - 1 : GV_KMAX;
+  if (r && k <= gv_kmax && ctx->geo.N % GV_SW == 0 && path != 3 && path != 1) {
     const double* tv = rinv ? rinv : ctx->ident + ident_offset(KP / 16);
-    const char* v1min_s = getenv("GNK_GRAM_V1MIN");       // tooling A/B: first k of the one-point form
-    const int v1min = v1min_s ? std::max(7, atoi(v1min_s)) : GV1_KMIN;
-    const bool one_pt = k >= v1min && !(v1_s && atoi(v1_s) == 0);
+    const int v1min = v1t > 0 ? std::max(7, v1t) : GV1_KMIN;
+    const bool one_pt = k >= v1min && v1t >= 0;
     const int64_t nstrips = ctx->geo.N / (one_pt ? 64 : GV_SW);
     const int64_t nrows = ctx->geo.nrows;
     // about 8 waves per CU, whole row ranges per strip
@@ -3911,11 +3915,8 @@ int gnk_gram(gnk_ctx* ctx, const double* u, const double* V, int64_t ldv, int k,
   }
   // staged kernel (measured faster than the chunked / marching kernels for the preconditioned
   // pass from k = 4 up; the marching kernel stays faster for the plain pass);
-  // GNK_GRAM_STAGED=2 forces it for every pass (tests), 0 disables it
-  const char* staged_s = getenv("GNK_GRAM_STAGED");        // read per call: tests force the kernel
-  const int staged_env = staged_s ? atoi(staged_s) : 1;
-  if (staged_env && (staged_env == 2 || (rinv && k >= 4)) && k <= GS_KMAX && ctx->geo.N % GS_SW == 0 &&
-      !getenv("GNK_DEBUG_GRAM")) {
+  // tuning GNK_TUNE_GRAM_PATH 1 forces it for every pass (tests), 2 disables it
+  if (path != 2 && (path == 1 || (rinv && k >= 4)) && k <= GS_KMAX && ctx->geo.N % GS_SW == 0) {
     const int nbs = k <= 16 ? 1 : 2;                        // MFMA transform blocks of the V columns
     const int nrow = k + 1 + (r ? 1 : 0);
     const int L = (nrow + 1 + GS_NW - 1) / GS_NW;
@@ -3923,9 +3924,8 @@ int gnk_gram(gnk_ctx* ctx, const double* u, const double* V, int64_t ldv, int k,
     // CU, else 4 slots if that makes two blocks fit, else 5 slots at one block per CU.  Two blocks
     // need <= 128 VGPRs, which KSL = 4 only reaches by spilling (measured 1.2-1.5x slower), so the
     // 4-slot ring is for KSL <= 3: k = 12 with r, 1.98 ms vs 2.31 ms at 8192^2.
-    // GNK_GRAM_RING=5 / 4 forces a depth (tooling A/B).
-    const char* ring_s = getenv("GNK_GRAM_RING");
-    const int ring_env = ring_s ? atoi(ring_s) : 0;
+    // tuning GNK_TUNE_GRAM_RING 5 / 4 forces a depth (tooling A/B).
+    const int ring_env = tuning(ctx, GNK_TUNE_GRAM_RING);
     const size_t slot_bytes = (size_t(nrow) * GS_CS + 128) * sizeof(double);
     const size_t half_lds = 80 * 1024;
     int ring = 5;
@@ -3986,13 +3986,9 @@ int gnk_gram(gnk_ctx* ctx, const double* u, const double* V, int64_t ldv, int k,
     }
   }
   if (KP <= 64) {
-    // wave-independent streaming kernel (GNK_DEBUG_GRAM: tooling-only ablation switch,
-    // 1 = no loads, 2 = no Gram MFMAs)
-    static const int dbg = getenv("GNK_DEBUG_GRAM") ? atoi(getenv("GNK_DEBUG_GRAM")) : 0;
-    static const int bc_env = getenv("GNK_GRAM_BC") ? atoi(getenv("GNK_GRAM_BC")) : 0;   // tooling A/B switch
-    static const int ch_env = getenv("GNK_GRAM_CH") ? atoi(getenv("GNK_GRAM_CH")) : 0;
+    // wave-independent streaming kernel
     // chunk height: 64 rows for one column block, 32 rows above (LDS tile 32 x (KP+1) per wave)
-    const int chv = (ch_env == 32 || ch_env == 64) ? ch_env : (KP <= 32 ? 64 : 32);   // instantiated heights
+    const int chv = KP <= 32 ? 64 : 32;
     const int nwave = 4;
     size_t ldsw = size_t(nwave) * chv * (KP + 1) * 8 + (rinv ? size_t(KP) * KP * 8 : 0);
     ldsw = std::max(ldsw, size_t(P) * 256 * 8);
@@ -4004,13 +4000,12 @@ int gnk_gram(gnk_ctx* ctx, const double* u, const double* V, int64_t ldv, int k,
     int64_t nblk = std::min<int64_t>((nch + nwave - 1) / nwave, int64_t(ctx->num_cus) * wg_per_cu);
     nblk = std::max<int64_t>(nblk, 1);
     if (size_t(nblk) * P * 256 > SCRATCH_DOUBLES) return fail(ctx, "gram: scratch too small");
-    const int bc = bc_env ? bc_env : (chv == 64 ? (nb == 1 ? 2 : 4) : 2);
-    static const int march_env = getenv("GNK_GRAM_MARCH") ? atoi(getenv("GNK_GRAM_MARCH")) : 1;
+    const int bc = chv == 64 ? (nb == 1 ? 2 : 4) : 2;
     // marching kernel: NB <= 2, strips of 64 (NB = 1) / 32 (NB = 2) columns, <= 8 columns per lane
     const int chm = nb == 1 ? 64 : 32;
     const int64_t nstrips = ctx->geo.N / chm;
     // (NB = 2 with the in-place transform keeps too few waves resident to win: chunked kernel)
-    if (march_env && (nb == 1 || (nb == 2 && !rinv)) && !dbg && ctx->geo.N % chm == 0 &&
+    if ((nb == 1 || (nb == 2 && !rinv)) && ctx->geo.N % chm == 0 &&
         k <= 8 * (64 / (chm / 2))) {
       const int nwm = 4;
       size_t ldsm = size_t(nwm) * chm * (KP + 1) * 8 + (rinv ? size_t(KP) * KP * 8 : 0);
@@ -4057,9 +4052,9 @@ int gnk_gram(gnk_ctx* ctx, const double* u, const double* V, int64_t ldv, int k,
     // block; at 8192^2, k = 51 / 61 with P^-1 and r: 23.0 / 24.5 ms vs 31.4 / 33.4 ms).  For NB <= 3
     // k_gram_w runs two waves per SIMD and stays ahead (k = 33: 12.4 vs 16.7 ms), so it keeps those.
     // 16-row chunks (less LDS and fewer registers per wave) and two waves per SIMD measured slower
-    // for every NB (k = 51: 24.4 ms).  GNK_GRAM_WP=0 / 2: tooling A/B (never / also for NB = 2, 3)
-    static const int wp_env = getenv("GNK_GRAM_WP") ? atoi(getenv("GNK_GRAM_WP")) : 1;
-    if (wp_env && !dbg && !ch_env && !bc_env && (nb == 4 || (wp_env == 2 && nb >= 2))) {
+    // for every NB (k = 51: 24.4 ms).  Tuning GNK_TUNE_GRAM_WIDE 1 / 2: never / also for NB = 2, 3
+    const int wide = tuning(ctx, GNK_TUNE_GRAM_WIDE);
+    if (wide != 1 && (nb == 4 || (wide == 2 && nb >= 2))) {
       constexpr int chp = 32;
       size_t ldsp = size_t(nwave) * chp * (KP + 1) * 8 + (rinv ? size_t(KP) * KP * 8 : 0);
       ldsp = std::max(ldsp, size_t(P) * 256 * 8);
@@ -4091,7 +4086,7 @@ int gnk_gram(gnk_ctx* ctx, const double* u, const double* V, int64_t ldv, int k,
     TimedLaunch tl(ctx, GNK_TIMER_GRAM, 8.0 * double(nown) * double(k + 1 + (r ? 1 : 0)));
 #define GRAMW1(NBV, BCV, CHV) hipLaunchKernelGGL((k_gram_w<NBV, BCV, CHV>), dim3(unsigned(nblk)), dim3(64 * nwave), \
                                                  ldsw, ctx->stream, u, V, ldv, k, rinv, r, ctx->geo, ctx->coef,     \
-                                                 nch, ctx->scratch, dbg)
+                                                 nch, ctx->scratch)
 #define GRAMW(PP)                                                  \
   do {                                                             \
     if (chv == 64) {                                               \
@@ -4340,9 +4335,8 @@ int gnk_flat_gram(gnk_ctx* ctx, const double* W, int64_t ldw, int k, const doubl
 
 int gnk_cg_normal_matvec(gnk_ctx* ctx, const double* d, const double* p, double* q, double* pq_out) {
   if (!ready(ctx)) return -1;
-  const char* cgm_s = getenv("GNK_CG_MATVEC");            // tooling A/B: 0 = the point-wise kernel
   int nblk;
-  if (ctx->geo.N % 2 == 0 && !(cgm_s && atoi(cgm_s) == 0)) {
+  if (ctx->geo.N % 2 == 0 && tuning(ctx, GNK_TUNE_CG_MATVEC) != 1) {
     const int64_t nbc = (ctx->geo.N + 4 * CGM_SW - 1) / (4 * CGM_SW);
     const int64_t nrows = ctx->geo.nrows;
     int64_t nranges = std::max<int64_t>(1, std::min<int64_t>(nrows, int64_t(ctx->num_cus) * 8 / nbc));

@@ -38,7 +38,12 @@ from .slab import Comm
 
 class BratuGNOps:
     """Problem side of GN / CGLS for the matrix-free Bratu problem (slab vectors on this rank):
-    the fused 13-point J^T J p stencil, the closed-form diag(J^T J), halos of p."""
+    the fused 13-point J^T J p stencil, the closed-form diag(J^T J), halos of p.
+
+    The CG scalars (p.q, r.r, r.z) and the squared norms are compensated (Dot2) sums on the device;
+    this rank's context returns them as unevaluated (s, c) pairs (gnk_set_reduce_pairs) and the ranks'
+    pairs are merged with TwoSum in rank order (slab.Comm.sum_pairs) before rounding, so a multi-rank
+    CG runs on the same exactly rounded scalars as a single rank (ref:gauss_newton.py:11-60)."""
 
     jacobian_is_free = True
 
@@ -48,8 +53,11 @@ class BratuGNOps:
         self.comm = self.dev.comm
         self.n_global = self.dev.slab.n_global
         self.y = None if y is None else self.dev.load(y)
-        self._s1 = self.dev.scalar(1)
-        self._s2 = self.dev.scalar(2)
+        self.be.set_reduce_pairs(True)
+        self._n1 = self.dev.scalar(1)              # residual sum of squares (plain reduction)
+        self._s1 = self.dev.scalar(2)              # one compensated pair
+        self._s2 = self.dev.scalar(4)              # two compensated pairs
+        self._st = self.dev.scalar(3)              # vec_stats: (s, c, max |x|)
         self.dvec = self.dev.vec()
         self._jd = None
 
@@ -59,14 +67,14 @@ class BratuGNOps:
     rvec = vec
 
     def scalar3(self):
-        return self.dev.scalar(3)
+        return self.dev.scalar(4)                  # [r.u, r.r] (plain) + the (s, c) pair of u.w
 
     def load(self, x0):
         return self.dev.load(x0)
 
     def residual(self, x, r) -> float:
-        self.be.residual(x, self.y, r, self._s1)
-        return float(self.comm.sum(self._s1)[0])
+        self.be.residual(x, self.y, r, self._n1)
+        return float(self.comm.sum(self._n1)[0])
 
     def to_host(self, x):
         return self.dev.slab.to_host(x)
@@ -87,9 +95,8 @@ class BratuGNOps:
         self.be.vec_axpy(x, t, d, out, True)                         # x + t d (whole slab)
 
     def sumsq(self, v) -> float:
-        self.be.vec_stats(v, self._s2)
-        s, _ = self.comm.sum_max(self._s2)
-        return s
+        self.be.vec_stats(v, self._st)
+        return float(self.comm.sum_pairs(self._st, 1)[0])
 
     # CG pieces
     def cg_rhs(self, u, y, b):
@@ -105,11 +112,11 @@ class BratuGNOps:
         sl = self.dev.slab
         self.comm.halo(p, sl.N, sl.nrows)
         self.be.cg_matvec(self.dvec, p, q, self._s1)
-        return float(self.comm.sum(self._s1)[0])
+        return float(self.comm.sum_pairs(self._s1, 1)[0])
 
     def cg_update_xr(self, alpha, p, q, x, r, dinv, z):
         self.be.cg_update_xr(alpha, p, q, x, r, dinv, z, self._s2)
-        rr, rz = self.comm.sum(self._s2)
+        rr, rz = self.comm.sum_pairs(self._s2, 2)
         return float(rr), float(rz)
 
     def cg_update_p(self, beta, first, z, p):
@@ -131,11 +138,11 @@ class BratuGNOps:
 
     def cg_step_matvec(self, z, p_in, p_out, q, beta, first, x, xalpha) -> float:
         self.be.cg_step_matvec(self.dvec, z, p_in, p_out, q, beta, first, x, xalpha, self._s1)
-        return float(self.comm.sum(self._s1)[0])
+        return float(self.comm.sum_pairs(self._s1, 1)[0])
 
     def cg_update_rz(self, alpha, q, r, dinv, z):
         self.be.cg_update_xr(alpha, None, q, None, r, dinv, z, self._s2)
-        rr, rz = self.comm.sum(self._s2)
+        rr, rz = self.comm.sum_pairs(self._s2, 2)
         return float(rr), float(rz)
 
     def cg_axpy(self, x, alpha, p):
@@ -143,12 +150,13 @@ class BratuGNOps:
 
     # single-reduction iteration (cg_variant="single_reduction"): the three scalars of one
     # iteration are partial sums in one device buffer, read with one collective
-    def cg_sr_update(self, alpha, beta, first, w, p, s, x, r, dinv, u, out):
-        self.be.cg_sr_update(alpha, beta, first, w, p, s, x, r, dinv, u, out)
+    def cg_sr_update(self, alpha, beta, first, w, p, s, x, r, dinv, u, buf):
+        self.be.cg_sr_update(alpha, beta, first, w, p, s, x, r, dinv, u, buf[0:2])
 
-    def cg_sr_matvec(self, u, w, out):
-        """w = A^T A u and u . w: the row-marching kernel (first-iteration form, p_out = u) when N is
-        even, else the point-wise one."""
+    def cg_sr_matvec(self, u, w, buf):
+        """w = A^T A u and u . w (into buf[2:4], a compensated pair): the row-marching kernel
+        (first-iteration form, p_out = u) when N is even, else the point-wise one."""
+        out = buf[2:4]
         sl = self.dev.slab
         self.comm.halo(u, sl.N, sl.nrows)
         if self.cg_fused:
@@ -159,7 +167,11 @@ class BratuGNOps:
             self.be.cg_matvec(self.dvec, u, w, out)
 
     def cg_sr_read(self, buf):
-        return self.comm.sum(buf)
+        parts = self.comm._gather(buf)                  # per rank [r.u, r.r, s(u.w), c(u.w)]
+        s = parts[0, :2].copy()
+        for p in range(1, parts.shape[0]):
+            s = s + parts[p, :2]                          # rank order, as Comm.sum
+        return float(s[0]), float(s[1]), float(self.comm.merge_pairs(parts[:, 2:4])[0])
 
 
 class DeviceCG:
@@ -303,13 +315,13 @@ class DeviceCG:
             return 0
         # u0 = M r0 (alpha = 0 update: x, r unchanged, p = u, s = w are overwritten below)
         w.zero_()
-        ops.cg_sr_update(0.0, 0.0, True, w, self.p, sv, self.x, self.r, dinv, u, buf[0:2])
-        ops.cg_sr_matvec(u, w, buf[2:3])
+        ops.cg_sr_update(0.0, 0.0, True, w, self.p, sv, self.x, self.r, dinv, u, buf)
+        ops.cg_sr_matvec(u, w, buf)
         gamma, rr, delta = ops.cg_sr_read(buf)
         alpha, beta, first = gamma / delta, 0.0, True
         for iteration in range(maxiter):
-            ops.cg_sr_update(alpha, beta, first, w, self.p, sv, self.x, self.r, dinv, u, buf[0:2])
-            ops.cg_sr_matvec(u, w, buf[2:3])
+            ops.cg_sr_update(alpha, beta, first, w, self.p, sv, self.x, self.r, dinv, u, buf)
+            ops.cg_sr_matvec(u, w, buf)
             gamma_new, rr, delta = ops.cg_sr_read(buf)
             cb()
             if math.sqrt(rr) < atol:

@@ -242,6 +242,12 @@ class HostCallableOps:
         if k > FLAT_GRAM_KMAX:
             raise NotImplementedError(f"generic problems: at most {FLAT_GRAM_KMAX} basis columns per "
                                       "least-squares solve (use krylow_restart)")
+        kp = self.be.gram_dim(k, r is not None)
+        if kp > 64 and kp * self.m > self.be.scratch_doubles():
+            # the wide pass materialises Y = W RinvAug (m x kp) in the library's scratch arena
+            raise NotImplementedError(f"generic problems: a {k}-column basis over {self.m} residuals exceeds the "
+                                      f"wide Gram's arena ({self.be.scratch_doubles()} doubles; use krylow_restart "
+                                      f"<= {max(1, self.be.scratch_doubles() // self.m - 1)})")
         if self._W is None or self._W.shape[0] < k:
             self._W = self.be.zeros(max(k, 8), self.m)
         J = self._jac_of(u)

@@ -125,7 +125,7 @@ class CholQR2Solver:
         self.history = []           # per solve: (k, passes, cond(R_Y) of each pass) -- diagnostics
         self.R_prev = None          # R of the last solve (k_prev x k_prev); None: no usable factor
         self.R_last = None          # R of the last solve (diagnostics)
-        self._tentative = None      # (R, d) of a solve over a pending column
+        self._tentative = None      # (R, d, singular) of a solve over a pending column
         # device solve (k_lls): k <= lsk
         self.lsk = (min(int(self.be.lls_max_k()), int(kmax))
                     if device_solve and hasattr(self.be, "lls_solve") else 0)
@@ -279,7 +279,7 @@ class CholQR2Solver:
             return None
         self.history.append((k, 1, [cond]))
         if ls.pending:
-            self._tentative = (R, d)
+            self._tentative = (R, d, False)
         else:
             self._settle(R)
         return d, jdd
@@ -361,7 +361,7 @@ class CholQR2Solver:
             d, jdd, R = self._min_norm(u, basis, k, M, r)
             self.history.append((k, self.passes - p0, conds + [np.inf]))
             if pending:
-                self._tentative = (R, d)
+                self._tentative = (R, d, True)           # resolve_pending drops R as a preconditioner
                 return d, jdd, R
             self._settle(R)
             self.R_prev = None                           # no usable preconditioner: CholQR2 next time
@@ -369,7 +369,12 @@ class CholQR2Solver:
         if self.min_norm_if_singular:
             # the dense lstsq branch: scipy.linalg.lstsq (gelsd, cond = eps) returns the minimum-norm
             # solution when J is rank-deficient; J = Q R, so that is R's truncated-SVD solution of
-            # R d' = z with the same cut-off (singular values <= eps sigma_max are zero)
+            # R d' = z with the same cut-off (singular values <= eps sigma_max are zero).  Where R
+            # comes from a shifted factorisation (a numerically singular Gram) its small singular
+            # values are lifted to ~ sqrt(11 n k eps) ||J|| and are no longer below that cut-off:
+            # for J with singular values between eps and ~sqrt(n k eps) of sigma_max this branch
+            # (like _min_norm, which truncates at the shift) keeps directions gelsd would drop --
+            # the two agree for exactly rank-deficient J (tests: rank-1 Jacobians), not in that band.
             U, S, Wt = np.linalg.svd(R)
             keep = S > EPS * S[0]
             if not np.all(keep):
@@ -383,7 +388,7 @@ class CholQR2Solver:
         jdd = float(np.sum((R @ d) ** 2))
         self.history.append((k, self.passes - p0, conds))
         if pending:
-            self._tentative = (R, d)
+            self._tentative = (R, d, False)
             return d, jdd, R
         self._settle(R)
         return d, jdd, R
@@ -413,12 +418,14 @@ class CholQR2Solver:
     def resolve_pending(self, nrm: float) -> np.ndarray:
         """The pending column was settled with norm nrm: R and d in reference units
         (column w -> w / nrm: R[:, -1] / nrm, d[-1] * nrm); prints; returns d."""
-        R, d = self._tentative
+        R, d, singular = self._tentative
         R = R.copy()
         d = d.copy()
         R[:, -1] /= nrm
         d[-1] *= nrm
         self._settle(R)
+        if singular:
+            self.R_prev = None                  # a rank-deficient factor does not precondition the next pass
         return d
 
     def discard_pending(self):

@@ -66,6 +66,16 @@ class Comm:
             s.add_(parts[p])
         return s
 
+    # -- transport: the two collectives of the data path (RCCL on GPUs, gloo on CPU) ---------
+    def _all_gather_into(self, buf: torch.Tensor, t: torch.Tensor):
+        dist.all_gather_into_tensor(buf, t, group=self.group)
+
+    def _p2p(self, ops):
+        """ops: (dist.isend | dist.irecv, tensor, peer) -> one batched P2P exchange, waited for."""
+        reqs = dist.batch_isend_irecv([dist.P2POp(op, t, peer, self.group) for op, t, peer in ops])
+        for req in reqs:
+            req.wait()
+
     # -- reductions -------------------------------------------------------------
     def _gather(self, t: torch.Tensor) -> np.ndarray:
         if self.world == 1:
@@ -74,8 +84,30 @@ class Comm:
         if self.stage:
             t = t.to("cpu")
         buf = torch.empty(self.world * t.numel(), dtype=t.dtype, device=t.device)
-        dist.all_gather_into_tensor(buf, t, group=self.group)
+        self._all_gather_into(buf, t)
         return buf.to("cpu").numpy().reshape(self.world, -1)
+
+    @staticmethod
+    def merge_pairs(parts: np.ndarray) -> np.ndarray:
+        """Rank-ordered compensated sum of per-rank unevaluated pairs: parts[p] = [s_0, c_0, s_1, c_1,
+        ...] (gnk_set_reduce_pairs).  The s are added with TwoSum in rank order, their rounding errors
+        and the c are accumulated beside them, and the result is rounded once at the end
+        (Ogita-Rump-Oishi Sum2): the device's Dot2 accuracy carried across ranks.  One rank: s + c,
+        the value the device itself returns without pairs."""
+        S = parts[0, 0::2].copy()
+        C = parts[0, 1::2].copy()
+        for p in range(1, parts.shape[0]):
+            sp, cp = parts[p, 0::2], parts[p, 1::2]
+            x = S + sp
+            z = x - S
+            err = (S - (x - z)) + (sp - z)
+            S = x
+            C = C + (err + cp)
+        return S + C
+
+    def sum_pairs(self, t: torch.Tensor, nq: int) -> np.ndarray:
+        """nq compensated per-rank sums given as (s, c) pairs in t[:2 nq] -> their sums over ranks."""
+        return self.merge_pairs(self._gather(t[:2 * nq]))
 
     def sum(self, t: torch.Tensor) -> np.ndarray:
         """Sum of a small per-rank tensor over ranks, in rank order (host result)."""
@@ -142,7 +174,7 @@ class Comm:
             gath = t.reshape(-1)
         else:
             gath = torch.empty(self.world * n, dtype=t.dtype, device=t.device)
-            dist.all_gather_into_tensor(gath, t.contiguous().reshape(-1), group=self.group)
+            self._all_gather_into(gath, t.contiguous().reshape(-1))
         wn = self.world * n
         host = pinned[:wn + m]
         host[:wn].copy_(gath, non_blocking=True)
@@ -195,7 +227,7 @@ class Comm:
             return torch.from_numpy(self.sum(t)).to(t.device)
         t = t.contiguous().reshape(-1)
         buf = torch.empty(self.world * t.numel(), dtype=t.dtype, device=t.device)
-        dist.all_gather_into_tensor(buf, t, group=self.group)
+        self._all_gather_into(buf, t)
         return self._sum_parts_device(buf, t.numel())
 
     def barrier(self):
@@ -213,13 +245,12 @@ class Comm:
         host = vec.to("cpu") if staged else vec
         ops = []
         if self.rank > 0:
-            ops.append(dist.P2POp(dist.isend, host[g:2 * g], self.rank - 1, self.group))
-            ops.append(dist.P2POp(dist.irecv, host[0:g], self.rank - 1, self.group))
+            ops.append((dist.isend, host[g:2 * g], self.rank - 1))
+            ops.append((dist.irecv, host[0:g], self.rank - 1))
         if self.rank < self.world - 1:
-            ops.append(dist.P2POp(dist.isend, host[own_end - g:own_end], self.rank + 1, self.group))
-            ops.append(dist.P2POp(dist.irecv, host[own_end:own_end + g], self.rank + 1, self.group))
-        for req in dist.batch_isend_irecv(ops):
-            req.wait()
+            ops.append((dist.isend, host[own_end - g:own_end], self.rank + 1))
+            ops.append((dist.irecv, host[own_end:own_end + g], self.rank + 1))
+        self._p2p(ops)
         if staged:
             if self.rank > 0:
                 vec[0:g].copy_(host[0:g])
@@ -237,7 +268,7 @@ class Comm:
         pad = torch.zeros(big, dtype=torch.float64, device=dev)
         pad[:owned.numel()] = owned.detach().reshape(-1)
         buf = torch.empty(self.world * big, dtype=torch.float64, device=dev)
-        dist.all_gather_into_tensor(buf, pad, group=self.group)
+        self._all_gather_into(buf, pad)
         del pad
         parts = buf.view(self.world, big)
         return torch.cat([parts[p, :sizes[p]] for p in range(self.world)]).to("cpu").numpy()

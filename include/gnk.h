@@ -33,7 +33,7 @@ extern "C" {
 #endif
 
 #define GNK_GHOST_ROWS 2
-#define GNK_ABI_VERSION 1
+#define GNK_ABI_VERSION 2
 
 typedef struct gnk_ctx gnk_ctx;
 
@@ -43,6 +43,31 @@ int gnk_ctx_create(int device, gnk_ctx** out);
 void gnk_ctx_destroy(gnk_ctx* ctx);
 const char* gnk_last_error(const gnk_ctx* ctx);
 int gnk_set_stream(gnk_ctx* ctx, void* hip_stream);
+/* Compensated (Dot2) reductions -- the CG scalars of gnk_cg_normal_matvec / gnk_cg_step_matvec /
+ * gnk_cg_update_xr and sum x**2 of gnk_vec_stats -- are normally returned as one
+ * double s + c.  With on != 0 they are returned as the unevaluated pair: out[2j] = s_j,
+ * out[2j+1] = c_j (gnk_vec_stats: {s, c, max|x|}), so a multi-rank caller can merge every rank's
+ * pair with TwoSum in rank order before rounding (slab.Comm.sum_pairs).  Default 0. */
+int gnk_set_reduce_pairs(gnk_ctx* ctx, int on);
+/* Kernel-choice overrides for tests and A/B tooling (value 0 = the library's own choice, the
+ * default; the solver never sets them):
+ *   GNK_TUNE_GRAM_PATH   1 = the staged MFMA Gram kernel for every pass it covers (k <= 20),
+ *                        2 = never the staged kernel, 3 = no all-VALU Gram kernels
+ *   GNK_TUNE_GRAM_RING   4 / 5 = LDS ring slots of the staged Gram kernel
+ *   GNK_TUNE_GRAM_V1MIN  first k of the one-point VALU Gram kernel (-1: never)
+ *   GNK_TUNE_CG_MATVEC   1 = the point-wise normal matvec instead of the row-marching one
+ *   GNK_TUNE_VJPG_BLOCKS cap on the blocks of gnk_vjp_gemv_t
+ *   GNK_TUNE_GRAM_WIDE   1 = never the prefetching wide Gram kernel, 2 = also for 2..3 column blocks */
+#define GNK_TUNE_GRAM_PATH 0
+#define GNK_TUNE_GRAM_RING 1
+#define GNK_TUNE_GRAM_V1MIN 2
+#define GNK_TUNE_CG_MATVEC 3
+#define GNK_TUNE_VJPG_BLOCKS 4
+#define GNK_TUNE_GRAM_WIDE 5
+#define GNK_TUNE_COUNT 6
+int gnk_set_tuning(gnk_ctx* ctx, int key, int value);
+/* doubles in the context's scratch arena (bounds the wide generic Gram: kp * m <= this) */
+int64_t gnk_scratch_doubles(void);
 
 /* Bratu slab geometry + coefficients.  h = grid_resolution, alpha = ALPHA,
  * lambda = LAMBDA of BratuPdeProblem (ref:bratu_pde_problem.py:20-67). */

@@ -1,0 +1,127 @@
+"""C4 at its size on ONE GPU: Bratu 32768^2 row-partitioned over 8 ranks (BASELINE configs[3]).
+
+All ranks share cuda:0 (RCCL refuses several ranks on one device), so the collectives go through
+the host-staged transport of tests/transport_shim.py -- slab.Comm's RCCL branches with gloo moving
+the bytes.  Every rank stages only its own slab of the inputs (inputs.slab_inputs: u0's normal draws
+streamed, y = F(u_true) by the forward kernel + halo), runs GNKSolver at krylow_restart = RESTART for
+ITERS outer iterations (ref:gauss_newton_krylow.py:84-136) and keeps only scalars; then every rank
+frees its state and rank 0 runs the same solve on one rank over the whole grid.  Checked
+(rank 0 writes --out):
+  * every rank took identical decisions and holds identical per-iteration scalars;
+  * 8 ranks vs 1 rank: nit / nrev / njev / success, per-iteration nfev, basis sizes, stdout identical,
+    per-iteration ||x_k|| and sum(r_k^2) within TOL (relative).
+Memory: the GNK state at restart 5 is (6 basis columns + ~9 vectors) x 8.6 GB ~ 130 GB, on 8 ranks
+or on one.
+
+  python -m torch.distributed.run --standalone --nproc-per-node 8 tests/c4_worker.py --out c4.json
+"""
+import argparse
+import contextlib
+import io
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import gauss_newton_via_generalized_krylov_subspaces_amd as gnk  # noqa: E402
+from gauss_newton_via_generalized_krylov_subspaces_amd._device import BratuDevice  # noqa: E402
+from gauss_newton_via_generalized_krylov_subspaces_amd.inputs import slab_inputs  # noqa: E402
+from gauss_newton_via_generalized_krylov_subspaces_amd.slab import Comm  # noqa: E402
+from tests.transport_shim import StagedTransportComm  # noqa: E402
+
+TOL = 1e-10
+
+
+def log(msg):
+    print(f"[rank {dist.get_rank()} {time.strftime('%X')}] {msg}", file=sys.stderr, flush=True)
+
+
+def solve(N, comm, restart, iters):
+    prob = gnk.BratuPdeProblem(N + 1, 5, 10)
+    dev = BratuDevice(prob, comm)
+    u0, y, ut = slab_inputs(dev)
+    del ut
+    own = dev.slab.own
+    rec = {"xnorm2": [], "rsumsq": [], "nfev": []}
+
+    def cb(x, nfev, cg_iter):
+        part = torch.sum(x.x[own] * x.x[own]).reshape(1)
+        rec["xnorm2"].append(float(comm.sum(part)[0]))           # rank-ordered sum of the parts
+        rec["rsumsq"].append(float(x.sumsq))
+        rec["nfev"].append(int(nfev))
+
+    s = gnk.GNKSolver(prob, y, krylow_restart=restart, max_iter=iters + 1, comm=comm, backend=dev.backend,
+                      callback=cb, callback_format="device")
+    buf = io.StringIO()
+    t0 = time.time()
+    with contextlib.redirect_stdout(buf):
+        s.setup(u0)
+        del u0
+        while not s.step():
+            pass
+        r = s.finish(result_format="torch")
+    torch.cuda.synchronize()
+    out = {"nit": r.nit, "nrev": r.nrev, "njev": r.njev, "success": bool(r.success), **rec,
+           "k": [t["k"] for t in s.trace], "trials": [t["trials"] for t in s.trace], "stdout": buf.getvalue(),
+           "spec": dict(s.spec_stats), "seconds": time.time() - t0}
+    del s, r, y, dev
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+    return out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--grid", type=int, default=32768)
+    ap.add_argument("--restart", type=int, default=5)
+    ap.add_argument("--iters", type=int, default=6)
+    ap.add_argument("--out", required=True)
+    a = ap.parse_args()
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo")
+    rank, world = dist.get_rank(), dist.get_world_size()
+    log(f"multi-rank solve, grid {a.grid}, world {world}")
+    comm = StagedTransportComm()
+    mine = solve(a.grid, comm, a.restart, a.iters)
+    log(f"multi-rank done in {mine['seconds']:.1f} s: nit {mine['nit']} nrev {mine['nrev']} k {mine['k']}")
+    every = [None] * world
+    dist.all_gather_object(every, mine)
+    dist.barrier()
+    if rank != 0:
+        dist.barrier()                                      # rank 0's single-rank solve
+        dist.destroy_process_group()
+        return 0
+    log("single-rank solve over the whole grid")
+    one = solve(a.grid, Comm(single=True), a.restart, a.iters)
+    log(f"single-rank done in {one['seconds']:.1f} s")
+    dist.barrier()
+    ranks_identical = all({k: v for k, v in e.items() if k != "seconds"} ==
+                          {k: v for k, v in mine.items() if k != "seconds"} for e in every)
+    keys = ("nit", "nrev", "njev", "success", "nfev", "k", "trials", "stdout")
+    same = all(mine[k] == one[k] for k in keys)
+
+    def rel(a_, b_):
+        a_, b_ = np.sqrt(np.array(a_)), np.sqrt(np.array(b_))
+        return float(np.max(np.abs(a_ - b_) / np.abs(b_))) if len(a_) == len(b_) and len(b_) else float("inf")
+
+    rx, rr = rel(mine["xnorm2"], one["xnorm2"]), rel(mine["rsumsq"], one["rsumsq"])
+    ok = bool(ranks_identical and same and rx <= TOL and rr <= TOL)
+    rep = {"ok": ok, "grid": a.grid, "world": world, "restart": a.restart, "iters": a.iters,
+           "ranks_identical": ranks_identical, "bookkeeping_equal": same, "max_rel_xnorm_diff": rx,
+           "max_rel_rnorm_diff": rr, "tol": TOL, "multi": {k: v for k, v in mine.items() if k != "stdout"},
+           "single": {k: v for k, v in one.items() if k != "stdout"}, "shim_calls": comm.staged_calls}
+    with open(a.out, "w") as f:
+        json.dump(rep, f, indent=1)
+    log(json.dumps({k: rep[k] for k in ("ok", "ranks_identical", "bookkeeping_equal", "max_rel_xnorm_diff",
+                                        "max_rel_rnorm_diff")}))
+    dist.destroy_process_group()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

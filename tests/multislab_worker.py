@@ -10,8 +10,16 @@ Driven by tests/test_gpu_multislab.py.  Every rank runs every case; rank 0 colle
 results, repeats each solve single-rank and writes the comparison to --out:
   * all ranks took identical decisions (bookkeeping, stdout, per-iteration nfev) and hold the same
     iterate norms bit for bit;
-  * multi-rank vs single-rank: bookkeeping identical, per-iteration ||x_k|| within TOL[case], each
-    bound backed by a committed oracle sensitivity test (tests/test_oracle_sensitivity.py);
+  * multi-rank vs single-rank: bookkeeping identical, per-iteration ||x_k|| within the case's bound:
+    GN + CGLS at north_star's 1e-10 (the CG scalars are compensated pairs merged across ranks,
+    slab.Comm.sum_pairs), GNK at the spread of the reference's own arithmetic reordered as 2 .. 8 slabs
+    order it (tests/test_oracle_sensitivity.py);
+  * multi-rank vs the ORACLE (oracle/gnk_oracle.py, on rank 0's host): GNK bookkeeping and stdout
+    identical, ||x_k|| within the same sensitivity bound; GN against the oracle with exactly rounded
+    CG dot products (math.fsum -- what the device's compensated sums compute): bookkeeping and every
+    cg_iter identical, ||x_k|| within 1e-10;
+  * ``--transport shim``: slab.Comm's RCCL branches (device all-gathers, pinned read_async, k_rank_sum,
+    sum_device, device halos) with the bytes moved over gloo underneath (tests/transport_shim.py);
   * GNKSolver on slab-staged inputs (u0, y built per rank, no full-grid vector) == the same solver
     on full-grid host inputs, bit for bit.
 """
@@ -41,7 +49,63 @@ def bound(kind, kw, grid):
     from tests import tolerances as T
     if kind == "gnk":
         return T.trajectory_bound(f"multislab{grid}_{kw['version']}")
-    return T.trajectory_bound(f"gn{grid}" + ("_pre" if kw.get("cg_preconditioner") else ""))
+    return T.NORTH_STAR
+
+
+def exact_cg(matvec, b, psolve=None, rtol=1e-5, maxiter=None, callback=None):
+    """oracle.scipy_cg (scipy iterative.py:305-422) with every dot product exactly rounded (math.fsum)."""
+    import math
+    dot = lambda a, c: math.fsum(a * c)                     # noqa: E731
+    bnrm2 = math.sqrt(dot(b, b))
+    atol = max(0.0, float(rtol) * float(bnrm2))
+    if bnrm2 == 0:
+        return b, 0
+    maxiter = len(b) * 10 if maxiter is None else maxiter
+    x, r, rho_prev, p = np.zeros_like(b), b.copy(), None, None
+    for it in range(maxiter):
+        if math.sqrt(dot(r, r)) < atol:
+            return x, 0
+        z = r if psolve is None else psolve(r)
+        rho = dot(r, z)
+        if it > 0:
+            p *= rho / rho_prev
+            p += z
+        else:
+            p = z.copy()
+        q = matvec(p)
+        alpha = rho / dot(p, q)
+        x += alpha * p
+        r -= alpha * q
+        rho_prev = rho
+        if callback:
+            callback(x)
+    return x, maxiter
+
+
+def run_oracle(kind, N, **kw):
+    """The same case on the CPU oracle (GN: with exactly rounded CG dot products)."""
+    from oracle import gnk_oracle as O
+    prob, y, u0 = O.bratu_workload(N)
+    norms, nfevs, cgs = [], [], []
+
+    def cb(x, nfev, cg_iter):
+        norms.append(float(np.linalg.norm(x)))
+        nfevs.append(nfev)
+        cgs.append(cg_iter)
+
+    res, jac = prob.make_res(y), prob.make_jac()
+    orig = O.scipy_cg
+    with contextlib.redirect_stdout(io.StringIO()) as out:
+        if kind == "gnk":
+            r = O.gauss_newton_krylow(res, u0, jac, callback=cb, **kw)
+        else:
+            O.scipy_cg = exact_cg
+            try:
+                r = O.gauss_newton(res, u0, jac, callback=cb, **kw)
+            finally:
+                O.scipy_cg = orig
+    return {"nit": r.nit, "nrev": r.nrev, "njev": r.njev, "success": bool(r.success), "nfev": nfevs,
+            "cg_iter": cgs, "norms": norms, "stdout": out.getvalue()}
 
 
 BACKEND = None          # --numpy: the NumPy test double of the C-ABI (CPU rehearsal of this script)
@@ -52,11 +116,12 @@ def _be():
 
 
 def run(kind, prob, y, u0, comm, **kw):
-    norms, nfevs = [], []
+    norms, nfevs, cgs = [], [], []
 
     def cb(x, nfev, cg_iter):
         norms.append(float(np.linalg.norm(x)))
         nfevs.append(nfev)
+        cgs.append(cg_iter)
 
     res, jac = prob.make_res(y), prob.make_jac()
     with contextlib.redirect_stdout(io.StringIO()) as out:
@@ -65,7 +130,13 @@ def run(kind, prob, y, u0, comm, **kw):
         else:
             r = gnk.gauss_newton(res, u0, jac, callback=cb, comm=comm, _backend=_be(), **kw)
     return {"nit": r.nit, "nrev": r.nrev, "njev": r.njev, "success": bool(r.success), "nfev": nfevs,
-            "norms": norms, "xnorm": float(np.linalg.norm(r.x)), "stdout": out.getvalue()}
+            "cg_iter": cgs, "norms": norms, "xnorm": float(np.linalg.norm(r.x)), "stdout": out.getvalue()}
+
+
+def rel_diff(a, b):
+    if len(a) != len(b) or not b:
+        return float("inf")
+    return float(np.max(np.abs(np.array(a) - np.array(b)) / np.abs(b)))
 
 
 def staged_vs_host(prob, y_full, u0_full, comm, steps):
@@ -96,6 +167,8 @@ def main():
     ap.add_argument("--iters", type=int, default=45)
     ap.add_argument("--out", required=True)
     ap.add_argument("--numpy", action="store_true")
+    ap.add_argument("--transport", choices=("gloo", "shim"), default="gloo")
+    ap.add_argument("--oracle", type=int, default=1)
     a = ap.parse_args()
     if a.numpy:
         global BACKEND
@@ -120,8 +193,15 @@ def main():
     if f"gn{N}" in T.sensitivity():               # unpreconditioned GN: evidence recorded at grid 256
         cases.append(("gn", dict(max_iter=4, cg_rtol=1e-4)))
     cases.append(("gn", dict(max_iter=3, cg_rtol=1e-4, cg_preconditioner=True)))
-    mine = [run(kind, prob, y, u0, Comm(), **kw) for kind, kw in cases]
-    staging = staged_vs_host(prob, y, u0, Comm(), steps=24)
+    if a.transport == "shim":
+        from tests.transport_shim import StagedTransportComm
+        make_comm = StagedTransportComm
+    else:
+        make_comm = Comm
+    comm = make_comm()
+    mine = [run(kind, prob, y, u0, comm, **kw) for kind, kw in cases]
+    staging = staged_vs_host(prob, y, u0, make_comm(), steps=24)
+    shim_calls = getattr(comm, "staged_calls", None)
     every = [None] * world
     dist.all_gather_object(every, {"cases": mine, "staging": staging})
     dist.barrier()
@@ -129,22 +209,32 @@ def main():
         dist.destroy_process_group()
         return 0
     report, ok = [], True
+    keys = ("nit", "nrev", "njev", "success", "nfev", "cg_iter", "stdout")
     for i, ((kind, kw), d) in enumerate(zip(cases, mine)):
         ranks_equal = all(e["cases"][i] == d for e in every)
         s = run(kind, prob, y, u0, Comm(single=True), **kw)
-        same = all(d[f] == s[f] for f in ("nit", "nrev", "njev", "success", "nfev", "stdout"))
-        rel = float(np.max(np.abs(np.array(d["norms"]) - np.array(s["norms"])) / np.abs(s["norms"]))) \
-            if len(d["norms"]) == len(s["norms"]) and s["norms"] else float("inf")
+        same = all(d[f] == s[f] for f in keys)
+        rel = rel_diff(d["norms"], s["norms"])
         tol = bound(kind, kw, N)
         case_ok = same and ranks_equal and rel <= tol
+        entry = {"case": kind, **kw, "world": world, "grid": N, "transport": a.transport,
+                 "ranks_identical": ranks_equal, "bookkeeping_equal": same, "max_rel_norm_diff": rel, "tol": tol,
+                 "nit": s["nit"], "nrev": s["nrev"]}
+        if a.oracle:
+            o = run_oracle(kind, N, **kw)
+            o_keys = keys if kind == "gn" else ("nit", "nrev", "njev", "success", "nfev", "stdout")
+            o_same = all(d[f] == o[f] for f in o_keys)
+            o_rel = rel_diff(d["norms"], o["norms"])
+            entry.update(oracle_bookkeeping_equal=o_same, oracle_max_rel_norm_diff=o_rel, oracle_tol=tol)
+            case_ok = case_ok and o_same and o_rel <= tol
+        entry["ok"] = case_ok
         ok &= case_ok
-        report.append({"case": kind, **kw, "world": world, "grid": N, "ranks_identical": ranks_equal,
-                       "bookkeeping_equal": same, "max_rel_norm_diff": rel, "tol": tol, "ok": case_ok,
-                       "nit": s["nit"], "nrev": s["nrev"]})
+        report.append(entry)
     stage_ok = all(e["staging"]["staged_equals_host_inputs"] for e in every)
     ok &= stage_ok
     with open(a.out, "w") as f:
-        json.dump({"ok": bool(ok), "world": world, "grid": N, "staging_ok": stage_ok, "cases": report}, f, indent=1)
+        json.dump({"ok": bool(ok), "world": world, "grid": N, "transport": a.transport, "staging_ok": stage_ok,
+                   "shim_calls": shim_calls, "cases": report}, f, indent=1)
     dist.destroy_process_group()
     return 0
 

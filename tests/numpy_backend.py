@@ -19,6 +19,26 @@ class NumpyBackend:
     def __init__(self):
         self.device = torch.device("cpu")
         self.geo = None
+        self.pairs = False
+
+    def set_reduce_pairs(self, on):
+        """gnk_set_reduce_pairs: compensated results as (s, c) pairs; the double's c is 0."""
+        self.pairs = bool(on)
+
+    def set_tuning(self, key, value):
+        pass
+
+    def scratch_doubles(self):
+        return 16 << 20
+
+    def _put(self, out, vals, extra=()):
+        """Write compensated results (pairs when enabled), then the plain extras."""
+        o = []
+        for v in vals:
+            o += [float(v), 0.0] if self.pairs else [float(v)]
+        o += [float(e) for e in extra]
+        for i, v in enumerate(o):
+            out[i] = v
 
     # -- setup -------------------------------------------------------------------------
     def set_bratu(self, N, row0, nrows, h, alpha, lam):
@@ -381,8 +401,7 @@ class NumpyBackend:
     def vec_stats(self, x, stats):
         own = slice(GHOST * self.N, (GHOST + self.nrows) * self.N)
         o = x.numpy()[own]
-        stats[0] = float(np.sum(o * o))
-        stats[1] = float(np.max(np.abs(o)))
+        self._put(stats, [np.sum(o * o)], [np.max(np.abs(o))])
 
     def vec_div(self, src, denom, dst, full_slab):
         sl = slice(None) if full_slab else slice(GHOST * self.N, (GHOST + self.nrows) * self.N)
@@ -429,7 +448,7 @@ class NumpyBackend:
         Q = self._m(q)
         Q[lo:hi] = self._vjp_block(Dm[lo:hi], *self._nb(T, lo, hi))
         own = slice(GHOST * self.N, (GHOST + self.nrows) * self.N)
-        pq[0] = float(np.dot(p.numpy()[own], q.numpy()[own]))
+        self._put(pq, [np.dot(p.numpy()[own], q.numpy()[own])])
 
     def cg_step_matvec(self, d, z, p_in, p_out, q, beta, first, x, xalpha, pq):
         # p_out on every slab row (owned + ghost, as the kernel's boundary ranges), lagged x update
@@ -452,8 +471,7 @@ class NumpyBackend:
             zz = z.numpy()[own]
         else:
             zz = rv[own]
-        out[0] = float(np.dot(rv[own], rv[own]))
-        out[1] = float(np.dot(rv[own], zz))
+        self._put(out, [np.dot(rv[own], rv[own]), np.dot(rv[own], zz)])
 
     def cg_sr_update(self, alpha, beta, first, w, p, s, x, r, dinv, u, out):
         own = slice(GHOST * self.N, (GHOST + self.nrows) * self.N)

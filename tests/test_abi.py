@@ -33,7 +33,8 @@ def test_binding_table_matches_header():
 
 def test_load_library_binds_and_reports_version():
     lib = _native.load_library()
-    assert lib.gnk_abi_version() == 1
+    assert lib.gnk_abi_version() == _native.ABI_VERSION == 2
+    assert lib.gnk_scratch_doubles() == 16 << 20
     assert lib.gnk_gram_padded_dim(20, 1) == 32
     assert lib.gnk_gram_padded_dim(16, 0) == 16
     assert lib.gnk_gram_padded_dim(16, 1) == 32
@@ -45,3 +46,11 @@ def test_no_cpu_fallback_without_gpu():
         pytest.skip("GPU present")
     with pytest.raises(_native.NativeLibraryError):
         _native.HipBackend(torch.device("cpu"))
+
+
+def test_tuning_keys_match_header():
+    with open(os.path.join(ROOT, "include", "gnk.h")) as f:
+        text = f.read()
+    keys = {m.group(1).lower(): int(m.group(2)) for m in re.finditer(r"#define GNK_TUNE_([A-Z0-9_]+) (\d+)", text)}
+    count = keys.pop("count")
+    assert keys == _native.TUNE and count == len(keys)

@@ -262,18 +262,18 @@ def test_cgs_max_propagates_nan():
                                                   # NB = 4: flattened order (N % 32 != 0) / down-strip walks crossing strips
                                                   (100, 55, True, True), (96, 50, True, False), (416, 49, True, True)])
 @pytest.mark.parametrize("staged", ["default", "forced", "ring4"])
-def test_gram_mfma(N, k, with_r, with_rinv, staged, monkeypatch):
+def test_gram_mfma(N, k, with_r, with_rinv, staged):
     """W = [J V | r] @ RinvAug on fp64 MFMA vs an fp64 NumPy Gram (host BLAS).  "forced" runs
     the staged LDS-DMA kernel for every pass it supports (N % 128 == 0, k <= 20); "ring4" also
     forces its 4-slot ring (two blocks per CU, the default only for k = 12)."""
-    if staged != "default":
-        if N % 128 or k > 20:
-            pytest.skip("staged kernel does not cover this shape")
-        monkeypatch.setenv("GNK_GRAM_STAGED", "2")
-        if staged == "ring4":
-            monkeypatch.setenv("GNK_GRAM_RING", "4")
+    if staged != "default" and (N % 128 or k > 20):
+        pytest.skip("staged kernel does not cover this shape")
     prob, dev, ref = make(N)
     be = dev.backend
+    if staged != "default":
+        be.set_tuning("gram_path", 1)
+        if staged == "ring4":
+            be.set_tuning("gram_ring", 4)
     rng = np.random.default_rng(N + k)
     n = N * N
     Vh = np.linalg.qr(rng.standard_normal((n, k)))[0].T.copy()
@@ -309,11 +309,11 @@ def test_gram_mfma(N, k, with_r, with_rinv, staged, monkeypatch):
     np.testing.assert_array_equal(Gdev, Gdev.T)
 
 
-@pytest.mark.parametrize("staged", ["1", "2"])
-def test_gram_deterministic(staged, monkeypatch):
-    monkeypatch.setenv("GNK_GRAM_STAGED", staged)
+@pytest.mark.parametrize("staged", [0, 1])
+def test_gram_deterministic(staged):
     prob, dev, ref = make(512)
     be = dev.backend
+    be.set_tuning("gram_path", staged)
     rng = np.random.default_rng(3)
     k = 12
     V = be.zeros(k, dev.slab.length)
@@ -334,7 +334,7 @@ def test_gram_deterministic(staged, monkeypatch):
 
 
 @pytest.mark.parametrize("N", [24, 100, 101, 512, 640, 1030])
-def test_cg_matvec_matches_two_pass(N, monkeypatch):
+def test_cg_matvec_matches_two_pass(N):
     """q = J^T J p (13-point fused) vs the oracle's two passes; even N runs the row-marching kernel,
     whose q must equal the point-wise kernel's bit for bit (same per-point arithmetic)."""
     prob, dev, ref = make(N)
@@ -355,7 +355,7 @@ def test_cg_matvec_matches_two_pass(N, monkeypatch):
     pq_again = dev.scalar(1)
     be.cg_matvec(d, ps, q, pq_again)
     assert pq_again.item() == pq.item()                            # deterministic reduction
-    monkeypatch.setenv("GNK_CG_MATVEC", "0")
+    be.set_tuning("cg_matvec", 1)
     q0, pq0 = dev.vec(), dev.scalar(1)
     be.cg_matvec(d, ps, q0, pq0)
     np.testing.assert_array_equal(own(dev, q), own(dev, q0))

@@ -23,12 +23,16 @@ def main():
     ap.add_argument("--k", type=int, default=15)
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--kernels", default="gram1,gram2,jvp,gemv,vjpg,cgs,resid,cg")
+    ap.add_argument("--tune", default="", help="gnk_set_tuning overrides, e.g. gram_path=1,gram_ring=4")
     a = ap.parse_args()
     torch.cuda.set_device(0)
     N, k = a.grid, a.k
     n = N * N
     dev = BratuDevice(BratuPdeProblem(N + 1, 5, 10), Comm(single=True))
     be, sl = dev.backend, dev.slab
+    for kv in filter(None, a.tune.split(",")):
+        key, val = kv.split("=")
+        be.set_tuning(key, int(val))
     g = torch.Generator(device=be.device).manual_seed(0)
     V = be.zeros(k + 1, sl.length)
     V[:, sl.own] = torch.randn(k + 1, n, generator=g, device=be.device, dtype=torch.float64) / np.sqrt(n)
