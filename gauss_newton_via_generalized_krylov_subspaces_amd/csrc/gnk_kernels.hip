@@ -201,15 +201,17 @@ struct RowLaunch {
   int64_t lr0, nlr;  // local row range [lr0, lr0 + nlr)
 };
 
-// Element loop helper: for local row lr and element iy of a row.
-#define ROW_LOOP_BEGIN(VEC)                                                          \
-  const int64_t N = geo.N;                                                           \
-  const int64_t iy = (int64_t(blockIdx.x) * BLOCK + threadIdx.x) * (VEC);           \
-  for (int64_t lr = lr0 + blockIdx.y; lr < lr0 + nlr; lr += gridDim.y) {             \
-    if (iy >= N) continue;                                                           \
-    const int64_t li = lr * N + iy;
+// Element loop helper: for local row lr and element iy of a row.  grid.x strides along the row:
+// the Bratu launches (rows()) cover a whole row with grid.x (one pass), the flat launches of the
+// generic path (flat_rows(), one "row" of n) may cap grid.x, and then every thread walks the row.
+#define ROW_LOOP_BEGIN(VEC)                                                                      \
+  const int64_t N = geo.N;                                                                       \
+  for (int64_t lr = lr0 + blockIdx.y; lr < lr0 + nlr; lr += gridDim.y) {                         \
+    for (int64_t iy = (int64_t(blockIdx.x) * BLOCK + threadIdx.x) * (VEC); iy < N;               \
+         iy += int64_t(gridDim.x) * BLOCK * (VEC)) {                                             \
+      const int64_t li = lr * N + iy;
 
-#define ROW_LOOP_END }
+#define ROW_LOOP_END }}
 
 // ---------------------------------------------------------------- operator kernels
 template <int VEC>
@@ -1885,8 +1887,12 @@ __global__ __launch_bounds__(64 * GS_NW) __attribute__((amdgpu_waves_per_eu(WPE)
       dsrc[m] = rowp + col0 + 2 * lane;
       ddst[m] = q * GS_CS;
     } else {
-      const int cc = min(lane >> 1, k - 1);          // halo: lane -> column lane/2, side lane&1
-      dsrc[m] = V + int64_t(cc) * ldv + col0 + ((lane & 1) ? GS_SW : -2);
+      // halo: lane -> column lane/2, side lane&1.  The domain's outer columns (coefficient 0) load an
+      // inside pair instead: the east pair of the last strip would be the 2 elements after a row --
+      // past the end of the column on its last ghost row (a fault when V[k-1] ends an allocation)
+      const int cc = min(lane >> 1, k - 1);
+      const int64_t off = (lane & 1) ? (col0 + GS_SW < N ? col0 + GS_SW : col0 + GS_SW - 2) : (col0 > 0 ? col0 - 2 : 0);
+      dsrc[m] = V + int64_t(cc) * ldv + off;
       ddst[m] = nrow * GS_CS;
     }
   }

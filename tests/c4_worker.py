@@ -3,15 +3,17 @@
 All ranks share cuda:0 (RCCL refuses several ranks on one device), so the collectives go through
 the host-staged transport of tests/transport_shim.py -- slab.Comm's RCCL branches with gloo moving
 the bytes.  Every rank stages only its own slab of the inputs (inputs.slab_inputs: u0's normal draws
-streamed, y = F(u_true) by the forward kernel + halo), runs GNKSolver at krylow_restart = RESTART for
-ITERS outer iterations (ref:gauss_newton_krylow.py:84-136) and keeps only scalars; then every rank
+streamed, y = F(u_true) by the forward kernel + halo), runs GNKSolver at krylow_restart = 20 (C4's
+restart) for ITERS outer iterations (ref:gauss_newton_krylow.py:84-136) and keeps only scalars; then every rank
 frees its state and rank 0 runs the same solve on one rank over the whole grid.  Checked
 (rank 0 writes --out):
   * every rank took identical decisions and holds identical per-iteration scalars;
   * 8 ranks vs 1 rank: nit / nrev / njev / success, per-iteration nfev, basis sizes, stdout identical,
     per-iteration ||x_k|| and sum(r_k^2) within TOL (relative).
-Memory: the GNK state at restart 5 is (6 basis columns + ~9 vectors) x 8.6 GB ~ 130 GB, on 8 ranks
-or on one.
+Memory: ITERS = 6 iterations hold at most 7 basis columns (+ ~9 vectors) x 8.6 GB ~ 140 GB, on 8
+ranks or on one.  (A restart inside the window would make the next step a k = 1 step whose Armijo
+test compares two sums of 1e9 squares differing by less than their rounding: the reference's own
+arithmetic decides it by noise at this size, so the window stays inside the first restart cycle.)
 
   python -m torch.distributed.run --standalone --nproc-per-node 8 tests/c4_worker.py --out c4.json
 """
@@ -54,6 +56,7 @@ def solve(N, comm, restart, iters):
         rec["xnorm2"].append(float(comm.sum(part)[0]))           # rank-ordered sum of the parts
         rec["rsumsq"].append(float(x.sumsq))
         rec["nfev"].append(int(nfev))
+        log(f"it {len(rec['nfev'])}: nfev {nfev} ||x||^2 {rec['xnorm2'][-1]!r} ||r||^2 {rec['rsumsq'][-1]!r}")
 
     s = gnk.GNKSolver(prob, y, krylow_restart=restart, max_iter=iters + 1, comm=comm, backend=dev.backend,
                       callback=cb, callback_format="device")
@@ -78,7 +81,7 @@ def solve(N, comm, restart, iters):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--grid", type=int, default=32768)
-    ap.add_argument("--restart", type=int, default=5)
+    ap.add_argument("--restart", type=int, default=20)
     ap.add_argument("--iters", type=int, default=6)
     ap.add_argument("--out", required=True)
     a = ap.parse_args()
@@ -97,13 +100,17 @@ def main():
         dist.destroy_process_group()
         return 0
     log("single-rank solve over the whole grid")
-    one = solve(a.grid, Comm(single=True), a.restart, a.iters)
-    log(f"single-rank done in {one['seconds']:.1f} s")
+    try:
+        one = solve(a.grid, Comm(single=True), a.restart, a.iters)
+        log(f"single-rank done in {one['seconds']:.1f} s")
+    except Exception as e:                                   # report it; the other ranks wait at the barrier
+        log(f"single-rank solve raised {type(e).__name__}: {e}")
+        one = {"error": f"{type(e).__name__}: {e}", "xnorm2": [], "rsumsq": []}
     dist.barrier()
     ranks_identical = all({k: v for k, v in e.items() if k != "seconds"} ==
                           {k: v for k, v in mine.items() if k != "seconds"} for e in every)
     keys = ("nit", "nrev", "njev", "success", "nfev", "k", "trials", "stdout")
-    same = all(mine[k] == one[k] for k in keys)
+    same = all(mine[k] == one.get(k) for k in keys)
 
     def rel(a_, b_):
         a_, b_ = np.sqrt(np.array(a_)), np.sqrt(np.array(b_))

@@ -199,7 +199,10 @@ def main():
     else:
         make_comm = Comm
     comm = make_comm()
-    mine = [run(kind, prob, y, u0, comm, **kw) for kind, kw in cases]
+    mine = []
+    for kind, kw in cases:
+        print(f"[rank {rank}] {kind} {kw}", file=sys.stderr, flush=True)
+        mine.append(run(kind, prob, y, u0, comm, **kw))
     staging = staged_vs_host(prob, y, u0, make_comm(), steps=24)
     shim_calls = getattr(comm, "staged_calls", None)
     every = [None] * world
@@ -211,6 +214,7 @@ def main():
     report, ok = [], True
     keys = ("nit", "nrev", "njev", "success", "nfev", "cg_iter", "stdout")
     for i, ((kind, kw), d) in enumerate(zip(cases, mine)):
+        print(f"[rank 0] single-rank and oracle runs of case {i}: {kind} {kw}", file=sys.stderr, flush=True)
         ranks_equal = all(e["cases"][i] == d for e in every)
         s = run(kind, prob, y, u0, Comm(single=True), **kw)
         same = all(d[f] == s[f] for f in keys)

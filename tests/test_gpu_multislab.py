@@ -10,15 +10,12 @@ bounds the oracle sensitivity tests back; per-rank staged inputs (inputs.py) rep
 inputs' run bit for bit.  World 8 is the C4 rank count (8 x 32 rows of a 256^2 grid).
 """
 import json
-import os
-import subprocess
-import sys
 
 import pytest
 
-pytestmark = pytest.mark.gpu
+from tests._subproc import run_workers
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+pytestmark = pytest.mark.gpu
 
 
 @pytest.mark.parametrize("world,grid,transport", [(2, 256, "gloo"), (2, 256, "shim"), (3, 384, "shim"),
@@ -27,12 +24,9 @@ def test_multislab_hip_matches_single_rank_and_oracle(world, grid, transport, tm
     """transport "gloo": host-staged collectives (Comm.stage); "shim": Comm's RCCL branches (device
     all-gathers, pinned read_async, gnk_rank_sum, device halos) over a host-staged transport."""
     out = tmp_path / "multislab.json"
-    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", OMP_NUM_THREADS="2")
-    cmd = [sys.executable, "-u", "-m", "torch.distributed.run", "--standalone", "--local-addr", "127.0.0.1",
-           "--nproc-per-node", str(world), os.path.join(ROOT, "tests", "multislab_worker.py"),
-           "--grid", str(grid), "--out", str(out), "--transport", transport]
-    p = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=400)
-    assert p.returncode == 0, p.stderr[-4000:]
+    rc, err = run_workers(world, "multislab_worker.py", ["--grid", grid, "--out", out, "--transport", transport],
+                          f"multislab_{world}_{grid}_{transport}", timeout=600)
+    assert rc == 0, err
     rep = json.loads(out.read_text())
     print(json.dumps(rep))
     assert rep["world"] == world and rep["staging_ok"] and rep["transport"] == transport, rep
