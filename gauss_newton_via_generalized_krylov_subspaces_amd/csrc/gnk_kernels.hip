@@ -1826,22 +1826,37 @@ __device__ __forceinline__ double bcast_row(double v) {
 // then r . Y[:, block] per block, then r . r
 constexpr int gs_nacc(int nb, int ksl) { return nb == 1 ? 2 : 2 * 4 * ksl + 2 + 1; }
 
-template <int NB, int L, int KSL, int R, int WPE>
+// Ring layout: [ring row q][slot s][point] with slot stride gs_ss(R) doubles and ring-row stride R * gs_ss(R)
+// (== 16 mod 32, so a half-wave's fragment reads -- 16 points x 2 columns -- hit 64 distinct banks);
+// ring rows q = 0 .. nrow - 1 are V_0 .. V_{k-1}, u, (r), ring row nrow the halo blocks (the strip's
+// outer neighbours: column c at 4c + {0, 1 | 2, 3}).  With the slot index a compile-time constant of the
+// unrolled step loop, every LDS read is a per-lane base plus an immediate offset.
+constexpr int gs_ss(int R) { return R == 4 ? 132 : 144; }
+
+// Software pipeline (one 16-point row step per wave; the barrier at its end also frees a ring slot):
+//   step x:  DMA row x+R-1 into the slot of row x-1;
+//            Gram of row x from its transform H (issued in step x-1: the MFMA results have had a whole
+//            step to land) -- MFMA tile + VALU tail / r;
+//            A fragments of row x+1 (rows x .. x+2 of the ring) with dn(x+1) from step x-1;
+//            transform of row x+1 -> H (MFMA, consumed in step x+1);  dn(x+2) = -jdiag(u(x+2)).
+// Every MFMA accumulates in one chain per output (no register copies, no h0 + h1 adds): the chains of
+// the Gram and of the transform interleave, so no MFMA waits on its predecessor.
+template <int NB, int L, int KSL, int TAIL, int R, int WPE>
 __global__ __launch_bounds__(64 * GS_NW) __attribute__((amdgpu_waves_per_eu(WPE))) void k_gram_s(const double* __restrict__ u, const double* __restrict__ V,
                                                        int64_t ldv, int k, const double* __restrict__ rinv,
                                                        int ldr, const double* __restrict__ r, Geo geo, Coef cf,
                                                        int64_t rpr, double* __restrict__ partial) {
   constexpr int NACC = gs_nacc(NB, KSL);
-  constexpr int TMAX = NB == 2 ? 4 * KSL : 0;             // tail columns this instance covers
+  constexpr int TMAX = NB == 2 ? 4 * KSL : 0;             // tail accumulator slots of this instance
   constexpr int ER = NB * TMAX, RR = ER + NB;             // accumulator slots of r . Y and r . r
+  constexpr int SS = gs_ss(R);                            // slot stride (doubles)
   extern __shared__ __attribute__((aligned(16))) double lds[];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int64_t N = geo.N;
-  const int nrow = k + 1 + (r ? 1 : 0);             // LDS rows per slot: V_0..V_{k-1}, u, (r)
-  const int slotd = nrow * GS_CS + 128;             // + halo block: 64 lanes x 16 B
+  const int nrow = k + 1 + (r ? 1 : 0);             // ring rows: V_0..V_{k-1}, u, (r)
+  const int QS = R * SS;                            // ring-row stride
   const int ninst = nrow + 1;                       // DMA instructions per grid row (rows + halo)
-  const int tail = NB == 2 ? k - 16 : 0;            // columns 16..k-1 (VALU Gram)
 
   // block -> (row range, strip); consecutive range-major tiles share an XCD (blockIdx % 8),
   // so strip neighbours read each other's halo lines from the same L2
@@ -1852,8 +1867,6 @@ __global__ __launch_bounds__(64 * GS_NW) __attribute__((amdgpu_waves_per_eu(WPE)
   const int64_t x1 = min(geo.nrows, x0 + rpr);
   const int64_t col0 = int64_t(idx % nstrips) * GS_SW;
 
-  // KSL = 4-column k-steps of the last column block holding V columns (compile time: the
-  // transform below is straight-line, no guards)
   auto nks = [](int ab) constexpr { return ab == NB - 1 ? KSL : 4; };
   // RinvAug B fragments [cb][ab][ks] (ordinary loads, before any DMA is in flight)
   double rB[NB][NB][4];
@@ -1868,14 +1881,14 @@ __global__ __launch_bounds__(64 * GS_NW) __attribute__((amdgpu_waves_per_eu(WPE)
         // when a DMA is in flight makes hipcc wait vmcnt(0) at its first use in the step loop)
         asm volatile("" : "+v"(rB[cb][ab][ks]));
       }
-  d4 acc = d4{0.0, 0.0, 0.0, 0.0}, acc1 = acc;     // MFMA tile: columns 0..15 x 0..15 (2 chains)
+  d4 acc = d4{0.0, 0.0, 0.0, 0.0};                  // MFMA tile: columns 0..15 x 0..15
   double ev[NACC];                                  // VALU Gram accumulators (see gs_nacc)
 #pragma unroll
   for (int q = 0; q < NACC; ++q) ev[q] = 0.0;
 
   // This wave's DMA instructions q = wave + 8m (a q past the end re-loads the u row: same bytes,
-  // same place): a per-lane source at row 0 and the LDS offset inside a slot are fixed; a step
-  // only adds the row offset.
+  // same place): a per-lane source at row 0 and the LDS offset of slot 0 are fixed; a step only adds
+  // the row offset and the slot's.
   const double* dsrc[L];
   int ddst[L];
 #pragma unroll
@@ -1885,32 +1898,32 @@ __global__ __launch_bounds__(64 * GS_NW) __attribute__((amdgpu_waves_per_eu(WPE)
     if (q < nrow) {
       const double* rowp = q < k ? V + int64_t(q) * ldv : (q == k ? u : r);
       dsrc[m] = rowp + col0 + 2 * lane;
-      ddst[m] = q * GS_CS;
     } else {
       // halo: lane -> column lane/2, side lane&1.  The domain's outer columns (coefficient 0) load an
       // inside pair instead: the east pair of the last strip would be the 2 elements after a row --
-      // past the end of the column on its last ghost row (a fault when V[k-1] ends an allocation)
+      // past the end of the column on its last ghost row
       const int cc = min(lane >> 1, k - 1);
       const int64_t off = (lane & 1) ? (col0 + GS_SW < N ? col0 + GS_SW : col0 + GS_SW - 2) : (col0 > 0 ? col0 - 2 : 0);
       dsrc[m] = V + int64_t(cc) * ldv + off;
-      ddst[m] = nrow * GS_CS;
     }
+    ddst[m] = q * QS;
   }
   const int64_t rmax = geo.nrows + G - 1;           // last slab row (ghost)
   auto issue_row = [&](int64_t xr, int slot) {     // rows past the slab re-load the last one
     const int64_t roff = (G + min(xr, rmax)) * N;
-    double* sbase = lds + slot * slotd;
+    double* sbase = lds + slot * SS;
 #pragma unroll
     for (int m = 0; m < L; ++m)
       __builtin_amdgcn_global_load_lds((glb_cvp)(dsrc[m] + roff), (lds_vp)(sbase + ddst[m]), 16, 0, 0);
   };
 
-  // fixed per-lane stencil offsets of every fragment (column j = 16ab + 4ks + l>>4, point e)
+  // fixed per-lane stencil offsets of every fragment (column j = 16ab + 4ks + l>>4, point e), slot 0
   const int e = wave * 16 + (lane & 15);            // this lane's point in the strip
   const int cq = lane >> 4;
   const double cwm = (col0 + e > 0) ? cf.hm2 : 0.0;
   const double cem = (col0 + e + 1 < N) ? cf.hm2 : 0.0;
   const double up = -cf.j_lin_up;
+  const int hq = nrow * QS;                         // the halo ring row
   int fo[NB][4], fw[NB][4], fe[NB][4];
   unsigned fv = 0;                                  // per fragment bit: a V column (else padding)
 #pragma unroll
@@ -1920,63 +1933,79 @@ __global__ __launch_bounds__(64 * GS_NW) __attribute__((amdgpu_waves_per_eu(WPE)
       const int j = ab * 16 + ks * 4 + cq;
       const bool isV = j < k;
       const int jr = isV ? j : 0;
-      fo[ab][ks] = jr * GS_CS + e;
-      fw[ab][ks] = e > 0 ? jr * GS_CS + e - 1 : nrow * GS_CS + 4 * jr + 1;             // halo: element -1
-      fe[ab][ks] = e < GS_SW - 1 ? jr * GS_CS + e + 1 : nrow * GS_CS + 4 * jr + 2;     // halo: element 128
+      fo[ab][ks] = jr * QS + e;
+      fw[ab][ks] = e > 0 ? jr * QS + e - 1 : hq + 4 * jr + 1;             // halo: element -1
+      fe[ab][ks] = e < GS_SW - 1 ? jr * QS + e + 1 : hq + 4 * jr + 2;     // halo: element 128
       fv |= unsigned(isV) << (ab * 4 + ks);
     }
-  const int ou = k * GS_CS + e;
-  const int orr = (k + 1) * GS_CS + wave * 16 + cq;  // r at point 16w + (l>>4) (+ 4i)
+  const int ou = k * QS + e;
+  const int orr = (k + 1) * QS + wave * 16 + cq;    // r at point 16w + (l>>4) (+ 4i)
 
-  // Software pipeline inside the wave (2 waves/SIMD cannot hide the latency chains):
-  //   step x: A fragments of row x (LDS reads, FMAs) with dn(x) computed during step x-1;
-  //           dn(x+1) = -jdiag(u(x+1)) (the exp chain runs under the MFMAs);
-  //           transform(x) interleaved with the Gram (MFMA tile + VALU tail / r) of row x-1.
-  double a[NB][4];
-  d4 qp[NB];                                        // transformed rows of the previous step
-  // two independent accumulation chains per block (f64 MFMA chains stall on the RAW dependency)
-  auto transform = [&](d4 (&qv)[NB]) {
+  // A fragments of one row (north / centre / south ring slots) with the diagonal dn of that row
+  auto stencil = [&](const double* Ln, const double* Lc, const double* Ls, double dn, double (&a)[NB][4]) {
+#pragma unroll
+    for (int ab = 0; ab < NB; ++ab)
+#pragma unroll
+      for (int ks = 0; ks < nks(ab); ++ks) {
+        const int o = fo[ab][ks];
+        const double vn = Ln[o], vw = Lc[fw[ab][ks]], vc = Lc[o], ve = Lc[fe[ab][ks]], vs = Ls[o];
+        // J V with explicit FMAs in CSR term order (as k_gram_w).  Only the last fragment can hold
+        // columns >= k (padding, coefficients 0): every earlier one is all V columns.
+        double sv;
+        if (ab == NB - 1 && ks == nks(ab) - 1) {
+          const bool isV = (fv >> (ab * 4 + ks)) & 1;
+          const double cn = isV ? cf.hm2 : 0.0, cw = isV ? cwm : 0.0, cc = isV ? dn : 0.0;
+          const double ce = isV ? cem : 0.0, cs = isV ? up : 0.0;
+          sv = cn * vn;
+          sv = fma(cw, vw, sv);
+          sv = fma(cc, vc, sv);
+          sv = fma(ce, ve, sv);
+          sv = fma(cs, vs, sv);
+        } else {
+          sv = cf.hm2 * vn;
+          sv = fma(cwm, vw, sv);
+          sv = fma(dn, vc, sv);
+          sv = fma(cem, ve, sv);
+          sv = fma(up, vs, sv);
+        }
+        a[ab][ks] = sv;
+      }
+  };
+  // H[cb] = A . RinvAug[:, cb block]: one accumulation chain per output block
+  auto transform = [&](const double (&a)[NB][4], d4 (&H)[NB]) {
 #pragma unroll
     for (int cb = 0; cb < NB; ++cb) {
-      d4 h0 = d4{0.0, 0.0, 0.0, 0.0}, h1 = d4{0.0, 0.0, 0.0, 0.0};
-      int n = 0;
+      d4 h = d4{0.0, 0.0, 0.0, 0.0};
 #pragma unroll
       for (int ab = 0; ab <= cb; ++ab)
 #pragma unroll
-        for (int ks = 0; ks < nks(ab); ++ks, ++n) {
-          if (n & 1) h1 = mfma64(a[ab][ks], rB[cb][ab][ks], h1);
-          else h0 = mfma64(a[ab][ks], rB[cb][ab][ks], h0);
-        }
-      qv[cb] = h0 + h1;
+        for (int ks = 0; ks < nks(ab); ++ks) h = mfma64(a[ab][ks], rB[cb][ab][ks], h);
+      H[cb] = h;
     }
   };
-  // qv[cb][i] = Y[16w + (l>>4) + 4i][16cb + (l&15)]: the MFMA operand of rows 4i..4i+3, and for
+  // H[cb][i] = Y[16w + (l>>4) + 4i][16cb + (l&15)]: the MFMA operand of rows 4i..4i+3, and for
   // the VALU part this lane's column c = 16cb + (l&15) at point p = 16w + (l>>4) + 4i
-  auto gram = [&](const d4 (&qv)[NB], const double* Lr) {
-    acc = mfma64(qv[0][0], qv[0][0], acc);
-    acc1 = mfma64(qv[0][1], qv[0][1], acc1);
-    acc = mfma64(qv[0][2], qv[0][2], acc);
-    acc1 = mfma64(qv[0][3], qv[0][3], acc1);
+  auto gram = [&](const d4 (&Y)[NB], const double* Lr) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) acc = mfma64(Y[0][i], Y[0][i], acc);
     if (NB == 2) {
 #pragma unroll
-      for (int t = 0; t < TMAX; ++t) {
-        if (t < tail) {                              // wave-uniform, registers only
+      for (int t = 0; t < TAIL; ++t) {
 #pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            double yt;
-            switch (t) {
-              case 0: yt = bcast_row<0>(qv[NB - 1][i]); break;
-              case 1: yt = bcast_row<1>(qv[NB - 1][i]); break;
-              case 2: yt = bcast_row<2>(qv[NB - 1][i]); break;
-              case 3: yt = bcast_row<3>(qv[NB - 1][i]); break;
-              case 4: yt = bcast_row<4>(qv[NB - 1][i]); break;
-              case 5: yt = bcast_row<5>(qv[NB - 1][i]); break;
-              case 6: yt = bcast_row<6>(qv[NB - 1][i]); break;
-              default: yt = bcast_row<7>(qv[NB - 1][i]); break;
-            }
-#pragma unroll
-            for (int cb = 0; cb < NB; ++cb) ev[t * NB + cb] = fma(yt, qv[cb][i], ev[t * NB + cb]);
+        for (int i = 0; i < 4; ++i) {
+          double yt;
+          switch (t) {
+            case 0: yt = bcast_row<0>(Y[NB - 1][i]); break;
+            case 1: yt = bcast_row<1>(Y[NB - 1][i]); break;
+            case 2: yt = bcast_row<2>(Y[NB - 1][i]); break;
+            case 3: yt = bcast_row<3>(Y[NB - 1][i]); break;
+            case 4: yt = bcast_row<4>(Y[NB - 1][i]); break;
+            case 5: yt = bcast_row<5>(Y[NB - 1][i]); break;
+            case 6: yt = bcast_row<6>(Y[NB - 1][i]); break;
+            default: yt = bcast_row<7>(Y[NB - 1][i]); break;
           }
+#pragma unroll
+          for (int cb = 0; cb < NB; ++cb) ev[t * NB + cb] = fma(yt, Y[cb][i], ev[t * NB + cb]);
         }
       }
     }
@@ -1985,82 +2014,54 @@ __global__ __launch_bounds__(64 * GS_NW) __attribute__((amdgpu_waves_per_eu(WPE)
       for (int i = 0; i < 4; ++i) {
         const double rv = Lr[orr + 4 * i];
 #pragma unroll
-        for (int cb = 0; cb < NB; ++cb) ev[ER + cb] = fma(rv, qv[cb][i], ev[ER + cb]);
+        for (int cb = 0; cb < NB; ++cb) ev[ER + cb] = fma(rv, Y[cb][i], ev[ER + cb]);
         ev[RR] = fma(rv, rv, ev[RR]);
       }
     }
   };
-  // R = 5: row x+3 is issued in step x and lands by the end of step x+1 (one row in flight across
-  // each barrier); R = 4: row x+2 is issued in step x and waited for at its end (a smaller ring,
-  // so two blocks fit a CU at larger k)
+
+  // R = 5: row x+4 is issued in step x, row x+3 waited for at its end (one row in flight across
+  // each barrier); R = 4: row x+3 is issued in step x and waited for at its end (a smaller ring,
+  // so two blocks fit a CU at larger k).  Slot of row xr: (xr - x0 + 1) mod R.
   constexpr int INF = R - 4;                        // rows still in flight at a barrier
   if (x0 < x1) {
-    // ring slots rotate: sn/sc/ss = rows x-1, x, x+1; sd = row x+R-2 (the slot of row x-2)
-    int sn = 0, sc = 1, ss = 2, sp = 3, sd = R - 1;
-    issue_row(x0 - 1, sn);
-    issue_row(x0, sc);
-    issue_row(x0 + 1, ss);
-    if (R == 5) issue_row(x0 + 2, sp);
-    __builtin_amdgcn_s_waitcnt(waitcnt_vm_lgkm0(L * INF));  // rows x0-1 .. x0+1 landed
+#pragma unroll
+    for (int s = 0; s < R; ++s) issue_row(x0 - 1 + s, s);
+    __builtin_amdgcn_s_waitcnt(waitcnt_vm_lgkm0(L * (INF + 1)));   // rows x0-1 .. x0+1 landed
     __builtin_amdgcn_s_barrier();
-    double dn = -jdiag(cf, lds[sc * slotd + ou]);
-    for (int64_t x = x0; x < x1; ++x) {
-      issue_row(x + R - 2, sd);
-      const double* Ln = lds + sn * slotd;
-      const double* Lc = lds + sc * slotd;
-      const double* Ls = lds + ss * slotd;
-#pragma unroll
-      for (int ab = 0; ab < NB; ++ab)
-#pragma unroll
-        for (int ks = 0; ks < nks(ab); ++ks) {
-          const int o = fo[ab][ks];
-          const double vn = Ln[o], vw = Lc[fw[ab][ks]], vc = Lc[o], ve = Lc[fe[ab][ks]], vs = Ls[o];
-          // J V with explicit FMAs in CSR term order (as k_gram_w).  Only the last fragment can hold
-          // columns >= k (padding, coefficients 0): every earlier one is all V columns.
-          double sv;
-          if (ab == NB - 1 && ks == nks(ab) - 1) {
-            const bool isV = (fv >> (ab * 4 + ks)) & 1;
-            const double cn = isV ? cf.hm2 : 0.0, cw = isV ? cwm : 0.0, cc = isV ? dn : 0.0;
-            const double ce = isV ? cem : 0.0, cs = isV ? up : 0.0;
-            sv = cn * vn;
-            sv = fma(cw, vw, sv);
-            sv = fma(cc, vc, sv);
-            sv = fma(ce, ve, sv);
-            sv = fma(cs, vs, sv);
-          } else {
-            sv = cf.hm2 * vn;
-            sv = fma(cwm, vw, sv);
-            sv = fma(dn, vc, sv);
-            sv = fma(cem, ve, sv);
-            sv = fma(up, vs, sv);
-          }
-          a[ab][ks] = sv;
-        }
-      dn = -jdiag(cf, Ls[ou]);                        // row x+1 (its u is in the ring)
-      d4 qv[NB];
-      transform(qv);
-      if (x > x0) gram(qp, Ln);                       // rows of x-1: r is in slot n
-#pragma unroll
-      for (int cb = 0; cb < NB; ++cb) qp[cb] = qv[cb];
-      const int t = sn;
-      sn = sc;
-      sc = ss;
-      if (R == 5) {
-        ss = sp;
-        sp = sd;
-      } else {
-        ss = sd;
-      }
-      sd = t;
-      __builtin_amdgcn_s_waitcnt(waitcnt_vm_lgkm0(L * INF));  // row x+2 landed (R = 5: x+3 in flight)
-      __builtin_amdgcn_s_barrier();
+    d4 H[NB];
+    {
+      double a[NB][4];
+      stencil(lds, lds + SS, lds + 2 * SS, -jdiag(cf, lds[SS + ou]), a);
+      transform(a, H);
     }
-    gram(qp, lds + sn * slotd);                       // last row x1-1 (its slot is now sn)
+    double dn = -jdiag(cf, lds[2 * SS + ou]);        // row x0 + 1
+    __builtin_amdgcn_s_waitcnt(waitcnt_vm_lgkm0(L * INF));         // row x0 + 2 landed
+    __builtin_amdgcn_s_barrier();
+    for (int64_t xb = x0; xb < x1; xb += R) {
+#pragma unroll
+      for (int st = 0; st < R; ++st) {
+        const int64_t x = xb + st;
+        if (x >= x1) break;
+        issue_row(x + R - 1, st);                     // into the slot of row x-1
+        const double* Lx = lds + ((st + 1) % R) * SS;   // row x
+        const double* Lx1 = lds + ((st + 2) % R) * SS;  // row x+1
+        const double* Lx2 = lds + ((st + 3) % R) * SS;  // row x+2
+        gram(H, Lx);                                  // row x (its r is in slot x)
+        if (x + 1 < x1) {
+          double a[NB][4];
+          stencil(Lx, Lx1, Lx2, dn, a);               // row x+1
+          transform(a, H);
+          dn = -jdiag(cf, Lx2[ou]);                   // row x+2
+        }
+        __builtin_amdgcn_s_waitcnt(waitcnt_vm_lgkm0(L * INF));     // row x+3 landed
+        __builtin_amdgcn_s_barrier();
+      }
+    }
   }
   __builtin_amdgcn_s_waitcnt(waitcnt_vm_lgkm0(0));
   __builtin_amdgcn_s_barrier();
 
-  acc = acc + acc1;
   // block partial = ((w0 + w1) + w2) + ... through LDS:
   //   [0, 256): MFMA tile (lane*4 + i), [256, 256 + 64 NACC): VALU sums (lane * NACC + q)
   constexpr int PL = 256 + 64 * NACC;
@@ -2119,10 +2120,7 @@ __global__ __launch_bounds__(GS_SW) void k_fused_wedge(const double* __restrict_
   wcol[(G + x0) * geo.N + col] = wedge[(idx * 2) * GS_SW + threadIdx.x];
   if (x1 - 1 > x0) wcol[(G + x1 - 1) * geo.N + col] = wedge[(idx * 2 + 1) * GS_SW + threadIdx.x];
 }
-// V columns of the fused pass.  The ring fits k <= 19, but a 16-column instance (k = 15, 8192^2)
-// faulted under tools/kbench.py's repeated launches and is not understood yet: capped at 13, the
-// range measured and tested on the GPU
-constexpr int GF_KMAX = 13;
+constexpr int GF_KMAX = 19;     // V columns of the fused pass (k + 1 <= GS_KMAX Gram columns)
 
 // (v_0 + v_1) + (v_2 + v_3) over the four 16-lane rows of the wave, the same bits in every lane
 __device__ __forceinline__ double sum_rows4(double v) {
@@ -3927,18 +3925,18 @@ int gnk_gram(gnk_ctx* ctx, const double* u, const double* V, int64_t ldv, int k,
     const int nrow = k + 1 + (r ? 1 : 0);
     const int L = (nrow + 1 + GS_NW - 1) / GS_NW;
     // ring depth and occupancy: 5 slots (one row in flight across a barrier) while two blocks fit a
-    // CU, else 4 slots if that makes two blocks fit, else 5 slots at one block per CU.  Two blocks
-    // need <= 128 VGPRs, which KSL = 4 only reaches by spilling (measured 1.2-1.5x slower), so the
-    // 4-slot ring is for KSL <= 3: k = 12 with r, 1.98 ms vs 2.31 ms at 8192^2.
+    // CU, else 4 slots if that makes two blocks fit (every one-block-column instance stays within
+    // the 128 VGPRs of 4 waves per SIMD: <= 104), else 5 slots at one block per CU.
     // tuning GNK_TUNE_GRAM_RING 5 / 4 forces a depth (tooling A/B).
     const int ring_env = tuning(ctx, GNK_TUNE_GRAM_RING);
-    const size_t slot_bytes = (size_t(nrow) * GS_CS + 128) * sizeof(double);
+    // ring rows (V columns, u, r) + the halo row, each R slots of gs_ss(R) doubles
+    auto ring_bytes = [&](int R) { return size_t(nrow + 1) * R * gs_ss(R) * sizeof(double); };
     const size_t half_lds = 80 * 1024;
     int ring = 5;
-    if (ring_env == 4 || (ring_env != 5 && 5 * slot_bytes > half_lds && 4 * slot_bytes <= half_lds && k <= 12))
+    if (ring_env == 4 || (ring_env != 5 && ring_bytes(5) > half_lds && ring_bytes(4) <= half_lds))
       ring = 4;
     if (nbs == 2) ring = 5;
-    const size_t lds = size_t(ring) * slot_bytes;
+    const size_t lds = ring_bytes(ring);
     const bool two_wg = lds <= half_lds;                      // 4 waves per SIMD: VGPRs capped at 128
     if (L <= 4 && lds <= 160 * 1024) {
       const double* rv = rinv ? rinv : ctx->ident + ident_offset(KP / 16);
@@ -3957,14 +3955,19 @@ int gnk_gram(gnk_ctx* ctx, const double* u, const double* V, int64_t ldv, int k,
         return fail(ctx, "gram: scratch too small (staged)");
       const int64_t nown = nrows * ctx->geo.N;
       TimedLaunch tls(ctx, GNK_TIMER_GRAM, 8.0 * double(nown) * double(k + 1 + (r ? 1 : 0)));
-#define GRAMS_RW(NBV, LV, KV, RV, WV)                                                                         \
-  hipLaunchKernelGGL((k_gram_s<NBV, LV, KV, RV, WV>), dim3(unsigned(nwg)), dim3(64 * GS_NW), lds, ctx->stream, u, V, \
-                     ldv, k, rv, KP, r, ctx->geo, ctx->coef, rpr, ctx->scratch)
+#define GRAMS_RW(NBV, LV, KV, TV, RV, WV)                                                                     \
+  hipLaunchKernelGGL((k_gram_s<NBV, LV, KV, TV, RV, WV>), dim3(unsigned(nwg)), dim3(64 * GS_NW), lds, ctx->stream, u, \
+                     V, ldv, k, rv, KP, r, ctx->geo, ctx->coef, rpr, ctx->scratch)
 #define GRAMS(NBV, LV, KV)                                                 \
   do {                                                                     \
-    if (ring == 4) GRAMS_RW(NBV, LV, KV, 4, 4);                       \
-    else if (two_wg) GRAMS_RW(NBV, LV, KV, 5, 4);                          \
-    else GRAMS_RW(NBV, LV, KV, 5, 2);                                      \
+    if (ring == 4) GRAMS_RW(NBV, LV, KV, 0, 4, 4);                         \
+    else if (two_wg) GRAMS_RW(NBV, LV, KV, 0, 5, 4);                       \
+    else GRAMS_RW(NBV, LV, KV, 0, 5, 2);                                   \
+  } while (0)
+#define GRAMS_T(LV)                                                                              \
+  do {                                                                                           \
+    if (k == 17) GRAMS_RW(2, LV, 1, 1, 5, 2); else if (k == 18) GRAMS_RW(2, LV, 1, 2, 5, 2);     \
+    else if (k == 19) GRAMS_RW(2, LV, 1, 3, 5, 2); else GRAMS_RW(2, LV, 1, 4, 5, 2);             \
   } while (0)
 #define GRAMS_K(NBV, LV)                                                    \
   do {                                                                      \
@@ -3974,8 +3977,9 @@ int gnk_gram(gnk_ctx* ctx, const double* u, const double* V, int64_t ldv, int k,
       if (nbs == 1) {
         if (L == 1) GRAMS_K(1, 1); else if (L == 2) GRAMS_K(1, 2); else if (L == 3) GRAMS_K(1, 3); else GRAMS_K(1, 4);
       } else {
-        if (L == 3) GRAMS_RW(2, 3, 1, 5, 2); else GRAMS_RW(2, 4, 1, 5, 2);     // k <= 20: one tail k-step
+        if (L == 3) GRAMS_T(3); else GRAMS_T(4);      // k = 17..20: one tail k-step, k - 16 tail columns
       }
+#undef GRAMS_T
 #undef GRAMS_K
 #undef GRAMS
 #undef GRAMS_RW

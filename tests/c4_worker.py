@@ -9,7 +9,12 @@ frees its state and rank 0 runs the same solve on one rank over the whole grid. 
 (rank 0 writes --out):
   * every rank took identical decisions and holds identical per-iteration scalars;
   * 8 ranks vs 1 rank: nit / nrev / njev / success, per-iteration nfev, basis sizes, stdout identical,
-    per-iteration ||x_k|| and sum(r_k^2) within TOL (relative).
+    per-iteration ||r_k|| within north_star's 1e-10 (relative), ||x_k|| within max(1e-10, CANCEL u ||x_0|| /
+    ||x_k||): on this workload the first steps take the iterate from ||x_0|| ~ 3e3 to ||x_k|| ~ 1e-9 .. 1e-5
+    (the cancellation of c + d along x_0, ref:gauss_newton_krylow.py:98), so two correctly rounded
+    evaluations of the same step already differ by O(u ||x_0||) in x_k -- the floor of any relative
+    comparison of ||x_k||, whatever the summation order (at 8192^2 the reference's own reorderings move
+    ||x_1|| by 2e-7: tests/golden/sensitivity.json, head8192).
 Memory: ITERS = 6 iterations hold at most 7 basis columns (+ ~9 vectors) x 8.6 GB ~ 140 GB, on 8
 ranks or on one.  (A restart inside the window would make the next step a k = 1 step whose Armijo
 test compares two sums of 1e9 squares differing by less than their rounding: the reference's own
@@ -37,6 +42,8 @@ from gauss_newton_via_generalized_krylov_subspaces_amd.slab import Comm  # noqa:
 from tests.transport_shim import StagedTransportComm  # noqa: E402
 
 TOL = 1e-10
+CANCEL = 16          # roundings of size u ||x_0|| allowed in x_k
+U = np.finfo(np.float64).eps / 2
 
 
 def log(msg):
@@ -64,12 +71,13 @@ def solve(N, comm, restart, iters):
     t0 = time.time()
     with contextlib.redirect_stdout(buf):
         s.setup(u0)
+        x0norm = float(s.c[0])                               # ||x_0|| (ref:krylow.py:36)
         del u0
         while not s.step():
             pass
         r = s.finish(result_format="torch")
     torch.cuda.synchronize()
-    out = {"nit": r.nit, "nrev": r.nrev, "njev": r.njev, "success": bool(r.success), **rec,
+    out = {"nit": r.nit, "nrev": r.nrev, "njev": r.njev, "success": bool(r.success), "x0norm": x0norm, **rec,
            "k": [t["k"] for t in s.trace], "trials": [t["trials"] for t in s.trace], "stdout": buf.getvalue(),
            "spec": dict(s.spec_stats), "seconds": time.time() - t0}
     del s, r, y, dev
@@ -114,13 +122,17 @@ def main():
 
     def rel(a_, b_):
         a_, b_ = np.sqrt(np.array(a_)), np.sqrt(np.array(b_))
-        return float(np.max(np.abs(a_ - b_) / np.abs(b_))) if len(a_) == len(b_) and len(b_) else float("inf")
+        return np.abs(a_ - b_) / np.abs(b_) if len(a_) == len(b_) and len(b_) else np.array([np.inf])
 
-    rx, rr = rel(mine["xnorm2"], one["xnorm2"]), rel(mine["rsumsq"], one["rsumsq"])
-    ok = bool(ranks_identical and same and rx <= TOL and rr <= TOL)
+    ex, er = rel(mine["xnorm2"], one["xnorm2"]), rel(mine["rsumsq"], one["rsumsq"])
+    xb = np.maximum(TOL, CANCEL * U * one.get("x0norm", 0.0) / np.sqrt(np.array(one["xnorm2"]))) \
+        if len(ex) == len(one["xnorm2"]) else np.array([0.0])
+    rx, rr = float(np.max(ex)), float(np.max(er))
+    ok = bool(ranks_identical and same and np.all(ex <= xb) and rr <= TOL)
     rep = {"ok": ok, "grid": a.grid, "world": world, "restart": a.restart, "iters": a.iters,
            "ranks_identical": ranks_identical, "bookkeeping_equal": same, "max_rel_xnorm_diff": rx,
-           "max_rel_rnorm_diff": rr, "tol": TOL, "multi": {k: v for k, v in mine.items() if k != "stdout"},
+           "max_rel_rnorm_diff": rr, "tol": TOL, "rel_xnorm_diff": ex.tolist(), "xnorm_bound": xb.tolist(),
+           "x_within_bound": bool(np.all(ex <= xb)) if len(ex) == len(xb) else False, "multi": {k: v for k, v in mine.items() if k != "stdout"},
            "single": {k: v for k, v in one.items() if k != "stdout"}, "shim_calls": comm.staged_calls}
     with open(a.out, "w") as f:
         json.dump(rep, f, indent=1)

