@@ -143,3 +143,59 @@ def test_c3_cgls_8192_capped_vs_reference():
     np.testing.assert_allclose(rn, meta["per_iter"]["resnorm"][-1], rtol=1e-8)
     xs = xh[::meta["subsample_stride"]]
     np.testing.assert_allclose(xs, arr["x_sub"], rtol=0, atol=TOL * np.abs(xs).max())
+
+
+def test_headline_8192_full_restart_cycle_vs_oracle():
+    """The bench workload over one whole restart cycle (8192^2, restart 20, res_old: iterations 1..20 at
+    k = 1..20, then the restart and iteration 21 at k = 1) against the pinned oracle run in the build
+    container (tests/golden/make_cycle8192.py: the reference does not fit there at k = 20; its lean
+    restatement reproduces the reference's own head8192 fixture to 5e-13).  This pins the staged MFMA
+    Gram passes that dominate the timed window (k = 10..20, ref:gauss_newton_krylow.py:86-89) on the
+    real trajectory.  Bookkeeping (per-iteration nfev, basis size) exact; ||x_k||, ||r_k|| of the first
+    cycle within max(1e-10, E_i): E_i = the head8192 envelope (i <= 4) and 2 |exact_k1_i - base_i|, the
+    move of the reference's trajectory when its cancellation-limited k = 1 dot products are exactly
+    rounded (the device's k = 1 step is within 1e-12 of the exact one)."""
+    from gauss_newton_via_generalized_krylov_subspaces_amd._device import BratuDevice
+    from gauss_newton_via_generalized_krylov_subspaces_amd.inputs import slab_inputs
+    from gauss_newton_via_generalized_krylov_subspaces_amd.slab import Comm
+    with open(os.path.join(GOLDEN, "large_cycle8192.json")) as f:
+        fx = json.load(f)
+    base, ex = fx["variants"]["base"], fx["variants"]["exact_k1"]
+    N = fx["N"]
+    prob = gnk.BratuPdeProblem(N + 1, 5, 10)
+    comm = Comm(single=True)
+    dev = BratuDevice(prob, comm)
+    u0, y, _ = slab_inputs(dev)
+    own = dev.slab.own
+    xs, rs, nf = [], [], []
+
+    def cb(x, nfev, cg_iter):
+        xs.append(float(torch.linalg.norm(x.x[own])))
+        rs.append(float(np.sqrt(x.sumsq)))
+        nf.append(int(nfev))
+
+    s = gnk.GNKSolver(prob, y, comm=comm, backend=dev.backend, callback=cb, callback_format="device",
+                      **fx["kwargs"])
+    buf = io.StringIO()
+    with contextlib.redirect_stdout(buf):
+        s.setup(u0)
+        while not s.step():
+            pass
+    ks = [t["k"] for t in s.trace]
+    assert ks == base["k"] and nf == base["nfev"], (ks, nf)
+    assert buf.getvalue().splitlines() == base["stdout"]          # rank / breakdown messages (none expected)
+    n = 20
+    env = np.zeros(n)
+    env[:4] = np.maximum(T.envelope("head8192")[:4], 0)
+    ek = 2 * np.abs(np.array(ex["xnorm"][:n]) - base["xnorm"][:n]) / np.abs(base["xnorm"][:n])
+    ekr = 2 * np.abs(np.array(ex["rnorm"][:n]) - base["rnorm"][:n]) / np.abs(base["rnorm"][:n])
+    tol_x = np.maximum(TOL, np.maximum(env, ek))
+    tol_r = np.maximum(TOL, np.maximum(np.maximum(T.envelope("head8192", "r")[:4].max(), 0) * (np.arange(n) < 4), ekr))
+    dx = np.abs(np.array(xs[:n]) - base["xnorm"][:n]) / np.abs(base["xnorm"][:n])
+    dr = np.abs(np.array(rs[:n]) - base["rnorm"][:n]) / np.abs(base["rnorm"][:n])
+    dxe = np.abs(np.array(xs[:n]) - ex["xnorm"][:n]) / np.abs(ex["xnorm"][:n])
+    print(f"8192^2 cycle: rel ||x_k|| vs oracle {np.array2string(dx, precision=2)}")
+    print(f"  vs the exact-k1 oracle {np.array2string(dxe, precision=2)}; bound {np.array2string(tol_x, precision=2)}")
+    print(f"  rel ||r_k|| {np.array2string(dr, precision=2)}")
+    assert np.all(dx <= tol_x), np.nonzero(dx > tol_x)
+    assert np.all(dr <= tol_r), np.nonzero(dr > tol_r)
