@@ -11,7 +11,8 @@ arithmetic in lean memory:
     array (negation is exact) and factorised in place by scipy.linalg.qr(overwrite_a=True), the same
     LAPACK geqrf/orgqr calls with the same workspace queries as the reference's copy;
   * J V is kept (F-order) for Armijo's jdd = sum((J V d)^2) (ref:armijo_goldstein.py:50).
-Peak RSS ~ 40 GB.  Variants (each a list of per-iteration ||x_k||, ||r_k||, nfev):
+V and J V are file-backed (numpy memmaps under CYCLE_SCRATCH: the page cache holds them, so the
+process's anonymous memory stays ~ 25 GB -- at k = 17 an all-anonymous run reached 62 GB).  Variants (each a list of per-iteration ||x_k||, ||r_k||, nfev):
   base      the oracle's arithmetic (numpy dot products, LAPACK Householder QR);
   exact_k1  the one-column steps (k = 1) with exactly rounded sums (math.fsum) -- the cancellation-
             limited step the device's compensated k = 1 path computes (tests/golden/make_sensitivity.py).
@@ -44,11 +45,19 @@ MAX_ITER = 22          # iterations 1..21: k = 1..20, the restart after iteratio
 THREADS = 8
 
 
+SCRATCH = os.environ.get("CYCLE_SCRATCH", "/tmp")     # file-backed buffers (page cache, not anonymous RSS)
+
+
+def _mm(name, shape, order):
+    return np.lib.format.open_memmap(os.path.join(SCRATCH, f"cycle8192_{name}.npy"), mode="w+", dtype=np.float64,
+                                     shape=shape, fortran_order=(order == "F"))
+
+
 class LeanBasis:
-    """ref:krylow.py:16-73 over a preallocated C-order buffer."""
+    """ref:krylow.py:16-73 over a preallocated C-order buffer (file-backed)."""
 
     def __init__(self, n, kmax):
-        self.buf = np.empty((n, kmax))
+        self.buf = _mm("V", (n, kmax), "C")
         self.k = 0
 
     @property
@@ -106,7 +115,7 @@ def run(variant):
     n = N * N
     kmax = RESTART + 1
     kr = LeanBasis(n, kmax)
-    JVbuf = np.empty((n, kmax), order="F")
+    JVbuf = _mm("JV", (n, kmax), "F")
     Abuf = np.empty((n, kmax), order="F")
     rec = {"xnorm": [], "rnorm": [], "nfev": [], "k": []}
     t0 = time.time()

@@ -18,7 +18,6 @@ step() {
 }
 step fused timeout -k 10 400 python -u -m pytest -q --timeout 200 --timeout-method thread tests/test_gpu_fused.py > $O/fused.log 2>&1
 step fused_diag timeout -k 10 150 python -u tools/fused_fault_diag.py 8192 15 10 > $O/fused_diag.log 2>&1
-step cycle timeout -k 10 300 python -u -m pytest -q -s --timeout 250 --timeout-method thread tests/test_gpu_baseline_sizes.py -k full_restart_cycle > $O/cycle.log 2>&1
 step rocprof bash tools/rocprof_bench.sh
 step sq16 bash tools/pmc_sq.sh gpurun_out/r3d/sq16 --k 16 --reps 5 --kernels gram2
 step sq20 bash tools/pmc_sq.sh gpurun_out/r3d/sq20 --k 20 --reps 5 --kernels gram2
