@@ -26,6 +26,8 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <unordered_map>
+#include <utility>
 #include <vector>
 
 #include "../../include/gnk.h"
@@ -506,15 +508,15 @@ __global__ __launch_bounds__(BLOCK) void k_gemv_vjpg(const double* __restrict__ 
                                                      int64_t lr0, int64_t nlr, double* __restrict__ partial,
                                                      double* __restrict__ spart) {
   __shared__ double sh[(BLOCK / 64) * KCT];
+  __shared__ __attribute__((aligned(16))) double cl[2 * KCT];   // [c_0 .. c_{KCT-1} | hh_0 .. hh_{KCT-1}]
   const int lane = threadIdx.x & 63;
   const int kk = PEND ? k + 1 : k;                  // columns entering x and h
   const int jmax = PEND ? k - 1 : kk - 1;           // last column read through V (>= 0: k >= 1)
-  double cj[KCT], hj[KCT];
-#pragma unroll
-  for (int j = 0; j < KCT; ++j) {
-    cj[j] = j < kk ? cvec[j] : 0.0;
-    hj[j] = (PEND && j < k) ? hh[j] : 0.0;
-  }
+  // The coefficients live in LDS and are read per row (broadcast reads): held in SGPRs for the whole
+  // kernel they spilled (200+ SGPRs at KCT = 16, one v_readlane per use)
+  for (int j = threadIdx.x; j < 2 * KCT; j += BLOCK)
+    cl[j] = j < KCT ? (j < kk ? cvec[j] : 0.0) : ((PEND && j - KCT < k) ? hh[j - KCT] : 0.0);
+  __syncthreads();
   double acc[KCT];
 #pragma unroll
   for (int j = 0; j < KCT; ++j) acc[j] = 0.0;
@@ -522,15 +524,24 @@ __global__ __launch_bounds__(BLOCK) void k_gemv_vjpg(const double* __restrict__ 
   ROW_LOOP_BEGIN(VEC)
   const bool owned = lr >= G && lr < G + geo.nrows;       // block-uniform
   if (VEC == 2 && iy + 1 < N) {
+    // column j of this grid row: a wave-uniform base (SGPRs) + this lane's 32-bit byte offset
+    const uint32_t boff = uint32_t(iy) * uint32_t(sizeof(double));
     d2 vv[KCT];
 #pragma unroll
-    for (int j = 0; j < KCT; ++j) vv[j] = *reinterpret_cast<const d2*>(V + min(j, jmax) * ldv + li);
+    for (int j = 0; j < KCT; ++j) {
+      const char* rowj = reinterpret_cast<const char*>(V + (int64_t(min(j, jmax)) * ldv + lr * N));
+      vv[j] = *reinterpret_cast<const d2*>(rowj + boff);
+    }
+    int z = 0;
+    asm volatile("" : "+s"(z));                     // opaque 0: the LDS reads stay in the row loop
+    const double* cz = cl + z;
     if (PEND) {
       d2 s = {0.0, 0.0};
 #pragma unroll
       for (int j = 0; j < KCT; ++j) {
-        s.x = s.x + vv[j].x * hj[j];
-        s.y = s.y + vv[j].y * hj[j];
+        const double hj = cz[KCT + j];
+        s.x = s.x + vv[j].x * hj;
+        s.y = s.y + vv[j].y * hj;
       }
       d2 ww = *reinterpret_cast<const d2*>(wcol + li);
       ww.x = ww.x - s.x;
@@ -550,8 +561,9 @@ __global__ __launch_bounds__(BLOCK) void k_gemv_vjpg(const double* __restrict__ 
 #pragma unroll
     for (int j = 0; j < KCT; ++j) {
       // the rounding of k_gemv: acc + v_j * c_j in column order (c_j = 0 past k adds a zero)
-      xs.x = xs.x + vv[j].x * cj[j];
-      xs.y = xs.y + vv[j].y * cj[j];
+      const double cj = cz[j];
+      xs.x = xs.x + vv[j].x * cj;
+      xs.y = xs.y + vv[j].y * cj;
     }
     *reinterpret_cast<d2*>(x + li) = xs;
     if (owned) {
@@ -583,7 +595,7 @@ __global__ __launch_bounds__(BLOCK) void k_gemv_vjpg(const double* __restrict__ 
       if (PEND) {
         double s = 0.0;
 #pragma unroll
-        for (int j = 0; j < KCT; ++j) s = s + vv[j] * hj[j];
+        for (int j = 0; j < KCT; ++j) s = s + vv[j] * cl[KCT + j];
         const double wi = wcol[i] - s;
         wcol[i] = wi;
 #pragma unroll
@@ -596,7 +608,7 @@ __global__ __launch_bounds__(BLOCK) void k_gemv_vjpg(const double* __restrict__ 
       }
       double xs = 0.0;
 #pragma unroll
-      for (int j = 0; j < KCT; ++j) xs = xs + vv[j] * cj[j];
+      for (int j = 0; j < KCT; ++j) xs = xs + vv[j] * cl[j];
       x[i] = xs;
       if (owned) {
         const bool hw = yy > 0, he = yy < N - 1;
@@ -1815,11 +1827,9 @@ constexpr unsigned waitcnt_vm_lgkm0(int n) { return unsigned((n & 0xF) | ((n >> 
 // lane j of each 16-lane row, broadcast to the row (DPP row_newbcast)
 template <int J>
 __device__ __forceinline__ double bcast_row(double v) {
-  const int2 b = __builtin_bit_cast(int2, v);
-  // mov_dpp: every lane has a valid source, so no "old" value (update_dpp's costs a v_mov per half)
-  const int lo = __builtin_amdgcn_mov_dpp(b.x, 0x150 + J, 0xF, 0xF, false);
-  const int hi = __builtin_amdgcn_mov_dpp(b.y, 0x150 + J, 0xF, 0xF, false);
-  return __builtin_bit_cast(double, int2{lo, hi});
+  // one v_mov_b64_dpp (DPP64: row_newbcast is its broadcast); mov_dpp: every lane has a valid source,
+  // so no "old" value
+  return __builtin_amdgcn_mov_dpp(v, 0x150 + J, 0xF, 0xF, false);
 }
 
 // per-lane VALU Gram accumulators of the staged kernel: [tail t < 4 KSL][column block] (NB = 2),
@@ -1841,6 +1851,11 @@ constexpr int gs_ss(int R) { return R == 4 ? 132 : 144; }
 //            transform of row x+1 -> H (MFMA, consumed in step x+1);  dn(x+2) = -jdiag(u(x+2)).
 // Every MFMA accumulates in one chain per output (no register copies, no h0 + h1 adds): the chains of
 // the Gram and of the transform interleave, so no MFMA waits on its predecessor.
+// Two column blocks (k = 17..20) are laid out lead-first: block 0 = the TAIL = k - 16 lead columns
+// 0 .. TAIL-1 (Y there needs only the first 4-column k-step of the triangular transform: 1 MFMA),
+// block 1 = the 16 main columns TAIL .. TAIL+15 (every k-step: 5 MFMAs) -- 6 transform MFMAs per
+// row step instead of 9 with the 16 columns first (whose 4-column remainder needs all 5 k-steps too).
+// The MFMA Gram tile is the main block; the lead columns' sums run on VALU (row_newbcast).
 template <int NB, int L, int KSL, int TAIL, int R, int WPE>
 __global__ __launch_bounds__(64 * GS_NW) __attribute__((amdgpu_waves_per_eu(WPE))) void k_gram_s(const double* __restrict__ u, const double* __restrict__ V,
                                                        int64_t ldv, int k, const double* __restrict__ rinv,
@@ -1868,15 +1883,22 @@ __global__ __launch_bounds__(64 * GS_NW) __attribute__((amdgpu_waves_per_eu(WPE)
   const int64_t col0 = int64_t(idx % nstrips) * GS_SW;
 
   auto nks = [](int ab) constexpr { return ab == NB - 1 ? KSL : 4; };
+  // k-steps of output block cb from fragment block ab (NB = 2: the lead block needs the first only)
+  auto nkt = [](int cb, int ab) constexpr { return (NB == 2 && cb == 0) ? (ab == 0 ? 1 : 0) : (ab == NB - 1 ? KSL : 4); };
   // RinvAug B fragments [cb][ab][ks] (ordinary loads, before any DMA is in flight)
+  const int cl = lane & 15;
   double rB[NB][NB][4];
 #pragma unroll
   for (int cb = 0; cb < NB; ++cb)
 #pragma unroll
     for (int ab = 0; ab <= cb; ++ab)
 #pragma unroll
-      for (int ks = 0; ks < nks(ab); ++ks) {
-        rB[cb][ab][ks] = rinv[(ab * 16 + ks * 4 + (lane >> 4)) * ldr + cb * 16 + (lane & 15)];
+      for (int ks = 0; ks < nkt(cb, ab); ++ks) {
+        const int row = ab * 16 + ks * 4 + (lane >> 4);
+        if (NB == 2)   // lead block: columns 0 .. TAIL-1 (the rest of its tile 0); main: TAIL + cl
+          rB[cb][ab][ks] = cb == 0 ? (cl < TAIL ? rinv[row * ldr + cl] : 0.0) : rinv[row * ldr + TAIL + cl];
+        else
+          rB[cb][ab][ks] = rinv[row * ldr + cl];
         // opaque use: the load retires here, before the first DMA (a VGPR load still counted
         // when a DMA is in flight makes hipcc wait vmcnt(0) at its first use in the step loop)
         asm volatile("" : "+v"(rB[cb][ab][ks]));
@@ -1979,15 +2001,16 @@ __global__ __launch_bounds__(64 * GS_NW) __attribute__((amdgpu_waves_per_eu(WPE)
 #pragma unroll
       for (int ab = 0; ab <= cb; ++ab)
 #pragma unroll
-        for (int ks = 0; ks < nks(ab); ++ks) h = mfma64(a[ab][ks], rB[cb][ab][ks], h);
+        for (int ks = 0; ks < nkt(cb, ab); ++ks) h = mfma64(a[ab][ks], rB[cb][ab][ks], h);
       H[cb] = h;
     }
   };
-  // H[cb][i] = Y[16w + (l>>4) + 4i][16cb + (l&15)]: the MFMA operand of rows 4i..4i+3, and for
-  // the VALU part this lane's column c = 16cb + (l&15) at point p = 16w + (l>>4) + 4i
+  // H[cb][i] = Y[16w + (l>>4) + 4i][col(cb) + (l&15)] (col: 0 for NB = 1; 0 / TAIL for the lead / main
+  // block of NB = 2): the MFMA operand of rows 4i..4i+3, and for the VALU part this lane's column at
+  // point p = 16w + (l>>4) + 4i
   auto gram = [&](const d4 (&Y)[NB], const double* Lr) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) acc = mfma64(Y[0][i], Y[0][i], acc);
+    for (int i = 0; i < 4; ++i) acc = mfma64(Y[NB - 1][i], Y[NB - 1][i], acc);
     if (NB == 2) {
 #pragma unroll
       for (int t = 0; t < TAIL; ++t) {
@@ -1995,14 +2018,14 @@ __global__ __launch_bounds__(64 * GS_NW) __attribute__((amdgpu_waves_per_eu(WPE)
         for (int i = 0; i < 4; ++i) {
           double yt;
           switch (t) {
-            case 0: yt = bcast_row<0>(Y[NB - 1][i]); break;
-            case 1: yt = bcast_row<1>(Y[NB - 1][i]); break;
-            case 2: yt = bcast_row<2>(Y[NB - 1][i]); break;
-            case 3: yt = bcast_row<3>(Y[NB - 1][i]); break;
-            case 4: yt = bcast_row<4>(Y[NB - 1][i]); break;
-            case 5: yt = bcast_row<5>(Y[NB - 1][i]); break;
-            case 6: yt = bcast_row<6>(Y[NB - 1][i]); break;
-            default: yt = bcast_row<7>(Y[NB - 1][i]); break;
+            case 0: yt = bcast_row<0>(Y[0][i]); break;
+            case 1: yt = bcast_row<1>(Y[0][i]); break;
+            case 2: yt = bcast_row<2>(Y[0][i]); break;
+            case 3: yt = bcast_row<3>(Y[0][i]); break;
+            case 4: yt = bcast_row<4>(Y[0][i]); break;
+            case 5: yt = bcast_row<5>(Y[0][i]); break;
+            case 6: yt = bcast_row<6>(Y[0][i]); break;
+            default: yt = bcast_row<7>(Y[0][i]); break;
           }
 #pragma unroll
           for (int cb = 0; cb < NB; ++cb) ev[t * NB + cb] = fma(yt, Y[cb][i], ev[t * NB + cb]);
@@ -2829,12 +2852,15 @@ __global__ __launch_bounds__(64) void k_gram_scatter_v(const double* __restrict_
       }
 }
 
-// staged-kernel scatter: red = block-summed partials [256 MFMA tile | 64 lanes x NACC]
-//   G[c][c'] (c, c' < 16) from the MFMA tile, G[16 + t][c] from the tail sums, G[k][c], G[k][k]
-//   from the r sums; lane groups g = l >> 4 (points) summed in order 0..3.
+// staged-kernel scatter: red = block-summed partials [256 MFMA tile | 64 lanes x NACC]; lane groups
+// g = l >> 4 (points) summed in order 0..3.  tail = k - 16 columns in the VALU sums (nb = 2):
+//   lead = 0 (k_gram_sf): the MFMA tile holds columns 0..15, the VALU sums rows 16 + t;
+//   lead = 1 (k_gram_s):  the VALU sums hold the lead columns t < tail, the MFMA tile columns tail..tail+15;
+// then G[k][c], G[k][k] from the r sums.
 __global__ __launch_bounds__(BLOCK) void k_gram_scatter_s(const double* __restrict__ red, int nb, int nacc, int k,
-                                                          int has_r, int KP, double* __restrict__ Gout) {
+                                                          int has_r, int KP, double* __restrict__ Gout, int lead) {
   const int tail = nb == 2 ? k - 16 : 0;
+  const int c0 = (nb == 2 && lead) ? tail : 0;       // first column of the MFMA tile
   const int er = nb == 1 ? 0 : nacc - 3, rr = er + nb;
   const double* ev = red + 256;
   auto lsum = [&](int col_in_block, int q) {
@@ -2842,25 +2868,31 @@ __global__ __launch_bounds__(BLOCK) void k_gram_scatter_s(const double* __restri
     for (int g = 0; g < 4; ++g) s += ev[(16 * g + col_in_block) * nacc + q];
     return s;
   };
+  // column c of the Gram -> (block, column in block) of the VALU sums
+  auto blk = [&](int c) { return c0 ? (c < c0 ? 0 : 1) : (c >> 4); };
+  auto cin = [&](int c) { return c0 ? (c < c0 ? c : c - c0) : (c & 15); };
   for (int idx = blockIdx.x * BLOCK + threadIdx.x; idx < 256 + 24 * 33 + 33; idx += gridDim.x * BLOCK) {
     if (idx < 256) {
       const int lane = idx >> 2, i = idx & 3;
       const int row = (lane >> 4) + 4 * i, col = lane & 15;
-      if (row < k && col < k && row <= col) {
-        Gout[row * KP + col] = red[idx];
-        Gout[col * KP + row] = red[idx];
+      if (c0 + row < k && c0 + col < k && row <= col) {
+        Gout[(c0 + row) * KP + c0 + col] = red[idx];
+        Gout[(c0 + col) * KP + c0 + row] = red[idx];
       }
     } else if (idx < 256 + 24 * 33) {
-      const int t = (idx - 256) / 33, c = (idx - 256) % 33;   // row 16 + t, column c <= 16 + t
-      if (t < tail && c <= 16 + t) {
-        const double v = lsum(c & 15, t * nb + (c >> 4));
-        Gout[(16 + t) * KP + c] = v;
-        Gout[c * KP + 16 + t] = v;
+      const int t = (idx - 256) / 33, c = (idx - 256) % 33;
+      const int trow = c0 ? t : 16 + t;                 // the tail / lead column's Gram row
+      // lead = 0: columns c <= 16 + t of row 16 + t;  lead = 1: columns c <= t and the 16 main ones
+      const bool want = c0 ? (c <= t || (c >= c0 && c < c0 + 16)) : (c <= 16 + t);
+      if (t < tail && want && c < k) {
+        const double v = lsum(cin(c), t * nb + blk(c));
+        Gout[trow * KP + c] = v;
+        Gout[c * KP + trow] = v;
       }
     } else if (has_r) {
       const int c = idx - 256 - 24 * 33;
       if (c < k) {
-        const double v = lsum(c & 15, er + (c >> 4));
+        const double v = lsum(cin(c), er + blk(c));
         Gout[k * KP + c] = v;
         Gout[c * KP + k] = v;
       } else if (c == k) {
@@ -3351,6 +3383,7 @@ struct gnk_ctx {
   double* scratch = nullptr;
   double* ident = nullptr;     // 16², 32², 48², 64² identities (RinvAug of an unpreconditioned pass)
   int num_cus = 256;
+  std::unordered_map<const void*, int> resident;   // kernel -> resident workgroups per CU (BLOCK threads)
   std::string err;
   // gnk_set_reduce_pairs: compensated reductions written as unevaluated (s, c) pairs
   int pairs = 0;
@@ -3397,6 +3430,21 @@ RowLaunch rows(const gnk_ctx* ctx, int64_t lr0, int64_t nlr, int vec, int cap_bl
   L.lr0 = lr0;
   L.nlr = nlr;
   return L;
+}
+
+// Workgroups (of `block` threads) of `fn` resident on the whole device at once: a persistent
+// grid-stride launch sized to a multiple of it has no partly filled last round (at 8192^2 the trial
+// kernel's former fixed 2048 workgroups were 1.6 rounds at 5 waves per SIMD).
+int resident_blocks(gnk_ctx* ctx, const void* fn, int block = BLOCK) {
+  int per = 0;
+  const auto it = ctx->resident.find(fn);
+  if (it != ctx->resident.end()) {
+    per = it->second;
+  } else {
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, fn, block, 0) != hipSuccess || per < 1) per = 1;
+    ctx->resident[fn] = per;
+  }
+  return per * ctx->num_cus;
 }
 
 int vec_of(const gnk_ctx* ctx) { return (ctx->geo.N % 2 == 0) ? 2 : 1; }
@@ -3722,6 +3770,19 @@ int gnk_vjp_gemv_t(gnk_ctx* ctx, const double* u, const double* r, const double*
   return wreduce(ctx, ctx->scratch, nblk, k, kct, kct, int64_t(nblk) * kct, nullptr, h_out);
 }
 
+}  // extern "C"
+namespace {
+// k_gemv_vjpg<VEC, kct, PEND> for kct = 1 .. 24
+template <int V_, bool P_, int... K>
+const void* vjpg_table(int kct, std::integer_sequence<int, K...>) {
+  static const void* const t[] = {reinterpret_cast<const void*>(&k_gemv_vjpg<V_, K + 1, P_>)...};
+  return t[kct - 1];
+}
+template <int V_, bool P_>
+const void* vjpg_pick(int kct) { return vjpg_table<V_, P_>(kct, std::make_integer_sequence<int, 24>{}); }
+}  // namespace
+extern "C" {
+
 // shared body of gnk_basis_gemv_vjp_gemv_t (hh == nullptr) and its pending-column form
 static int gemv_vjpg_launch(gnk_ctx* ctx, const char* what, const double* V, int64_t ldv, int k, const double* c,
                      const double* hh, const double* r, double* x, double* g, double* h_out, double* stats_out) {
@@ -3732,37 +3793,20 @@ static int gemv_vjpg_launch(gnk_ctx* ctx, const char* what, const double* V, int
   if (vec_of(ctx) == 2 && (ldv % 2 != 0)) return fail(ctx, std::string(what) + ": ldv must be even");
   double* wcol = pend ? const_cast<double*>(V) + int64_t(k) * ldv : nullptr;
   if (pend && (g == wcol || x == wcol)) return fail(ctx, std::string(what) + ": g / x alias the pending column");
-  const int kct = std::max(4, (kk + 3) / 4 * 4);
-  RowLaunch L = rows(ctx, 0, ctx->geo.nrows + 2 * G, vec_of(ctx), 2048);
+  // one instance per width (no clamped surplus loads), grid = one full round of resident workgroups
+  const int kct = kk;
+  const void* fn = vec_of(ctx) == 2 ? (pend ? vjpg_pick<2, true>(kct) : vjpg_pick<2, false>(kct))
+                                    : (pend ? vjpg_pick<1, true>(kct) : vjpg_pick<1, false>(kct));
+  RowLaunch L = rows(ctx, 0, ctx->geo.nrows + 2 * G, vec_of(ctx), resident_blocks(ctx, fn));
   const int nblk = L.grid.x * L.grid.y;
   const size_t soff = (size_t(nblk) * kct + 1) & ~size_t(1);     // stats partials after the h partials
   if (soff + 2 * size_t(nblk) > SCRATCH_DOUBLES / 2) return fail(ctx, std::string(what) + ": scratch too small");
   double* spart = ctx->scratch + soff;
-#define GVJ_LAUNCH(V_, K_)                                                                                     \
-  do {                                                                                                         \
-    if (pend)                                                                                                  \
-      hipLaunchKernelGGL((k_gemv_vjpg<V_, K_, true>), L.grid, dim3(BLOCK), 0, ctx->stream, V, ldv, k, c, hh,   \
-                         wcol, r, x, g, ctx->geo, ctx->coef, L.lr0, L.nlr, ctx->scratch, spart);               \
-    else                                                                                                       \
-      hipLaunchKernelGGL((k_gemv_vjpg<V_, K_, false>), L.grid, dim3(BLOCK), 0, ctx->stream, V, ldv, k, c, hh,  \
-                         wcol, r, x, g, ctx->geo, ctx->coef, L.lr0, L.nlr, ctx->scratch, spart);               \
-  } while (0)
-#define GVJ_SWITCH(V_)                  \
-  switch (kct) {                        \
-    case 4: GVJ_LAUNCH(V_, 4); break;   \
-    case 8: GVJ_LAUNCH(V_, 8); break;   \
-    case 12: GVJ_LAUNCH(V_, 12); break; \
-    case 16: GVJ_LAUNCH(V_, 16); break; \
-    case 20: GVJ_LAUNCH(V_, 20); break; \
-    default: GVJ_LAUNCH(V_, 24); break; \
-  }
-  if (vec_of(ctx) == 2) {
-    GVJ_SWITCH(2)
-  } else {
-    GVJ_SWITCH(1)
-  }
-#undef GVJ_SWITCH
-#undef GVJ_LAUNCH
+  Geo geo = ctx->geo;
+  Coef coef = ctx->coef;
+  double* part = ctx->scratch;
+  void* args[] = {&V, &ldv, &k, &c, &hh, &wcol, &r, &x, &g, &geo, &coef, &L.lr0, &L.nlr, &part, &spart};
+  (void)hipLaunchKernel(fn, L.grid, dim3(BLOCK), args, 0, ctx->stream);
   int rc = check_launch(ctx, what);
   if (rc) return rc;
   rc = wreduce(ctx, ctx->scratch, nblk, kk, kct, kct, int64_t(nblk) * kct, nullptr, h_out);
@@ -3927,15 +3971,16 @@ int gnk_gram(gnk_ctx* ctx, const double* u, const double* V, int64_t ldv, int k,
     // ring depth and occupancy: 5 slots (one row in flight across a barrier) while two blocks fit a
     // CU, else 4 slots if that makes two blocks fit (every one-block-column instance stays within
     // the 128 VGPRs of 4 waves per SIMD: <= 104), else 5 slots at one block per CU.
-    // tuning GNK_TUNE_GRAM_RING 5 / 4 forces a depth (tooling A/B).
+    // tuning GNK_TUNE_GRAM_RING 4 / 5 forces a depth (tooling A/B).  Deeper rings at one block per CU
+    // (6 / 8 slots, profiles/round3/ring_sweep.jsonl) were no faster: the pass is not DMA-latency bound.
     const int ring_env = tuning(ctx, GNK_TUNE_GRAM_RING);
     // ring rows (V columns, u, r) + the halo row, each R slots of gs_ss(R) doubles
     auto ring_bytes = [&](int R) { return size_t(nrow + 1) * R * gs_ss(R) * sizeof(double); };
     const size_t half_lds = 80 * 1024;
     int ring = 5;
-    if (ring_env == 4 || (ring_env != 5 && ring_bytes(5) > half_lds && ring_bytes(4) <= half_lds))
-      ring = 4;
-    if (nbs == 2) ring = 5;
+    if (ring_env == 4 || ring_env == 5) ring = ring_env;
+    else if (ring_bytes(5) > half_lds && ring_bytes(4) <= half_lds && nbs == 1) ring = 4;
+    if (ring_bytes(ring) > 160 * 1024) ring = 5;
     const size_t lds = ring_bytes(ring);
     const bool two_wg = lds <= half_lds;                      // 4 waves per SIMD: VGPRs capped at 128
     if (L <= 4 && lds <= 160 * 1024) {
@@ -3960,14 +4005,20 @@ int gnk_gram(gnk_ctx* ctx, const double* u, const double* V, int64_t ldv, int k,
                      V, ldv, k, rv, KP, r, ctx->geo, ctx->coef, rpr, ctx->scratch)
 #define GRAMS(NBV, LV, KV)                                                 \
   do {                                                                     \
-    if (ring == 4) GRAMS_RW(NBV, LV, KV, 0, 4, 4);                         \
+    if (ring == 4 && two_wg) GRAMS_RW(NBV, LV, KV, 0, 4, 4);               \
+    else if (ring == 4) GRAMS_RW(NBV, LV, KV, 0, 4, 2);                    \
     else if (two_wg) GRAMS_RW(NBV, LV, KV, 0, 5, 4);                       \
     else GRAMS_RW(NBV, LV, KV, 0, 5, 2);                                   \
   } while (0)
+#define GRAMS_TR(LV, TV)                                                   \
+  do {                                                                     \
+    if (ring == 4) GRAMS_RW(2, LV, 1, TV, 4, 2);                           \
+    else GRAMS_RW(2, LV, 1, TV, 5, 2);                                     \
+  } while (0)
 #define GRAMS_T(LV)                                                                              \
   do {                                                                                           \
-    if (k == 17) GRAMS_RW(2, LV, 1, 1, 5, 2); else if (k == 18) GRAMS_RW(2, LV, 1, 2, 5, 2);     \
-    else if (k == 19) GRAMS_RW(2, LV, 1, 3, 5, 2); else GRAMS_RW(2, LV, 1, 4, 5, 2);             \
+    if (k == 17) GRAMS_TR(LV, 1); else if (k == 18) GRAMS_TR(LV, 2);                             \
+    else if (k == 19) GRAMS_TR(LV, 3); else GRAMS_TR(LV, 4);                                     \
   } while (0)
 #define GRAMS_K(NBV, LV)                                                    \
   do {                                                                      \
@@ -3980,6 +4031,7 @@ int gnk_gram(gnk_ctx* ctx, const double* u, const double* V, int64_t ldv, int k,
         if (L == 3) GRAMS_T(3); else GRAMS_T(4);      // k = 17..20: one tail k-step, k - 16 tail columns
       }
 #undef GRAMS_T
+#undef GRAMS_TR
 #undef GRAMS_K
 #undef GRAMS
 #undef GRAMS_RW
@@ -3991,7 +4043,7 @@ int gnk_gram(gnk_ctx* ctx, const double* u, const double* V, int64_t ldv, int k,
       rcs = wreduce(ctx, ctx->scratch, int(nwg), PL, int64_t(PL), PL, 0, nullptr, red);
       if (rcs) return rcs;
       hipLaunchKernelGGL(k_gram_scatter_s, dim3(4), dim3(BLOCK), 0, ctx->stream, red, nbs, nacc, k, r ? 1 : 0, KP,
-                         G_out);
+                         G_out, 1);
       return check_launch(ctx, "gram scatter (staged)");
     }
   }
@@ -4576,7 +4628,7 @@ int gnk_gram_fused(gnk_ctx* ctx, double* V, int64_t ldv, int k, const double* e_
   double* red = ctx->scratch + (SCRATCH_DOUBLES - size_t(PL));
   rc = wreduce(ctx, ctx->scratch, int(nwg), PL, int64_t(PL), PL, 0, nullptr, red);
   if (rc) return rc;
-  hipLaunchKernelGGL(k_gram_scatter_s, dim3(4), dim3(BLOCK), 0, ctx->stream, red, nbs, nacc, kg, 1, KP, G_out);
+  hipLaunchKernelGGL(k_gram_scatter_s, dim3(4), dim3(BLOCK), 0, ctx->stream, red, nbs, nacc, kg, 1, KP, G_out, 0);
   rc = check_launch(ctx, "gram_fused scatter");
   if (rc) return rc;
   return wreduce(ctx, tpart, int(nwg), 3 + k, GF_TPL, 3 + k, 0, pack_flags(), pack_out);
