@@ -1911,12 +1911,18 @@ __global__ __launch_bounds__(64 * GS_NW) __attribute__((amdgpu_waves_per_eu(WPE)
   // This wave's DMA instructions q = wave + 8m (a q past the end re-loads the u row: same bytes,
   // same place): a per-lane source at row 0 and the LDS offset of slot 0 are fixed; a step only adds
   // the row offset and the slot's.
+  // R = 4 (EB): the u ring row runs 3 grid rows ahead (slot of row y holds u(y + 3)), so every 4th
+  // step one jdiag per lane covers 4 rows (lane group g: row x + 2 + g) -- the other steps take their
+  // diagonal from that batch by a lane shuffle, not 4 lanes computing the same exp
+  constexpr bool EB = R == 4;
   const double* dsrc[L];
   int ddst[L];
+  bool isu[L];
 #pragma unroll
   for (int m = 0; m < L; ++m) {
     int q = wave + GS_NW * m;
     if (q >= ninst) q = k;
+    isu[m] = q == k;
     if (q < nrow) {
       const double* rowp = q < k ? V + int64_t(q) * ldv : (q == k ? u : r);
       dsrc[m] = rowp + col0 + 2 * lane;
@@ -1933,10 +1939,12 @@ __global__ __launch_bounds__(64 * GS_NW) __attribute__((amdgpu_waves_per_eu(WPE)
   const int64_t rmax = geo.nrows + G - 1;           // last slab row (ghost)
   auto issue_row = [&](int64_t xr, int slot) {     // rows past the slab re-load the last one
     const int64_t roff = (G + min(xr, rmax)) * N;
+    const int64_t roffu = (G + min(xr + (EB ? 3 : 0), rmax)) * N;
     double* sbase = lds + slot * SS;
 #pragma unroll
     for (int m = 0; m < L; ++m)
-      __builtin_amdgcn_global_load_lds((glb_cvp)(dsrc[m] + roff), (lds_vp)(sbase + ddst[m]), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((glb_cvp)(dsrc[m] + (isu[m] ? roffu : roff)), (lds_vp)(sbase + ddst[m]), 16,
+                                       0, 0);
   };
 
   // fixed per-lane stencil offsets of every fragment (column j = 16ab + 4ks + l>>4, point e), slot 0
@@ -2048,6 +2056,15 @@ __global__ __launch_bounds__(64 * GS_NW) __attribute__((amdgpu_waves_per_eu(WPE)
   // so two blocks fit a CU at larger k).  Slot of row xr: (xr - x0 + 1) mod R.
   constexpr int INF = R - 4;                        // rows still in flight at a barrier
   if (x0 < x1) {
+    // EB: u of rows x0, x0+1 (the ring's u rows start at x0+2) by ordinary loads before any DMA
+    double dn0 = 0.0, dnb = 0.0;                    // dnb: lane group g holds dn of row (batch x) + 2 + g
+    if (EB) {
+      const int64_t i0 = (G + x0) * N + col0 + e;
+      double ua = u[i0], ub = u[i0 + N];
+      asm volatile("" : "+v"(ua), "+v"(ub));
+      dn0 = -jdiag(cf, ua);
+      dnb = -jdiag(cf, ub);                         // every group: dn(x0 + 1), the first step's
+    }
 #pragma unroll
     for (int s = 0; s < R; ++s) issue_row(x0 - 1 + s, s);
     __builtin_amdgcn_s_waitcnt(waitcnt_vm_lgkm0(L * (INF + 1)));   // rows x0-1 .. x0+1 landed
@@ -2055,10 +2072,10 @@ __global__ __launch_bounds__(64 * GS_NW) __attribute__((amdgpu_waves_per_eu(WPE)
     d4 H[NB];
     {
       double a[NB][4];
-      stencil(lds, lds + SS, lds + 2 * SS, -jdiag(cf, lds[SS + ou]), a);
+      stencil(lds, lds + SS, lds + 2 * SS, EB ? dn0 : -jdiag(cf, lds[SS + ou]), a);
       transform(a, H);
     }
-    double dn = -jdiag(cf, lds[2 * SS + ou]);        // row x0 + 1
+    double dn = EB ? 0.0 : -jdiag(cf, lds[2 * SS + ou]);        // row x0 + 1
     __builtin_amdgcn_s_waitcnt(waitcnt_vm_lgkm0(L * INF));         // row x0 + 2 landed
     __builtin_amdgcn_s_barrier();
     for (int64_t xb = x0; xb < x1; xb += R) {
@@ -2066,6 +2083,18 @@ __global__ __launch_bounds__(64 * GS_NW) __attribute__((amdgpu_waves_per_eu(WPE)
       for (int st = 0; st < R; ++st) {
         const int64_t x = xb + st;
         if (x >= x1) break;
+        if (EB) {
+          if (st == 0) {
+            dn = __shfl(dnb, 48 + (lane & 15));       // dn(x+1): group 3 of the previous batch
+            // the new batch: group g = dn(x+2+g); u(x+2+g) sits in the slot of row x-1+g (slot g), read
+            // before this step's DMA refills slot 0
+            double ug = lds[cq * SS + ou];
+            asm volatile("" : "+v"(ug));
+            dnb = -jdiag(cf, ug);
+          } else {
+            dn = __shfl(dnb, (st - 1) * 16 + (lane & 15));
+          }
+        }
         issue_row(x + R - 1, st);                     // into the slot of row x-1
         const double* Lx = lds + ((st + 1) % R) * SS;   // row x
         const double* Lx1 = lds + ((st + 2) % R) * SS;  // row x+1
@@ -2075,7 +2104,7 @@ __global__ __launch_bounds__(64 * GS_NW) __attribute__((amdgpu_waves_per_eu(WPE)
           double a[NB][4];
           stencil(Lx, Lx1, Lx2, dn, a);               // row x+1
           transform(a, H);
-          dn = -jdiag(cf, Lx2[ou]);                   // row x+2
+          if (!EB) dn = -jdiag(cf, Lx2[ou]);          // row x+2
         }
         __builtin_amdgcn_s_waitcnt(waitcnt_vm_lgkm0(L * INF));     // row x+3 landed
         __builtin_amdgcn_s_barrier();
@@ -3968,19 +3997,21 @@ int gnk_gram(gnk_ctx* ctx, const double* u, const double* V, int64_t ldv, int k,
     const int nbs = k <= 16 ? 1 : 2;                        // MFMA transform blocks of the V columns
     const int nrow = k + 1 + (r ? 1 : 0);
     const int L = (nrow + 1 + GS_NW - 1) / GS_NW;
-    // ring depth and occupancy: 5 slots (one row in flight across a barrier) while two blocks fit a
-    // CU, else 4 slots if that makes two blocks fit (every one-block-column instance stays within
-    // the 128 VGPRs of 4 waves per SIMD: <= 104), else 5 slots at one block per CU.
-    // tuning GNK_TUNE_GRAM_RING 4 / 5 forces a depth (tooling A/B).  Deeper rings at one block per CU
-    // (6 / 8 slots, profiles/round3/ring_sweep.jsonl) were no faster: the pass is not DMA-latency bound.
+    // ring depth and occupancy: one column block (k <= 16): 4 slots (the batched jdiag of EB), two blocks
+    // per CU (the ring fits 80 KB; every such instance stays within the 128 VGPRs of 4 waves per SIMD);
+    // two column blocks: 5 slots, one block per CU.  tuning GNK_TUNE_GRAM_RING 4 / 5 forces a depth
+    // (tooling A/B; 5 slots compute one jdiag per row step).
+    // Deeper rings at one block per CU (6 / 8 slots, profiles/round3/ring_sweep.jsonl) were no faster:
+    // the pass is not DMA-latency bound.
     const int ring_env = tuning(ctx, GNK_TUNE_GRAM_RING);
     // ring rows (V columns, u, r) + the halo row, each R slots of gs_ss(R) doubles
     auto ring_bytes = [&](int R) { return size_t(nrow + 1) * R * gs_ss(R) * sizeof(double); };
     const size_t half_lds = 80 * 1024;
-    int ring = 5;
+    // (4 slots: one jdiag per lane every 4 rows, EB; two column blocks run one workgroup per CU, where
+    // 5 slots -- a row in flight across each barrier -- measured faster: profiles/round3/gram_eb.jsonl)
+    int ring = nbs == 1 ? 4 : 5;
     if (ring_env == 4 || ring_env == 5) ring = ring_env;
-    else if (ring_bytes(5) > half_lds && ring_bytes(4) <= half_lds && nbs == 1) ring = 4;
-    if (ring_bytes(ring) > 160 * 1024) ring = 5;
+    if (ring_bytes(ring) > 160 * 1024) ring = 4;
     const size_t lds = ring_bytes(ring);
     const bool two_wg = lds <= half_lds;                      // 4 waves per SIMD: VGPRs capped at 128
     if (L <= 4 && lds <= 160 * 1024) {

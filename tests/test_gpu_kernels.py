@@ -261,19 +261,19 @@ def test_cgs_max_propagates_nan():
                                                   (130, 33, True, True), (48, 60, True, True), (24, 30, True, False),
                                                   # NB = 4: flattened order (N % 32 != 0) / down-strip walks crossing strips
                                                   (100, 55, True, True), (96, 50, True, False), (416, 49, True, True)])
-@pytest.mark.parametrize("staged", ["default", "forced", "ring4"])
+@pytest.mark.parametrize("staged", ["default", "forced", "ring5"])
 def test_gram_mfma(N, k, with_r, with_rinv, staged):
     """W = [J V | r] @ RinvAug on fp64 MFMA vs an fp64 NumPy Gram (host BLAS).  "forced" runs
-    the staged LDS-DMA kernel for every pass it supports (N % 128 == 0, k <= 20); "ring4" also
-    forces its 4-slot ring (two blocks per CU, the default only for k = 12)."""
+    the staged LDS-DMA kernel for every pass it supports (N % 128 == 0, k <= 20) with its default
+    4-slot ring (jdiag batched over 4 rows); "ring5" forces the 5-slot ring (one jdiag per row step)."""
     if staged != "default" and (N % 128 or k > 20):
         pytest.skip("staged kernel does not cover this shape")
     prob, dev, ref = make(N)
     be = dev.backend
     if staged != "default":
         be.set_tuning("gram_path", 1)
-        if staged == "ring4":
-            be.set_tuning("gram_ring", 4)
+        if staged == "ring5":
+            be.set_tuning("gram_ring", 5)
     rng = np.random.default_rng(N + k)
     n = N * N
     Vh = np.linalg.qr(rng.standard_normal((n, k)))[0].T.copy()
