@@ -19,7 +19,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("GNK_LIB", os.path.join(_HERE, "libgnk.so"))
 GHOST = 2  # GNK_GHOST_ROWS
 TIMER_GRAM, TIMER_JVP, TIMER_CG_MATVEC = 1, 2, 3  # GNK_TIMER_*
-ABI_VERSION = 2  # GNK_ABI_VERSION
+ABI_VERSION = 3  # GNK_ABI_VERSION
 # GNK_TUNE_* keys of gnk_set_tuning (tests / A/B tooling only; the solver never sets them)
 TUNE = {"gram_path": 0, "gram_ring": 1, "gram_v1min": 2, "cg_matvec": 3, "vjpg_blocks": 4, "gram_wide": 5}
 
@@ -79,12 +79,6 @@ SIGNATURES = {
     "gnk_lls_solve": (_c_int, [_c_vp, _c_vp, _c_int, _c_int, _c_vp, _c_int, _c_vp, _c_vp, _c_vp, _c_vp]),
     "gnk_lls_next": (_c_int, [_c_vp, _c_int, _c_int, _c_vp, _c_vp, _c_vp, _c_vp, _c_int, _c_vp, _c_vp, _c_vp, _c_vp,
                               _c_vp, _c_vp]),
-    "gnk_gram_fused_max_k": (_c_int, []),
-    "gnk_gram_fused": (_c_int, [_c_vp, _c_vp, _c_i64, _c_int, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_i64, _c_vp, _c_vp,
-                                _c_vp, _c_vp]),
-    "gnk_lls_fused_t": (_c_int, [_c_vp, _c_int, _c_vp, _c_vp, _c_int, _c_vp]),
-    "gnk_lls_proj": (_c_int, [_c_vp, _c_int, _c_vp, _c_vp, _c_vp, _c_vp, _c_int, _c_vp, _c_dbl, _c_vp, _c_vp, _c_vp,
-                              _c_vp, _c_vp, _c_vp]),
     "gnk_probe_mfma_f64": (_c_int, [_c_vp, _c_vp, _c_int, _c_int]),
     "gnk_timer_start": (_c_int, [_c_vp, _c_int, _c_int]),
     "gnk_timer_collect": (_c_int, [_c_vp, ctypes.POINTER(_c_dbl), ctypes.POINTER(_c_dbl), _c_int]),
@@ -333,21 +327,6 @@ class HipBackend:
 
     def gram_dim(self, k, with_r):
         return int(self.lib.gnk_gram_padded_dim(int(k), int(bool(with_r))))
-
-    def gram_fused_max_k(self):
-        return int(self.lib.gnk_gram_fused_max_k())
-
-    def gram_fused(self, V, k, e_try, hh, r_old, y, T, x, r_t, G, pack):
-        kp = self.gram_dim(k + 1, True)
-        self._call("gnk_gram_fused", _p(V), V.stride(0), int(k), _p(e_try), _p(hh), _p(r_old), _p(y), _p(T), kp,
-                   _p(x), _p(r_t), _p(G), _p(pack))
-
-    def lls_fused_t(self, k, out, sc, kp_next, T):
-        self._call("gnk_lls_fused_t", int(k), _p(out), _p(sc), int(kp_next), _p(T))
-
-    def lls_proj(self, k, out, e_try, pack, sc, kp_next, G_fused, rho2_min, G, P, sdd, e, hh, scn):
-        self._call("gnk_lls_proj", int(k), _p(out), _p(e_try), _p(pack), _p(sc), int(kp_next), _p(G_fused),
-                   float(rho2_min), _p(G), _p(P), _p(sdd), _p(e), _p(hh), _p(scn))
 
     def gram(self, u, V, k, rinv, r, G):
         kp = self.gram_dim(k, r is not None)

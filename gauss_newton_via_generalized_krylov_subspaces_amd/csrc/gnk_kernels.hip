@@ -1796,24 +1796,21 @@ __global__ __launch_bounds__(BLOCK) void k_gram_m(const double* __restrict__ u, 
 // ---------------------------------------------------------------- staged Gram pass (LDS-DMA ring)
 // One workgroup (8 waves) walks a vertical strip of GS_SW = 128 grid points down a range of grid
 // rows.  The raw rows of every basis column, u and r stream global -> LDS by LDS-DMA
-// (global_load_lds_dwordx4, no VGPR staging) two grid rows ahead into a 5-slot ring:
-//   slot(x) = x mod 5 holds row x of [V_0 .. V_{k-1}, u, (r)] (column stride GS_CS doubles) and a
-//   halo block (the strip's outer neighbours of every column).
+// (global_load_lds_dwordx4, no VGPR staging) into an R-slot ring (R = 4 or 5, layout at gs_ss below):
+// each slot holds one grid row of [V_0 .. V_{k-1}, u, (r)] and a halo block (the strip's outer
+// neighbours of every column); with R = 4 the u row runs 3 grid rows ahead (the batched jdiag).
 // Wave w owns points 16w .. 16w+15 of each step.  It builds its A fragments of J V straight in
 // the MFMA operand layout (lane: point l&15, column block l>>4) from five LDS reads per value,
 // transforms them on MFMA with the RinvAug B fragments held in VGPRs (Y = J V P^-1), and --
 // because the transform's C/D layout equals the Gram's A/B operand layout -- feeds Y to the Gram
-// directly from registers.  Only the 16 x 16 tile of columns 0..15 runs on MFMA (f64 MFMA is no
-// faster than f64 VALU on MI355X and the two pipes run side by side):
-//   * columns 16..k-1 (k <= GS_KMAX): Y[p][t] is broadcast along its 16-lane row (DPP row_newbcast)
+// directly from registers.  Only one 16 x 16 column tile runs on MFMA (f64 MFMA is no faster than
+// f64 VALU on MI355X):
+//   * k > 16: the k - 16 lead columns' Y[p][t] is broadcast along its 16-lane row (DPP row_newbcast)
 //     and every lane accumulates Y[p][t] * Y[p][c] for its column c on VALU;
 //   * the r column (RinvAug is the identity there): Y[p][c] * r[p] and r[p]^2 on VALU.
 // Those per-lane sums (4 points per step, fixed order) are reduced over the lane groups, waves
 // and blocks in a fixed order, like the MFMA tile.
-// GS_CS = 144 == 16 (mod 32): the A-fragment reads of a half-wave (16 points x 2 columns) hit
-// 64 distinct banks.
 constexpr int GS_SW = 128;
-constexpr int GS_CS = 144;
 constexpr int GS_NW = 8;
 constexpr int GS_KMAX = 20;     // V columns the staged kernel covers (k 21..24 would fit the LDS
                                 // ring but the two-block instance then spills past 256 VGPRs)
@@ -2137,545 +2134,6 @@ __global__ __launch_bounds__(64 * GS_NW) __attribute__((amdgpu_waves_per_eu(WPE)
   for (int t = tid; t < PL; t += blockDim.x) out[t] = red[t];
 }
 
-// ---------------------------------------------------------------- fused first trial + next Gram pass
-//   One marching pass does the res_old first Armijo trial of step i and the
-// least-squares Gram pass of step i+1, from one read of V, r_old and y:
-//   w   = g_p - V[:, :k-1] hh      the pending column (slot k-1), materialised in place
-//   x   = V[:, :k] e_try           the trial point (w enters as column k-1)
-//   r_t = y - F(x)                 its residual
-//   g   = -J(x)^T r_old            the res_old update, stored raw in slot k (the next pending column)
-//   pack partial = [sum r_t^2, sum w^2, max |w|, V[:, :k]^T g]   (owned rows)
-//   Gram partial of [J(x) [V_0 .. V_{k-1} g] T | r_t]  (k_gram_s layout)
-// T carries the next step's preconditioner but not the pending column's projection (hh' = V^T g is
-// only known at the end of this pass): k_lls_proj applies it to the Gram afterwards.
-// The ring of k_gram_s holds, per grid row, [V_0 .. V_{k-1} | g | x | r_t | r_old | y]: V, r_old and
-// y arrive by LDS-DMA (issued three rows ahead, waited for at the end of the step), g, x and r_t are
-// computed into the ring.  Step x: the trial point of row x+2 (the basis columns split over the four
-// lane groups, the partial sums combined by permlane swaps), g at row x+1 (J at x(x+1), whose exp is
-// also the next step's diagonal), r_t at row x, the J [V g] fragments of row x (g's south value from
-// the register just computed), the transform of row x and the Gram of row x-1.  The strip's outer
-// neighbours of the computed rows (halo entries of w, x and g) come from a second trial-point round
-// in waves 0 and 7 (points -1 / 128) and from one lane group of those waves in the g stencil.
-constexpr int GF_TPL = 24;      // trial partial per block: [sum r^2, sum w^2, max |w|, h_0 .. h_{k-1}]
-#ifndef GNK_FDBG
-#define GNK_FDBG 0      // tooling-only ablation builds of the fused pass (tools/abl_fused.sh): 1 = no trial-point
-#endif                  // sums, 2 = no g stencil / exp, 4 = no r_t stencil, 8 = no halo round
-
-// the fused pass's pending column on the first / last row of every row range (staged by k_gram_sf)
-__global__ __launch_bounds__(GS_SW) void k_fused_wedge(const double* __restrict__ wedge, double* __restrict__ wcol,
-                                                      Geo geo, int64_t rpr) {
-  const int64_t nstrips = geo.N / GS_SW;
-  const int64_t idx = blockIdx.x;
-  const int64_t x0 = (idx / nstrips) * rpr, x1 = min(geo.nrows, x0 + rpr);
-  const int64_t col = (idx % nstrips) * GS_SW + threadIdx.x;
-  if (x0 >= x1) return;
-  wcol[(G + x0) * geo.N + col] = wedge[(idx * 2) * GS_SW + threadIdx.x];
-  if (x1 - 1 > x0) wcol[(G + x1 - 1) * geo.N + col] = wedge[(idx * 2 + 1) * GS_SW + threadIdx.x];
-}
-constexpr int GF_KMAX = 19;     // V columns of the fused pass (k + 1 <= GS_KMAX Gram columns)
-
-// (v_0 + v_1) + (v_2 + v_3) over the four 16-lane rows of the wave, the same bits in every lane
-__device__ __forceinline__ double sum_rows4(double v) {
-  const int2 b = __builtin_bit_cast(int2, v);
-  const auto lo = __builtin_amdgcn_permlane16_swap(b.x, b.x, false, false);
-  const auto hi = __builtin_amdgcn_permlane16_swap(b.y, b.y, false, false);
-  const double s = __builtin_bit_cast(double, int2{int(lo[0]), int(hi[0])}) +
-                   __builtin_bit_cast(double, int2{int(lo[1]), int(hi[1])});
-  const int2 c = __builtin_bit_cast(int2, s);
-  const auto lo2 = __builtin_amdgcn_permlane32_swap(c.x, c.x, false, false);
-  const auto hi2 = __builtin_amdgcn_permlane32_swap(c.y, c.y, false, false);
-  return __builtin_bit_cast(double, int2{int(lo2[0]), int(hi2[0])}) +
-         __builtin_bit_cast(double, int2{int(lo2[1]), int(hi2[1])});
-}
-
-template <int NB, int L, int KSL>
-__global__ __launch_bounds__(64 * GS_NW) __attribute__((amdgpu_waves_per_eu(2))) void k_gram_sf(
-    double* __restrict__ V, int64_t ldv, int k, const double* __restrict__ etry, const double* __restrict__ hh,
-    const double* __restrict__ rold, const double* __restrict__ yv, const double* __restrict__ tf, int ldr,
-    double* __restrict__ xout, double* __restrict__ rout, Geo geo, Coef cf, int64_t rpr,
-    double* __restrict__ partial, double* __restrict__ tpart, double* __restrict__ wedge,
-    double* __restrict__ trash) {
-  constexpr int NACC = gs_nacc(NB, KSL);
-  constexpr int TMAX = NB == 2 ? 4 * KSL : 0;
-  constexpr int ER = NB * TMAX, RR = ER + NB;
-  constexpr int JS = 4 * (NB - 1) + KSL;            // trial-point columns per lane group (j = cq + 4s)
-  extern __shared__ __attribute__((aligned(16))) double lds[];
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int64_t N = geo.N;
-  const int kg = k + 1;                             // Gram columns: V_0 .. V_{k-1}, g
-  const int RG = k, RX = k + 1, RT = k + 2, RO = k + 3, RY = k + 4;     // ring rows past the basis
-  const int nrow = k + 5;
-  const int slotd = nrow * GS_CS + 128;
-  const int hb = nrow * GS_CS;                      // halo block: column c at hb + 4c + {-2, -1, 128, 129}
-  const int ninst = k + 3;                          // DMA instructions per grid row: V, r_old, y, halo
-  const int tail = NB == 2 ? kg - 16 : 0;
-  double* const gcol = V + int64_t(k) * ldv;
-  double* const wcol = V + int64_t(k - 1) * ldv;
-
-  const int nstrips = int(N / GS_SW);
-  const int nwg = gridDim.x, b = blockIdx.x;
-  const int idx = (nwg % 8 == 0) ? (b % 8) * (nwg / 8) + b / 8 : b;
-  const int64_t x0 = int64_t(idx / nstrips) * rpr;
-  const int64_t x1 = min(geo.nrows, x0 + rpr);
-  const int64_t col0 = int64_t(idx % nstrips) * GS_SW;
-
-  auto nks = [](int ab) constexpr { return ab == NB - 1 ? KSL : 4; };
-  const int cq = lane >> 4, pl = lane & 15;
-  const int e = wave * 16 + pl;
-  // RinvAug B fragments and this lane group's trial-point coefficients (ordinary loads, retired
-  // before any DMA is in flight)
-  double rB[NB][NB][4];
-#pragma unroll
-  for (int cb = 0; cb < NB; ++cb)
-#pragma unroll
-    for (int ab = 0; ab <= cb; ++ab)
-#pragma unroll
-      for (int ks = 0; ks < nks(ab); ++ks) {
-        rB[cb][ab][ks] = tf[(ab * 16 + ks * 4 + cq) * ldr + cb * 16 + pl];
-        asm volatile("" : "+v"(rB[cb][ab][ks]));
-      }
-  double hq[JS], eq[JS];
-  int jq[JS];
-#pragma unroll
-  for (int s = 0; s < JS; ++s) {
-    const int j = cq + 4 * s;
-    const bool ok = j < k - 1;
-    jq[s] = ok ? j : 0;
-    hq[s] = ok ? hh[j] : 0.0;
-    eq[s] = ok ? etry[j] : 0.0;
-    asm volatile("" : "+v"(hq[s]), "+v"(eq[s]));
-  }
-  double ekp = etry[k - 1];                         // the pending column's coefficient
-  asm volatile("" : "+v"(ekp));
-  d4 acc = d4{0.0, 0.0, 0.0, 0.0}, acc1 = acc;
-  double ev[NACC];
-#pragma unroll
-  for (int q = 0; q < NACC; ++q) ev[q] = 0.0;
-
-  // DMA instructions q = wave + 8m: V rows, r_old, y, the halo block (past the end: V_0 again)
-  const double* dsrc[L];
-  int ddst[L];
-#pragma unroll
-  for (int m = 0; m < L; ++m) {
-    int q = wave + GS_NW * m;
-    if (q >= ninst) q = 0;
-    if (q < k) {
-      dsrc[m] = V + int64_t(q) * ldv + col0 + 2 * lane;
-      ddst[m] = q * GS_CS;
-    } else if (q == k) {
-      dsrc[m] = rold + col0 + 2 * lane;
-      ddst[m] = RO * GS_CS;
-    } else if (q == k + 1) {
-      dsrc[m] = yv + col0 + 2 * lane;
-      ddst[m] = RY * GS_CS;
-    } else {
-      // lane -> column lane / 2 (V_0 .. V_{k-1}; r_old at k + 1), side lane & 1; the domain's outer
-      // columns (zero coefficients) re-load an inside pair so that no access leaves the vector
-      const int hc = lane >> 1;
-      const double* base = hc < k ? V + int64_t(hc) * ldv : (hc == k + 1 ? rold : V);
-      const int64_t off = (lane & 1) ? (col0 + GS_SW < N ? col0 + GS_SW : col0 + GS_SW - 2) : (col0 > 0 ? col0 - 2 : 0);
-      dsrc[m] = base + off;
-      ddst[m] = hb;
-    }
-  }
-  const int64_t rmax = geo.nrows + G - 1;
-  auto issue_row = [&](int64_t xr, int slot) {
-    const int64_t roff = (G + min(xr, rmax)) * N;
-    double* sbase = lds + slot * slotd;
-#pragma unroll
-    for (int m = 0; m < L; ++m)
-      __builtin_amdgcn_global_load_lds((glb_cvp)(dsrc[m] + roff), (lds_vp)(sbase + ddst[m]), 16, 0, 0);
-  };
-
-  // fragment offsets (as k_gram_s, over the kg Gram columns; column k is g, ring row RG = k)
-  const double cwm = (col0 + e > 0) ? cf.hm2 : 0.0;
-  const double cem = (col0 + e + 1 < N) ? cf.hm2 : 0.0;
-  const double up = -cf.j_lin_up;
-  int fo[NB][4], fw[NB][4], fe[NB][4];
-  unsigned fv = 0;
-#pragma unroll
-  for (int ab = 0; ab < NB; ++ab)
-#pragma unroll
-    for (int ks = 0; ks < 4; ++ks) {
-      const int j = ab * 16 + ks * 4 + cq;
-      const bool isV = j < kg;
-      const int jr = isV ? j : 0;
-      fo[ab][ks] = jr * GS_CS + e;
-      fw[ab][ks] = e > 0 ? jr * GS_CS + e - 1 : hb + 4 * jr + 1;
-      fe[ab][ks] = e < GS_SW - 1 ? jr * GS_CS + e + 1 : hb + 4 * jr + 2;
-      fv |= unsigned(isV) << (ab * 4 + ks);
-    }
-  const int orr = RT * GS_CS + wave * 16 + cq;
-  const int kq = k & ~3;                            // 16 ab + 4 ks of the fragment holding column k
-  const bool gq = cq == (k & 3);                    // this lane holds column k there
-
-  // lane roles: the halo lane group hg never holds Gram column k; writers are the other groups
-  const int hg = (k + 2) & 3;
-  const bool hwave = wave == 0 || wave == GS_NW - 1;
-  const bool hedge = (wave == 0 && pl == 0) || (wave == GS_NW - 1 && pl == 15);
-  const int hs = wave == 0 ? 1 : 2;                 // halo element of point -1 / 128
-  const int64_t hcol = wave == 0 ? col0 - 1 : col0 + GS_SW;
-  const bool hin = hcol >= 0 && hcol < N;
-  const bool hl = hedge && cq == hg;                // g stencil at the halo point
-  const bool wr_w = cq == ((hg + 1) & 3), wr_x = cq == ((hg + 2) & 3);
-  const bool wr_g = (cq == ((hg + 3) & 3)) || hl, wr_r = cq == ((hg + 1) & 3);
-  // g stencil: r_old at the task point and its in-row neighbours, g's ring position
-  int oRc, oRw, oRe, oG;
-  int64_t gcC;
-  if (hl) {
-    oRc = hb + 4 * (k + 1) + hs;
-    oRw = wave == 0 ? hb + 4 * (k + 1) : RO * GS_CS + GS_SW - 1;
-    oRe = wave == 0 ? RO * GS_CS : hb + 4 * (k + 1) + 3;
-    oG = hb + 4 * k + hs;
-    gcC = hcol;
-  } else {
-    oRc = RO * GS_CS + e;
-    oRw = e > 0 ? oRc - 1 : hb + 4 * (k + 1) + 1;
-    oRe = e < GS_SW - 1 ? oRc + 1 : hb + 4 * (k + 1) + 2;
-    oG = RG * GS_CS + e;
-    gcC = col0 + e;
-  }
-  const bool cw = gcC > 0, ce = gcC < N - 1, cin = gcC >= 0 && gcC < N;
-  // r_t stencil: x at point e and its in-row neighbours
-  const int oXc = RX * GS_CS + e;
-  const int oXw = e > 0 ? oXc - 1 : hb + 4 * (k + 2) + 1;
-  const int oXe = e < GS_SW - 1 ? oXc + 1 : hb + 4 * (k + 2) + 2;
-  const bool fhw = col0 + e > 0, fhe = col0 + e < N - 1;
-
-  double ss = 0.0, mx = 0.0, rr = 0.0;              // sum w^2, max |w|, sum r_t^2 (writer lanes)
-  double hacc[NB][4];                               // V_j . g at this lane's points, j = 16ab + 4ks + cq
-#pragma unroll
-  for (int ab = 0; ab < NB; ++ab)
-#pragma unroll
-    for (int ks = 0; ks < 4; ++ks) hacc[ab][ks] = 0.0;
-
-  // trial point at one point (offset oV, column stride sV): w and x from this group's columns
-  auto trial_pt = [&](const double* Lp, int oV, int sV, double& wv, double& xv) {
-    if (GNK_FDBG & 1) {
-      wv = Lp[oV + (k - 1) * sV];
-      xv = wv;
-      return;
-    }
-    double sw = 0.0, sx = 0.0;
-#pragma unroll
-    for (int s = 0; s < JS; ++s) {
-      const double v = Lp[oV + jq[s] * sV];
-      sw = fma(v, hq[s], sw);
-      sx = fma(v, eq[s], sx);
-    }
-    sw = sum_rows4(sw);
-    sx = sum_rows4(sx);
-    wv = Lp[oV + (k - 1) * sV] - sw;
-    xv = fma(wv, ekp, sx);
-  };
-  // B: w and x of grid row xr (ring slot Lp) at point e (and the halo point in waves 0 / 7); direct:
-  // store them (the prologue), else the step loop stores them one step later (see st_ptr)
-  auto trial_row = [&](double* Lp, int64_t xr, double& xe, double& xh, double& we, bool direct) {
-    double wv, xv;
-    trial_pt(Lp, e, GS_CS, wv, xv);
-    const bool own = xr >= x0 && xr < x1;
-    const int64_t gi = (G + xr) * N + col0 + e;
-    if (wr_w) {
-      Lp[(k - 1) * GS_CS + e] = wv;
-      if (own) {
-        // the range's first and last rows are read as raw g by the neighbouring ranges' blocks:
-        // staged in wedge, copied into V after the pass (k_fused_wedge)
-        if (direct) {
-          if (xr == x0 || xr == x1 - 1) wedge[(size_t(idx) * 2 + (xr == x0 ? 0 : 1)) * GS_SW + e] = wv;
-          else wcol[gi] = wv;
-        }
-        ss += wv * wv;
-        mx = nan_max(mx, fabs(wv));
-      }
-    }
-    if (wr_x) {
-      Lp[RX * GS_CS + e] = xv;
-      if (own && direct) xout[gi] = xv;
-    }
-    xe = xv;
-    we = wv;
-    if (hwave && !(GNK_FDBG & 8)) {
-      double wh, xhv;
-      trial_pt(Lp, hb + hs, 4, wh, xhv);
-      if (!hin) {
-        wh = 0.0;
-        xhv = 0.0;
-      }
-      if (hl) {
-        Lp[hb + 4 * (k - 1) + hs] = wh;
-        Lp[hb + 4 * (k + 2) + hs] = xhv;
-      }
-      xh = xhv;
-    }
-  };
-  // C: g of grid row xr (r_old rows xr-1 / xr / xr+1 in slots Lq / Lr / Ls) from x(xr) at the task point;
-  // d1 = jdiag(x), ex1 = LAMBDA exp(x) (the residual's exp term)
-  auto g_row = [&](const double* Lq, double* Lr, const double* Ls, int64_t xr, double xt, double& d1,
-                   double& ex1, bool direct) -> double {
-    ex1 = (cf.lam_zero || (GNK_FDBG & 2)) ? xt : cf.lam * exp(xt);
-    d1 = cf.lam_zero ? cf.j_lin_diag : cf.j_lin_diag + ex1;
-    const int64_t grow = geo.row0 + xr;
-    double gv = (GNK_FDBG & 2) ? Lr[oRc] : -vjp_pt(cf, d1, Lq[oRc], Lr[oRw], cw, Lr[oRc], Lr[oRe], ce, Ls[oRc]);
-    if (grow < 0 || grow >= N || !cin) gv = 0.0;
-    if (wr_g) {
-      Lr[oG] = gv;
-      if (direct && !hl && xr >= x0 && xr < x1) gcol[(G + xr) * N + col0 + e] = gv;
-    }
-    return gv;
-  };
-  // D: r_t of grid row xr at point e (pde_operator in fwd_pt's order, with the trial point's exp)
-  auto r_row = [&](const double* Ln_, double* Lc_, double xc, double xs_, double exc) -> double {
-    if (GNK_FDBG & 4) {
-      const double rt = Lc_[RY * GS_CS + e] - xc;
-      if (wr_r) Lc_[RT * GS_CS + e] = rt;
-      return rt;
-    }
-    double l = 0.0 + cf.l_off * Ln_[oXc];
-    if (fhw) l = l + cf.l_off * Lc_[oXw];
-    l = l + cf.l_diag * xc;
-    if (fhe) l = l + cf.l_off * Lc_[oXe];
-    l = l + cf.l_off * xs_;
-    double dx = 0.0 + cf.dx_diag * xc;
-    dx = dx + cf.dx_up * xs_;
-    double f = l + dx;
-    if (!cf.lam_zero) f = f + exc;
-    const double rt = Lc_[RY * GS_CS + e] - f;
-    if (wr_r) {
-      Lc_[RT * GS_CS + e] = rt;
-      rr += rt * rt;
-    }
-    return rt;
-  };
-  // the fragments' diagonal -jdiag at point e (lanes of the g stencil at a halo point take it from
-  // the same point's lane in the next group)
-  auto own_dn = [&](double d1) {
-    double dn = -d1;
-    if (hwave) {
-      const double dno = __shfl_xor(dn, 16);
-      if (hl) dn = dno;
-    }
-    return dn;
-  };
-  // the residual's exp term at point e, the same way
-  auto own_ex = [&](double ex) {
-    if (hwave) {
-      const double o = __shfl_xor(ex, 16);
-      if (hl) ex = o;
-    }
-    return ex;
-  };
-
-  double a[NB][4];
-  d4 qp[NB];
-  auto transform = [&](d4 (&qv)[NB]) {
-#pragma unroll
-    for (int cb = 0; cb < NB; ++cb) {
-      d4 h0 = d4{0.0, 0.0, 0.0, 0.0}, h1 = d4{0.0, 0.0, 0.0, 0.0};
-      int n = 0;
-#pragma unroll
-      for (int ab = 0; ab <= cb; ++ab)
-#pragma unroll
-        for (int ks = 0; ks < nks(ab); ++ks, ++n) {
-          if (n & 1) h1 = mfma64(a[ab][ks], rB[cb][ab][ks], h1);
-          else h0 = mfma64(a[ab][ks], rB[cb][ab][ks], h0);
-        }
-      qv[cb] = h0 + h1;
-    }
-  };
-  auto gram = [&](const d4 (&qv)[NB], const double* Lr) {
-    acc = mfma64(qv[0][0], qv[0][0], acc);
-    acc1 = mfma64(qv[0][1], qv[0][1], acc1);
-    acc = mfma64(qv[0][2], qv[0][2], acc);
-    acc1 = mfma64(qv[0][3], qv[0][3], acc1);
-    if (NB == 2) {
-#pragma unroll
-      for (int t = 0; t < TMAX; ++t) {
-        if (t < tail) {
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            double yt;
-            switch (t) {
-              case 0: yt = bcast_row<0>(qv[NB - 1][i]); break;
-              case 1: yt = bcast_row<1>(qv[NB - 1][i]); break;
-              case 2: yt = bcast_row<2>(qv[NB - 1][i]); break;
-              case 3: yt = bcast_row<3>(qv[NB - 1][i]); break;
-              case 4: yt = bcast_row<4>(qv[NB - 1][i]); break;
-              case 5: yt = bcast_row<5>(qv[NB - 1][i]); break;
-              case 6: yt = bcast_row<6>(qv[NB - 1][i]); break;
-              default: yt = bcast_row<7>(qv[NB - 1][i]); break;
-            }
-#pragma unroll
-            for (int cb = 0; cb < NB; ++cb) ev[t * NB + cb] = fma(yt, qv[cb][i], ev[t * NB + cb]);
-          }
-        }
-      }
-    }
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const double rv = Lr[orr + 4 * i];
-#pragma unroll
-      for (int cb = 0; cb < NB; ++cb) ev[ER + cb] = fma(rv, qv[cb][i], ev[ER + cb]);
-      ev[RR] = fma(rv, rv, ev[RR]);
-    }
-  };
-
-  // Row x+3 is issued at the start of step x and waited for at its end.  The step's global stores
-  // (w, x at row x+2, g at row x+1, r_t at row x: one quantity per lane group, so one store
-  // instruction per wave) are issued at the start of the NEXT step, right after its DMA, so that the
-  // end-of-step vmcnt(1) waits for the DMA but not for the stores; lanes with nothing to store write
-  // their own word of `trash` (the count of vector-memory instructions per step stays fixed).
-  const int gw_ = (hg + 1) & 3, gx_ = (hg + 2) & 3, gg_ = (hg + 3) & 3;
-  double* const trash_l = trash + size_t(blockIdx.x) * (64 * GS_NW) + tid;
-  double* st_ptr = trash_l;
-  double st_val = 0.0;
-  if (x0 < x1) {
-    // ring slots: sq / sn / sc / ss / sp = rows x-2 .. x+2; sq receives row x+3 during step x
-    int sq = 4, sn = 0, sc = 1, ss_ = 2, sp = 3;
-    issue_row(x0 - 2, sq);
-    issue_row(x0 - 1, sn);
-    issue_row(x0, sc);
-    issue_row(x0 + 1, ss_);
-    issue_row(x0 + 2, sp);
-    __builtin_amdgcn_s_waitcnt(waitcnt_vm_lgkm0(0));
-    __builtin_amdgcn_s_barrier();
-    // prologue: trial points of rows x0-1 .. x0+1, g of rows x0-1 and x0 (stored directly)
-    double xm1, xt0, xt1, hm1 = 0.0, h0 = 0.0, h1 = 0.0, wdum;
-    trial_row(lds + sn * slotd, x0 - 1, xm1, hm1, wdum, true);
-    trial_row(lds + sc * slotd, x0, xt0, h0, wdum, true);
-    trial_row(lds + ss_ * slotd, x0 + 1, xt1, h1, wdum, true);
-    double d1, ex0, exm;
-    (void)g_row(lds + sq * slotd, lds + sn * slotd, lds + sc * slotd, x0 - 1, hl ? hm1 : xm1, d1, exm, true);
-    (void)g_row(lds + sn * slotd, lds + sc * slotd, lds + ss_ * slotd, x0, hl ? h0 : xt0, d1, ex0, true);
-    ex0 = own_ex(ex0);
-    double dn = own_dn(d1);                         // row x0
-    __builtin_amdgcn_s_waitcnt(waitcnt_vm_lgkm0(0));
-    __builtin_amdgcn_s_barrier();
-    for (int64_t x = x0; x < x1; ++x) {
-      issue_row(x + 3, sq);
-      asm volatile("" ::: "memory");                // the store stays behind the DMA (vmcnt order)
-      *st_ptr = st_val;                             // the previous step's store (or trash)
-      double* Ln = lds + sn * slotd;
-      double* Lc = lds + sc * slotd;
-      double* Ls = lds + ss_ * slotd;
-      double* Lp = lds + sp * slotd;
-      double xt2, h2 = 0.0, w2;
-      trial_row(Lp, x + 2, xt2, h2, w2, false);     // B: row x+2
-      double d1n, ex1;
-      const double gnext = g_row(Lc, Ls, Lp, x + 1, hl ? h1 : xt1, d1n, ex1, false);   // C: row x+1
-      const double rt = r_row(Ln, Lc, xt0, xt1, ex0);  // D: row x
-      {
-        // next step's store: lane group gw_ -> w(x+2), gx_ -> x(x+2), gg_ -> g(x+1), hg -> r_t(x)
-        const int64_t r2 = (G + x + 2) * N + col0 + e, r1 = (G + x + 1) * N + col0 + e;
-        const int64_t r0 = (G + x) * N + col0 + e;
-        const bool own2 = x + 2 < x1, own1 = x + 1 < x1;
-        double* pw = own2 ? (x + 2 == x1 - 1 ? wedge + (size_t(idx) * 2 + 1) * GS_SW + e : wcol + r2) : trash_l;
-        double* px = own2 ? xout + r2 : trash_l;
-        double* pg = own1 ? gcol + r1 : trash_l;
-        double* pr = rout + r0;
-        st_ptr = cq == gw_ ? pw : (cq == gx_ ? px : (cq == gg_ ? pg : pr));
-        st_val = cq == gw_ ? w2 : (cq == gx_ ? xt2 : (cq == gg_ ? gnext : rt));
-      }
-      const double gcur = Lc[RG * GS_CS + e];       // g(x) at point e (step x-1)
-#pragma unroll
-      for (int ab = 0; ab < NB; ++ab)
-#pragma unroll
-        for (int ks = 0; ks < nks(ab); ++ks) {
-          const int o = fo[ab][ks];
-          const double vn = Ln[o], vw = Lc[fw[ab][ks]], vc = Lc[o], ve = Lc[fe[ab][ks]];
-          double vs = Ls[o];
-          if (ab * 16 + ks * 4 == kq && gq) vs = gnext;
-          hacc[ab][ks] = fma(vc, gcur, hacc[ab][ks]);
-          double sv;
-          if (ab == NB - 1 && ks == nks(ab) - 1) {
-            const bool isV = (fv >> (ab * 4 + ks)) & 1;
-            const double cn = isV ? cf.hm2 : 0.0, cw2 = isV ? cwm : 0.0, cc = isV ? dn : 0.0;
-            const double ce2 = isV ? cem : 0.0, cs = isV ? up : 0.0;
-            sv = cn * vn;
-            sv = fma(cw2, vw, sv);
-            sv = fma(cc, vc, sv);
-            sv = fma(ce2, ve, sv);
-            sv = fma(cs, vs, sv);
-          } else {
-            sv = cf.hm2 * vn;
-            sv = fma(cwm, vw, sv);
-            sv = fma(dn, vc, sv);
-            sv = fma(cem, ve, sv);
-            sv = fma(up, vs, sv);
-          }
-          a[ab][ks] = sv;
-        }
-      dn = own_dn(d1n);                             // row x+1
-      d4 qv[NB];
-      transform(qv);
-      if (x > x0) gram(qp, Ln);                     // row x-1: its r_t is in slot n
-#pragma unroll
-      for (int cb = 0; cb < NB; ++cb) qp[cb] = qv[cb];
-      xt0 = xt1;
-      xt1 = xt2;
-      h1 = h2;
-      ex0 = own_ex(ex1);
-      const int t = sq;
-      sq = sn;
-      sn = sc;
-      sc = ss_;
-      ss_ = sp;
-      sp = t;
-      __builtin_amdgcn_s_waitcnt(waitcnt_vm_lgkm0(1));   // row x+3 landed (this step's store may fly)
-      __builtin_amdgcn_s_barrier();
-    }
-    *st_ptr = st_val;                               // the last step's store
-    gram(qp, lds + sn * slotd);                     // last row x1-1
-  }
-  __builtin_amdgcn_s_waitcnt(waitcnt_vm_lgkm0(0));
-  __builtin_amdgcn_s_barrier();
-
-  acc = acc + acc1;
-  constexpr int PL = 256 + 64 * NACC;
-  double* red = lds;
-  for (int w = 0; w < GS_NW; ++w) {
-    if (wave == w) {
-#pragma unroll
-      for (int ii = 0; ii < 4; ++ii) {
-        double* dst = red + lane * 4 + ii;
-        *dst = (w == 0) ? acc[ii] : *dst + acc[ii];
-      }
-#pragma unroll
-      for (int q = 0; q < NACC; ++q) {
-        double* dst = red + 256 + lane * NACC + q;
-        *dst = (w == 0) ? ev[q] : *dst + ev[q];
-      }
-    }
-    __syncthreads();
-  }
-  double* out = partial + size_t(blockIdx.x) * PL;
-  for (int t = tid; t < PL; t += blockDim.x) out[t] = red[t];
-  // trial partial: per wave [sum r^2, sum w^2, max |w|, h_j (lane groups summed over their 16 points)]
-  double* tr = lds + 1024;
-#pragma unroll
-  for (int ab = 0; ab < NB; ++ab)
-#pragma unroll
-    for (int ks = 0; ks < 4; ++ks) {
-      double v = hacc[ab][ks];
-#pragma unroll
-      for (int o = 1; o < 16; o <<= 1) v += __shfl_xor(v, o);
-      const int j = ab * 16 + ks * 4 + cq;
-      if (pl == 0 && j < k) tr[wave * GF_TPL + 3 + j] = v;
-    }
-  const double rs = wave_sum(rr), sws = wave_sum(ss), mxw = wave_max(mx);
-  if (lane == 0) {
-    tr[wave * GF_TPL] = rs;
-    tr[wave * GF_TPL + 1] = sws;
-    tr[wave * GF_TPL + 2] = mxw;
-  }
-  __syncthreads();
-  if (tid < 3 + k) {
-    double s = tr[tid];
-    for (int w = 1; w < GS_NW; ++w) s = (tid == 2) ? nan_max(s, tr[w * GF_TPL + tid]) : s + tr[w * GF_TPL + tid];
-    tpart[size_t(blockIdx.x) * GF_TPL + tid] = s;
-  }
-}
-
 // ---------------------------------------------------------------- VALU Gram pass (k <= 8, with r)
 // An f64 MFMA issues no more flops per cycle than f64 VALU FMAs on MI355X (tools/probes), and a
 // 16 x 16 MFMA tile spends most of them on padding when the Gram has K + 1 <= 9 columns.  Here the
@@ -2882,14 +2340,13 @@ __global__ __launch_bounds__(64) void k_gram_scatter_v(const double* __restrict_
 }
 
 // staged-kernel scatter: red = block-summed partials [256 MFMA tile | 64 lanes x NACC]; lane groups
-// g = l >> 4 (points) summed in order 0..3.  tail = k - 16 columns in the VALU sums (nb = 2):
-//   lead = 0 (k_gram_sf): the MFMA tile holds columns 0..15, the VALU sums rows 16 + t;
-//   lead = 1 (k_gram_s):  the VALU sums hold the lead columns t < tail, the MFMA tile columns tail..tail+15;
-// then G[k][c], G[k][k] from the r sums.
+// g = l >> 4 (points) summed in order 0..3.  nb = 1: the MFMA tile holds columns 0..15; nb = 2 (lead
+// first, k_gram_s): the VALU sums hold the tail = k - 16 lead columns, the MFMA tile columns
+// tail..tail+15; then G[k][c], G[k][k] from the r sums.
 __global__ __launch_bounds__(BLOCK) void k_gram_scatter_s(const double* __restrict__ red, int nb, int nacc, int k,
-                                                          int has_r, int KP, double* __restrict__ Gout, int lead) {
+                                                          int has_r, int KP, double* __restrict__ Gout) {
   const int tail = nb == 2 ? k - 16 : 0;
-  const int c0 = (nb == 2 && lead) ? tail : 0;       // first column of the MFMA tile
+  const int c0 = tail;                               // first column of the MFMA tile
   const int er = nb == 1 ? 0 : nacc - 3, rr = er + nb;
   const double* ev = red + 256;
   auto lsum = [&](int col_in_block, int q) {
@@ -3303,90 +2760,6 @@ __global__ __launch_bounds__(64) void k_lls_next(int k, int pending, const doubl
   }
 }
 
-// The fused pass's transform: k_lls_next's T' without the pending column's projection
-// and with the raw scale of this step's pending column, which the pass itself measures:
-//   T_f = [[diag(a) R^-1, 0], [0, 1]] (+ the r column), a = [sc[:k-1], 1].
-__global__ __launch_bounds__(64) void k_lls_fused_t(int k, const double* __restrict__ out, const double* __restrict__ sc,
-                                                    int kpn, double* __restrict__ T) {
-  const double* rinv = out + 3 + k + 2 * k * k;
-  for (int idx = threadIdx.x; idx < kpn * kpn; idx += 64) {
-    const int i = idx / kpn, j = idx % kpn;
-    double t = 0.0;
-    if (i < k && j < k) t = (i == k - 1 ? 1.0 : sc[i]) * rinv[i * k + j];
-    else if (i == j && i <= k + 1) t = 1.0;
-    T[idx] = t;
-  }
-}
-
-// After the fused pass: the next step's Gram and least-squares inputs (k_lls_next's outputs) from the
-// pass's Gram Gf of [J V T_f | J g | r] and its trial scalars pack (both rank-summed).  The pending
-// column's projection is applied in Gram space: with hh' = sc' (sc' h) (k_lls_next) and
-// beta = T_f[:k, :k]^-1 hh' = R diag(1 / a) hh', the column J w' = J g - J V hh' is Y_k - Y[:, :k] beta:
-//   G'[i][k] = Gf[i][k] - (Gf[i][:k] . beta)  (i != k),  G'[k][k] = Gf[k][k] - beta . (2 Gf[:k][k] - Gf[:k,:k] beta).
-// When rho^2 = G'[k][k] / Gf[k][k] < rho2_min the difference has cancelled too far for the Gram-space
-// form; G'[k][k] = NaN then makes k_lls report "not SPD" and the host re-runs the pass on the
-// materialised column.
-__global__ __launch_bounds__(64) void k_lls_proj(int k, const double* __restrict__ out, const double* __restrict__ etry,
-                                                 const double* __restrict__ pack, const double* __restrict__ sc,
-                                                 int kpn, const double* __restrict__ Gf, double rho2_min,
-                                                 double* __restrict__ Gp, double* __restrict__ Pn,
-                                                 double* __restrict__ sddn, double* __restrict__ en,
-                                                 double* __restrict__ hhn, double* __restrict__ scn) {
-  __shared__ double hs[LS_KMAX], beta[LS_KMAX], q[LS_KMAX + 2];
-  const int l = threadIdx.x;
-  const int kn = k + 1;
-  const double* R = out + 3 + k;
-  const double nrm = sqrt(pack[1]);
-  for (int j = l; j < k; j += 64) {
-    const double scj = (j == k - 1) ? 1.0 / nrm : sc[j];
-    scn[j] = scj;
-    sddn[j] = scj;
-    en[j] = etry[j];
-    const double h = scj * (scj * pack[3 + j]);
-    hhn[j] = h;
-    hs[j] = (j == k - 1) ? h : h / sc[j];
-  }
-  if (l == 0) {
-    sddn[k] = 1.0;
-    en[k] = 0.0;
-  }
-  for (int idx = l; idx < kn * kn; idx += 64) {
-    const int i = idx / kn, j = idx % kn;
-    double pv = 0.0;
-    if (i < k && j < k) pv = (j == k - 1) ? R[i * k + j] / nrm : R[i * k + j];
-    else if (i == k && j == k) pv = 1.0;
-    Pn[idx] = pv;
-  }
-  __syncthreads();
-  if (l < k) {
-    double s = 0.0;
-    for (int j = l; j < k; ++j) s = s + R[l * k + j] * hs[j];
-    beta[l] = s;
-  }
-  __syncthreads();
-  // q_i = Gf[i][:k] . beta for the rows i < k and the r row (k + 1)
-  if (l < k || l == k + 1) {
-    double s = 0.0;
-    for (int m = 0; m < k; ++m) s = s + Gf[l * kpn + m] * beta[m];
-    q[l] = s;
-  }
-  for (int idx = l; idx < kpn * kpn; idx += 64) Gp[idx] = Gf[idx];
-  __syncthreads();
-  if (l < k || l == k + 1) {
-    const double v = Gf[l * kpn + k] - q[l];
-    Gp[l * kpn + k] = v;
-    Gp[k * kpn + l] = v;
-  }
-  if (l == 0) {
-    double t = 0.0;
-    for (int m = 0; m < k; ++m) t = t + beta[m] * (2.0 * Gf[m * kpn + k] - q[m]);
-    const double g0 = Gf[k * kpn + k];
-    double gkk = g0 - t;
-    if (!(gkk >= rho2_min * g0)) gkk = NAN;
-    Gp[k * kpn + k] = gkk;
-  }
-}
-
 // ---------------------------------------------------------------- probes (tooling)
 __global__ void k_probe_mfma(double* out, int iters) {
   d4 c0 = {0, 0, 0, 0}, c1 = c0, c2 = c0, c3 = c0;
@@ -3562,15 +2935,6 @@ __device__ int d_sum_max_flags[2] = {0, 1};
 const int* sum_max_flags() {
   void* p = nullptr;
   (void)hipGetSymbolAddress(&p, HIP_SYMBOL(d_sum_max_flags));
-  return static_cast<const int*>(p);
-}
-
-// {sum, sum, max, sum ...} flags of a first trial's pack [sum r^2, sum w^2, max |w|, h ...]
-__device__ int d_pack_flags[GF_TPL] = {0, 0, 1};
-
-const int* pack_flags() {
-  void* p = nullptr;
-  (void)hipGetSymbolAddress(&p, HIP_SYMBOL(d_pack_flags));
   return static_cast<const int*>(p);
 }
 
@@ -4074,7 +3438,7 @@ int gnk_gram(gnk_ctx* ctx, const double* u, const double* V, int64_t ldv, int k,
       rcs = wreduce(ctx, ctx->scratch, int(nwg), PL, int64_t(PL), PL, 0, nullptr, red);
       if (rcs) return rcs;
       hipLaunchKernelGGL(k_gram_scatter_s, dim3(4), dim3(BLOCK), 0, ctx->stream, red, nbs, nacc, k, r ? 1 : 0, KP,
-                         G_out, 1);
+                         G_out);
       return check_launch(ctx, "gram scatter (staged)");
     }
   }
@@ -4565,104 +3929,6 @@ int gnk_lls_solve(gnk_ctx* ctx, const double* Gm, int kp, int k, const double* P
   if (!Gm || !P || !sdd || !e || !out || !e_try) return fail(ctx, "lls_solve: NULL argument");
   hipLaunchKernelGGL(k_lls, dim3(1), dim3(64), 0, ctx->stream, Gm, kp, k, P, rescale, sdd, e, out, e_try);
   return check_launch(ctx, "lls_solve");
-}
-
-int gnk_lls_fused_t(gnk_ctx* ctx, int k, const double* out, const double* sc, int kp_next, double* T_next) {
-  if (!ctx) return -1;
-  if (k < 2 || k + 1 > LS_KMAX) return fail(ctx, "lls_fused_t: k + 1 must be in [3, gnk_lls_max_k()]");
-  if (kp_next < k + 2) return fail(ctx, "lls_fused_t: kp_next < k + 2");
-  if (!out || !sc || !T_next) return fail(ctx, "lls_fused_t: NULL argument");
-  hipLaunchKernelGGL(k_lls_fused_t, dim3(1), dim3(64), 0, ctx->stream, k, out, sc, kp_next, T_next);
-  return check_launch(ctx, "lls_fused_t");
-}
-
-int gnk_lls_proj(gnk_ctx* ctx, int k, const double* out, const double* e_try, const double* pack, const double* sc,
-                 int kp_next, const double* G_fused, double rho2_min, double* G_next, double* P_next,
-                 double* sdd_next, double* e_next, double* hh_next, double* sc_next) {
-  if (!ctx) return -1;
-  if (k < 2 || k + 1 > LS_KMAX) return fail(ctx, "lls_proj: k + 1 must be in [3, gnk_lls_max_k()]");
-  if (kp_next < k + 2) return fail(ctx, "lls_proj: kp_next < k + 2");
-  if (!out || !e_try || !pack || !sc || !G_fused || !G_next || !P_next || !sdd_next || !e_next || !hh_next || !sc_next)
-    return fail(ctx, "lls_proj: NULL argument");
-  if (G_fused == G_next) return fail(ctx, "lls_proj: G_next must not alias G_fused");
-  hipLaunchKernelGGL(k_lls_proj, dim3(1), dim3(64), 0, ctx->stream, k, out, e_try, pack, sc, kp_next, G_fused,
-                     rho2_min, G_next, P_next, sdd_next, e_next, hh_next, sc_next);
-  return check_launch(ctx, "lls_proj");
-}
-
-int gnk_gram_fused_max_k(void) { return GF_KMAX; }
-
-int gnk_gram_fused(gnk_ctx* ctx, double* V, int64_t ldv, int k, const double* e_try, const double* hh,
-                   const double* r_old, const double* y, const double* T, int64_t ldt, double* x, double* r_t,
-                   double* G_out, double* pack_out) {
-  if (!ready(ctx)) return -1;
-  if (k < 2 || k > GF_KMAX) return fail(ctx, "gram_fused: k must be in [2, gnk_gram_fused_max_k()]");
-  if (ctx->geo.N % GS_SW != 0) return fail(ctx, "gram_fused: the grid size must be a multiple of 128");
-  if (!V || !e_try || !hh || !r_old || !y || !T || !x || !r_t || !G_out || !pack_out)
-    return fail(ctx, "gram_fused: NULL argument");
-  const int kg = k + 1;
-  const int KP = gnk_gram_padded_dim(kg, 1);
-  if (ldt != KP) return fail(ctx, "gram_fused: T must be the kp x kp augmented transform of k + 1 columns (ldt == kp)");
-  const int64_t slab = (ctx->geo.nrows + 2 * G) * ctx->geo.N;
-  if (ldv < slab) return fail(ctx, "gram_fused: ldv shorter than a slab vector");
-  auto in_v = [&](const double* p) { return p >= V && p < V + int64_t(k + 1) * ldv; };
-  if (in_v(x) || in_v(r_t) || in_v(r_old) || in_v(y)) return fail(ctx, "gram_fused: a vector aliases V[:, :k+1]");
-  if (r_t == r_old || x == r_t || x == r_old) return fail(ctx, "gram_fused: x, r_t and r_old must be distinct");
-  const int nbs = kg <= 16 ? 1 : 2;
-  const int ksl = ((kg - 16 * (nbs - 1)) + 3) / 4;
-  const int L = (k + 3 + GS_NW - 1) / GS_NW;
-  const size_t slot_bytes = ((size_t(k) + 5) * GS_CS + 128) * sizeof(double);
-  const size_t lds = size_t(5) * slot_bytes;
-  if (L > 3 || lds > 160 * 1024) return fail(ctx, "gram_fused: ring does not fit");
-  const int nacc = gs_nacc(nbs, ksl);
-  const int PL = 256 + 64 * nacc;
-  const int64_t nstrips = ctx->geo.N / GS_SW;
-  const int64_t nrows = ctx->geo.nrows;
-  int64_t nranges = std::max<int64_t>(1, std::min<int64_t>(nrows, int64_t(ctx->num_cus) / nstrips));
-  const int64_t rpr = (nrows + nranges - 1) / nranges;
-  nranges = (nrows + rpr - 1) / rpr;
-  const int64_t nwg = nstrips * nranges;
-  const size_t toff = (size_t(nwg) * PL + 1) & ~size_t(1);
-  const size_t eoff = toff + size_t(nwg) * GF_TPL;
-  const size_t xoff = eoff + size_t(nwg) * 2 * GS_SW;
-  if (nwg > 4096 || xoff + size_t(nwg) * 64 * GS_NW > SCRATCH_DOUBLES - size_t(PL))
-    return fail(ctx, "gram_fused: scratch too small");
-  double* tpart = ctx->scratch + toff;
-  double* wedge = ctx->scratch + eoff;
-  double* trash = ctx->scratch + xoff;             // per-thread sink of the deferred stores
-  const int64_t nown = nrows * ctx->geo.N;
-  // algorithmic bytes: read V (k), r_old, y; write w, x, r_t, g
-  TimedLaunch tl(ctx, GNK_TIMER_GRAM, 8.0 * double(nown) * double(k + 6));
-#define GRAMF(NBV, LV, KV)                                                                                          \
-  hipLaunchKernelGGL((k_gram_sf<NBV, LV, KV>), dim3(unsigned(nwg)), dim3(64 * GS_NW), lds, ctx->stream, V, ldv, k, \
-                     e_try, hh, r_old, y, T, KP, x, r_t, ctx->geo, ctx->coef, rpr, ctx->scratch, tpart, wedge, trash)
-#define GRAMF_K(NBV, LV)                                                                  \
-  do {                                                                                    \
-    if (ksl == 1) GRAMF(NBV, LV, 1); else if (ksl == 2) GRAMF(NBV, LV, 2);                \
-    else if (ksl == 3) GRAMF(NBV, LV, 3); else GRAMF(NBV, LV, 4);                         \
-  } while (0)
-  if (nbs == 1) {
-    if (L == 1) GRAMF_K(1, 1); else if (L == 2) GRAMF_K(1, 2); else GRAMF_K(1, 3);
-  } else {
-    GRAMF(2, 3, 1);                                 // k + 1 = 17 .. 20: one tail k-step, L = 3
-  }
-#undef GRAMF_K
-#undef GRAMF
-  tl.done();
-  int rc = check_launch(ctx, "gram_fused");
-  if (rc) return rc;
-  hipLaunchKernelGGL(k_fused_wedge, dim3(unsigned(nwg)), dim3(GS_SW), 0, ctx->stream, wedge,
-                     V + int64_t(k - 1) * ldv, ctx->geo, rpr);
-  rc = check_launch(ctx, "gram_fused wedge");
-  if (rc) return rc;
-  (void)hipMemsetAsync(G_out, 0, size_t(KP) * KP * sizeof(double), ctx->stream);
-  double* red = ctx->scratch + (SCRATCH_DOUBLES - size_t(PL));
-  rc = wreduce(ctx, ctx->scratch, int(nwg), PL, int64_t(PL), PL, 0, nullptr, red);
-  if (rc) return rc;
-  hipLaunchKernelGGL(k_gram_scatter_s, dim3(4), dim3(BLOCK), 0, ctx->stream, red, nbs, nacc, kg, 1, KP, G_out, 0);
-  rc = check_launch(ctx, "gram_fused scatter");
-  if (rc) return rc;
-  return wreduce(ctx, tpart, int(nwg), 3 + k, GF_TPL, 3 + k, 0, pack_flags(), pack_out);
 }
 
 // tooling: fp64 MFMA issue-rate probe (not part of the solver)

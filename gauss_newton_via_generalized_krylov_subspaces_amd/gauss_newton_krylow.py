@@ -26,7 +26,6 @@ every n- and m-sized operation of the loop runs in the HIP library (single GPU).
 """
 from __future__ import annotations
 
-import os
 from collections.abc import Callable
 from typing import Optional
 
@@ -67,7 +66,6 @@ class BratuOps:
     jacobian_is_free = True        # J(u) is u itself on the device: no evaluation to schedule
     fuse_trial = True              # the res_old first trial may carry the update products
     speculate = True               # the next step's solve may be enqueued before this one is read
-    FUSED_KMIN = 10                # Gram columns from which the first trial and the next Gram pass fuse
 
     def __init__(self, problem, y, comm=None, device=None, backend=None):
         self.dev = BratuDevice(problem, comm, device, backend)
@@ -107,27 +105,6 @@ class BratuOps:
         self.be.residual(x, self.y, r, pack[0:1])
         return self.comm.read_async(pack, shared, pinned)
 
-    def fused_gram_ok(self, kk):
-        """The fused trial + Gram pass covers a step over kk columns (the last pending):
-        the next Gram has kk + 1 columns in the staged kernel's range, on a 128-multiple grid."""
-        fmax = getattr(self, "_fmax", None)
-        if fmax is None:
-            fmax = self._fmax = int(self.be.gram_fused_max_k()) if hasattr(self.be, "gram_fused_max_k") else 0
-        return self.fused_kmin <= kk + 1 and kk <= fmax and self.dev.slab.N % 128 == 0
-
-    fused_kmin = int(os.environ.get("GNK_FUSED_KMIN", FUSED_KMIN))      # (tooling A/B: GNK_FUSED=0 disables)
-
-    def trial_fused(self, basis, coef_dev, x_t, r_old, r_t, T, G):
-        """``basis.trial_fused`` with the slab bookkeeping around it: r_old's ghost rows before (the
-        pass evaluates g on the first ghost row), and after it the ghost rows of r_t and of the
-        materialised column, which the pass writes on owned rows only."""
-        N, nrows = self.dev.slab.N, self.dev.slab.nrows
-        self.comm.halo(r_old, N, nrows)
-        pack, slot = basis.trial_fused(coef_dev, x_t, r_old, self.y, r_t, T, G)
-        self.comm.halo(r_t, N, nrows)
-        basis.halo_slot(slot - 1)
-        return pack, slot
-
     def to_host(self, x):
         return self.dev.slab.to_host(x)
 
@@ -146,8 +123,6 @@ class BratuOps:
 
 class GNKSolver:
     """One rank of the device GNK loop; ``step()`` runs exactly one outer iteration."""
-
-    FUSED_DEFAULT = False
 
     def __init__(self, problem, y, krylow_restart=None, tol=1e-8, max_iter=100, version="res_old",
                  comm: Optional[Comm] = None, device=None, backend=None, callback: Callable = None,
@@ -176,12 +151,6 @@ class GNKSolver:
         self._par = 0            # device buffer set of the current step's solve (two sets alternate)
         self._pin = None
         self.spec_stats = {"hit": 0, "miss": 0}
-        # fused first trial + next Gram pass: res_old on the Bratu slabs; measured at
-        # parity with the separate passes on MI355X (8192^2, k = 9..13), so off unless GNK_FUSED=1
-        fuse_on = os.environ.get("GNK_FUSED", "1" if self.FUSED_DEFAULT else "0") != "0"
-        self.fused = (self.pipeline and version == "res_old" and hasattr(self.ops, "fused_gram_ok")
-                      and hasattr(self.lls, "launch_fused_next") and fuse_on)
-        self.fused_stats = {"passes": 0, "fallback": 0}
 
     # -- pieces -------------------------------------------------------------------------
     def _residual(self, x, r) -> float:
@@ -226,20 +195,6 @@ class GNKSolver:
         self.basis.halo_slot(slot)
         sc_dev = self.basis.sc_device(par, ls.k)
         return self.lls.launch_next(x_t, self.basis, r_t, ls, self.comm.device_sum(rd), sc_dev, par)
-
-    def _launch_fused(self, ls, x_t, r_t, r_old, kk):
-        """This step's first trial and the next step's Gram pass in one pass over V (gnk_gram_fused), the
-        next step's solve enqueued after it (Gram-space projection + k_lls); -> (read handle, slot)."""
-        par = self._par ^ 1
-        lls = self.lls
-        sc_dev = self.basis.sc_device(par, ls.k)
-        T = lls.fused_transform(ls, sc_dev, par)
-        Gf = lls.bufs[par].Gf[:T.numel()]
-        pack, slot = self.ops.trial_fused(self.basis, ls.e_try, x_t, r_old, r_t, T, Gf)
-        rd = self.comm.read_async(pack[:3 + kk], ls.out, self._pinned())
-        self._spec = lls.launch_fused_next(ls, self.comm.sum_device(Gf), self.comm.device_sum(rd), sc_dev, par)
-        self.fused_stats["passes"] += 1
-        return rd, slot
 
     def _drop_spec(self):
         if self._spec is not None:
@@ -328,19 +283,12 @@ class GNKSolver:
                 rr, h, slot = self._trial_plain(e_ext + 1.0 * ds, x_t, r_t, r_old, prod)
                 return ls.d, ls.jdd, ds, rr, h, slot
             if ls.device:
-                fused = (self.fused and prod and pend and self._can_speculate(it, kk)
-                         and self.ops.fused_gram_ok(kk))
-                if fused:
-                    rd, slot = self._launch_fused(ls, x_t, r_t, r_old, kk)
-                else:
-                    pack, slot = basis.trial_first(None, x_t, r_old if prod else None, coef_dev=ls.e_try)
-                    rd = self.ops.residual_read(x_t, r_t, pack[:3 + kk], ls.out, self._pinned())
-                    if prod and self._can_speculate(it, kk):
-                        self._spec = self._launch_spec(ls, rd, x_t, r_t, slot)
+                pack, slot = basis.trial_first(None, x_t, r_old if prod else None, coef_dev=ls.e_try)
+                rd = self.ops.residual_read(x_t, r_t, pack[:3 + kk], ls.out, self._pinned())
+                if prod and self._can_speculate(it, kk):
+                    self._spec = self._launch_spec(ls, rd, x_t, r_t, slot)
                 host, lsout = self.comm.complete(rd, 2)
                 res = lls.finish(ls, lsout)
-                if res is None and ls.fused:
-                    self.fused_stats["fallback"] += 1
             else:
                 res = (ls.d, ls.jdd)
                 pack, slot = basis.trial_first(e_ext + 1.0 * (sdd * ls.d), x_t, r_old if prod else None)
@@ -367,8 +315,8 @@ class GNKSolver:
             ds = sdd * d
             if pend:
                 d = lls.resolve_pending(basis.last_norm)
-            # the speculative pass exchanged g's ghost rows (the fused pass leaves that to the update)
-            self._halo_done = self._spec is not None and not self._spec.fused
+            # the speculative pass exchanged g's ghost rows
+            self._halo_done = self._spec is not None
             return d, jdd, ds, float(host[0]), (host[3:3 + basis.k].copy() if prod else None), slot
 
     def step(self) -> bool:

@@ -58,7 +58,7 @@ def is_breakdown(sumsq: float, maxabs: float) -> bool:
 
 class DeviceKrylovBasis:
     deferred = True
-    FUSE_KMAX = 24                   # columns the fused first-trial kernel covers
+    FUSE_KMAX = 24                   # columns the first-trial kernel with the update products covers
 
     def __init__(self, dev, kmax: int):
         self.dev = dev
@@ -187,20 +187,6 @@ class DeviceKrylovBasis:
             self.be.upload(self._hh, self.pend["hh"])
         slot = self.enqueue_trial(self.k, pend, out, coef_dev, self._hh, pack, r_products)
         return pack, slot
-
-    def trial_fused(self, coef_dev, out, r_old, y, r_t, T, G):
-        """The res_old first trial fused with the next step's Gram pass (gnk_gram_fused):
-        the pending column (slot k) is materialised, out = V @ coef_dev over k + 1 columns, r_t = y - F(out),
-        g = -J(out)^T r_old into slot k + 1, pack = [sum r_t^2, sum w^2, max |w|, V^T g] (this rank) and G =
-        the Gram of [J(out) [V g] T | r_t].  Returns (pack, product slot)."""
-        if self.pend is None or self.pend["slot"] != self.k:
-            raise RuntimeError("trial_fused: needs the pending column in slot k")
-        kk = self.k + 1
-        if kk + 1 > self.kmax:
-            raise RuntimeError("trial_fused: no free slot for the update")
-        self.be.upload(self._hh, self.pend["hh"])
-        self.be.gram_fused(self.V, kk, coef_dev, self._hh, r_old, y, T, out, r_t, G, self.pack)
-        return self.pack, kk
 
     def resolve(self, sumsq: float, maxabs: float) -> bool:
         """Settle the pending column from its materialisation stats; True on breakdown (:66) --

@@ -40,9 +40,6 @@ import scipy.linalg
 EPS = np.finfo(np.float64).eps
 COND_ACCEPT = 30.0
 MAX_PASSES = 4
-# the fused pass's Gram-space projection (k_lls_proj) is used while ||J w'||^2 >= RHO2_MIN ||J g||^2:
-# its relative rounding error is then below u / RHO2_MIN ~ 2e-13
-RHO2_MIN = 1e-3
 
 
 def _chol_upper(G):
@@ -74,10 +71,9 @@ class DeviceSolve:
 
     device = True
 
-    def __init__(self, k, kp, M, M_cont, P, rescale, pending, G, out, e_try, fused=False):
+    def __init__(self, k, kp, M, M_cont, P, rescale, pending, G, out, e_try):
         self.k, self.kp, self.M, self.M_cont, self.P, self.rescale = k, kp, M, M_cont, P, rescale
         self.pending, self.G, self.out, self.e_try = pending, G, out, e_try
-        self.fused = fused          # G was formed in Gram space (k_lls_proj): never a first pass to continue
 
 
 class _LSBuffers:
@@ -87,7 +83,6 @@ class _LSBuffers:
     def __init__(self, be, L, kp):
         self.T = be.zeros(kp * kp)            # augmented transform of the first pass
         self.G = be.zeros(kp * kp)            # its Gram
-        self.Gf = be.zeros(kp * kp)           # the fused pass's Gram (before the Gram-space projection)
         self.P = be.zeros(L * L)
         self.sdd = be.zeros(L)
         self.e = be.zeros(L)
@@ -232,27 +227,6 @@ class CholQR2Solver:
         self.be.lls_solve(G, kp, k, B.P, True, B.sdd, B.e, B.out, B.etry)
         return DeviceSolve(k, kp, None, None, None, True, True, G, B.out[:3 + k + 3 * k * k], B.etry[:k])
 
-    def fused_transform(self, ls: "DeviceSolve", sc_dev, par):
-        """The transform of the fused pass (gnk_lls_fused_t): the next step's T without the pending
-        column's projection, from this step's device solve ``ls``."""
-        B = self.bufs[par]
-        kp = self.be.gram_dim(ls.k + 1, True)
-        self.be.lls_fused_t(ls.k, ls.out, sc_dev, kp, B.T)
-        return B.T[:kp * kp]
-
-    def launch_fused_next(self, ls: "DeviceSolve", Gf_sum, pack_sum, sc_dev, par):
-        """``launch_next`` after a fused pass: the pass's rank-summed Gram ``Gf_sum`` is projected in
-        Gram space (gnk_lls_proj) instead of a second pass over V, then k_lls solves."""
-        k = ls.k + 1
-        B = self.bufs[par]
-        kp = self.be.gram_dim(k, True)
-        self.be.lls_proj(ls.k, ls.out, ls.e_try, pack_sum, sc_dev, kp, Gf_sum, RHO2_MIN, B.G, B.P, B.sdd, B.e, B.hh,
-                         B.sc)
-        self.passes += 1
-        self.be.lls_solve(B.G, kp, k, B.P, True, B.sdd, B.e, B.out, B.etry)
-        return DeviceSolve(k, kp, None, None, None, True, True, B.G, B.out[:3 + k + 3 * k * k], B.etry[:k],
-                           fused=True)
-
     def adopt(self, ls: "DeviceSolve", basis):
         """A speculative solve became the current step: fill its host-side fields from the (now
         updated) host state -- the same values k_lls_next computed on the device."""
@@ -289,10 +263,6 @@ class CholQR2Solver:
         host from the first pass's Gram (a pending column has been settled by the trial since: it is
         mapped by ls.M_cont).  -> (d, jdd) in the units of the launch (tentative if it was pending)."""
         self.solves -= 1            # counted again by _passes
-        if ls.fused:
-            # a Gram-space projection is no first pass to build on: start over on the materialised column
-            d, jdd, _ = self._passes(u, basis, ls.k, ls.M_cont, ls.P.copy(), ls.rescale, r, ls.pending)
-            return d, jdd
         G0 = ls.G.to("cpu").numpy().reshape(ls.kp, ls.kp).copy()
         d, jdd, _ = self._passes(u, basis, ls.k, ls.M_cont, ls.P.copy(), ls.rescale, r, ls.pending, G0=G0,
                                  passes_before=1)

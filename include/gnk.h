@@ -33,7 +33,7 @@ extern "C" {
 #endif
 
 #define GNK_GHOST_ROWS 2
-#define GNK_ABI_VERSION 2
+#define GNK_ABI_VERSION 3
 
 typedef struct gnk_ctx gnk_ctx;
 
@@ -152,32 +152,6 @@ int gnk_lls_solve(gnk_ctx* ctx, const double* G, int kp, int k, const double* P,
 int gnk_lls_next(gnk_ctx* ctx, int k, int pending, const double* out, const double* e_try, const double* pack,
                  const double* sc, int kp_next, double* T_next, double* P_next, double* sdd_next, double* e_next,
                  double* hh_next, double* sc_next);
-
-/* ---- fused first trial + next Gram pass (res_old) ----
- * One pass over V[:, :k] (column k-1 the pending raw column of this step, k >= 2) doing this step's
- * first Armijo trial and the next step's Gram pass:
- *   w = V[k-1] - V[:, :k-1] @ hh (in place), x = V[:, :k] @ e_try, r_t = y - F(x) (owned rows),
- *   g = -(J(x)^T r_old) into V[k] (owned rows),
- *   pack_out = [sum r_t**2, sum w**2, max |w|, V[:, :k]^T g (k)]   (owned rows, this rank),
- *   G_out (kp x kp, kp = gnk_gram_padded_dim(k + 1, 1)) = Gram of [J(x) @ [V[:, :k] g] | r_t] @ T
- * with T the transform gnk_lls_fused_t builds (ldt == kp).  Ghost rows of w, g, r_t are not written
- * (multi-rank: the caller exchanges them).  k <= gnk_gram_fused_max_k(); N a multiple of 128.
- *             ref:krylow.py:41-42,62-73, armijo_goldstein.py:49-56, gauss_newton_krylow.py:16-36,86-89 */
-int gnk_gram_fused_max_k(void);
-int gnk_gram_fused(gnk_ctx* ctx, double* V, int64_t ldv, int k, const double* e_try, const double* hh,
-                   const double* r_old, const double* y, const double* T, int64_t ldt, double* x, double* r_t,
-                   double* G_out, double* pack_out);
-/* The fused pass's transform from this step's solve (out, k columns, the last one pending):
- * T_next = [[diag(a) R^-1, 0], [0, 1]] (+ r), a = [sc[:k-1], 1]: gnk_lls_next's T_next without the
- * pending column's projection.                                                 */
-int gnk_lls_fused_t(gnk_ctx* ctx, int k, const double* out, const double* sc, int kp_next, double* T_next);
-/* After gnk_gram_fused: gnk_lls_next's outputs (from the rank-summed pack) and G_next = the Gram
- * gnk_gram would give for gnk_lls_next's T_next, formed from G_fused in Gram space (the projection
- * of the new pending column).  Where that form has cancelled (||J w'||^2 < rho2_min ||J g||^2)
- * G_next[k][k] is NaN: gnk_lls_solve then reports status 1.                    */
-int gnk_lls_proj(gnk_ctx* ctx, int k, const double* out, const double* e_try, const double* pack, const double* sc,
-                 int kp_next, const double* G_fused, double rho2_min, double* G_next, double* P_next,
-                 double* sdd_next, double* e_next, double* hh_next, double* sc_next);
 
 /* g -= V[:, :k] @ h on owned rows; stats_out = {sum g**2, max|g|}
  *                                               ref:krylow.py:64,66,71 */

@@ -132,76 +132,6 @@ class NumpyBackend:
         sdd.numpy()[:k + 1] = np.append(s, 1.0)
         e.numpy()[:k + 1] = np.append(e_try.numpy()[:k], 0.0)
 
-    def lls_fused_t(self, k, out, sc, kp_next, T):
-        """NumPy double of gnk_lls_fused_t."""
-        o = out.numpy()
-        rinv = o[3 + k + 2 * k * k:3 + k + 3 * k * k].reshape(k, k)
-        a = sc.numpy()[:k].copy()
-        a[k - 1] = 1.0
-        t = np.zeros((kp_next, kp_next))
-        t[:k, :k] = a[:, None] * rinv
-        t[k, k] = t[k + 1, k + 1] = 1.0
-        T.numpy()[:kp_next * kp_next] = t.reshape(-1)
-
-    def lls_proj(self, k, out, e_try, pack, sc, kp_next, G_fused, rho2_min, G, P, sdd, e, hh, scn):
-        """NumPy double of gnk_lls_proj (k_lls_next's outputs + the Gram-space projection)."""
-        T = torch.zeros(kp_next * kp_next, dtype=torch.float64)
-        self.lls_next(k, True, out, e_try, pack, sc, kp_next, T, P, sdd, e, hh, scn)
-        o = out.numpy()
-        R = o[3 + k:3 + k + k * k].reshape(k, k)
-        a = sc.numpy()[:k].copy()
-        a[k - 1] = 1.0
-        beta = R @ (hh.numpy()[:k] / a)
-        gf = G_fused.numpy()[:kp_next * kp_next].reshape(kp_next, kp_next)
-        g = gf.copy()
-        q = gf[:, :k] @ beta
-        for i in list(range(k)) + [k + 1]:
-            g[i, k] = g[k, i] = gf[i, k] - q[i]
-        gkk = gf[k, k] - beta @ (2.0 * gf[:k, k] - q[:k])
-        g[k, k] = gkk if gkk >= rho2_min * gf[k, k] else np.nan
-        G.numpy()[:kp_next * kp_next] = g.reshape(-1)
-
-    def gram_fused_max_k(self):
-        return 13
-
-    def gram_fused(self, V, k, e_try, hh, r_old, y, T, x, r_t, G, pack):
-        """NumPy double of gnk_gram_fused (owned rows written; w, x and g evaluated on the slab rows the
-        kernel's ring covers)."""
-        N, nr = self.N, self.nrows
-        own = slice(GHOST * N, (GHOST + nr) * N)
-        Vn = V.numpy()
-        Vf = Vn[:k].copy()
-        Vf[k - 1] = Vn[k - 1] - hh.numpy()[:k - 1] @ Vn[:k - 1]
-        Vn[k - 1][own] = Vf[k - 1][own]
-        wo = Vf[k - 1][own]
-        xs = e_try.numpy()[:k] @ Vf
-        x.numpy()[own] = xs[own]
-        X = xs.reshape(nr + 2 * GHOST, N)
-        lo, hi = GHOST, GHOST + nr
-        Rt = self._m(y)[lo:hi] - self._fwd(X, lo, hi)
-        self._m(r_t)[lo:hi] = Rt
-        # g on the owned rows and the first ghost row each side (zero outside the domain)
-        glo = GHOST - 1 if self.row0 > 0 else GHOST
-        ghi = GHOST + nr + 1 if self.row0 + nr < N else GHOST + nr
-        gf = np.zeros((nr + 2 * GHOST, N))
-        gf[glo:ghi] = -self._vjp_block(self._diag(X[glo:ghi]), *self._nb(self._m(r_old), glo, ghi))
-        Vn[k].reshape(nr + 2 * GHOST, N)[lo:hi] = gf[lo:hi]
-        h = Vf[:, own] @ gf.reshape(-1)[own]
-        D = self._diag(X[lo:hi])
-        cols = [self._jvp_block(D, *self._nb(Vf[j].reshape(nr + 2 * GHOST, N), lo, hi)).reshape(-1) for j in range(k)]
-        cols.append(self._jvp_block(D, *self._nb(gf, lo, hi)).reshape(-1))
-        cols.append(Rt.reshape(-1))
-        kp = self.gram_dim(k + 1, True)
-        W = np.zeros((len(cols[0]), kp))
-        W[:, :len(cols)] = np.stack(cols, axis=1)
-        W = W @ T.numpy()[:kp * kp].reshape(kp, kp)
-        G.numpy()[:kp * kp] = (W.T @ W).reshape(-1)
-        p = pack.numpy()
-        p[0] = float(np.sum(Rt * Rt))
-        p[1] = float(np.sum(wo * wo))
-        p[2] = float(np.max(np.abs(wo))) if not np.isnan(wo).any() else float("nan")
-        p[3:3 + k] = h
-
     def gram_dim(self, k, with_r):
         return ((k + (1 if with_r else 0) + 15) // 16) * 16
 

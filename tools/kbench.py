@@ -50,15 +50,12 @@ def main():
     d = dev.vec()
     be.jdiag(u, d)
     q = dev.vec()
-    # fused first trial + next Gram (k V columns, the last pending; Gram of k + 1 columns) and the
-    # unfused pieces it replaces: gram2n (Gram of k + 1 columns), trialp (pending first trial), resid
+    # gram2n (Gram of k + 1 columns), trialp (pending first trial over k columns, the last pending)
     kpn = be.gram_dim(k + 1, True)
     tf = np.zeros((kpn, kpn)); tf[:k + 2, :k + 2] = np.triu(np.ones((k + 2, k + 2))) * 0.1 + np.eye(k + 2)
     tf_d = be.to_device(tf.reshape(-1))
     Gn = be.zeros(kpn * kpn)
     hh = be.to_device(0.01 * np.random.default_rng(1).standard_normal(k))
-    pack = be.zeros(3 + k)
-    t2 = dev.vec()
     ops = {
         "gram1": (lambda: be.gram(u, V, k, None, None, G), 8.0 * n * (k + 1)),
         "gram2": (lambda: be.gram(u, V, k, rinv_d, r, G), 8.0 * n * (k + 2)),
@@ -69,7 +66,6 @@ def main():
         "cgs": (lambda: be.cgs_update(V, k, h, V[k], st), 8.0 * n * (k + 2)),
         "resid": (lambda: be.residual(x, y, t1, st), 24.0 * n),
         "cg": (lambda: be.cg_matvec(d, r, q, st), 24.0 * n),
-        "fused": (lambda: be.gram_fused(V, k, c, hh, r, y, tf_d, x, t2, Gn, pack), 8.0 * n * (k + 6)),
         "gram2n": (lambda: be.gram(u, V, k + 1, tf_d, r, Gn), 8.0 * n * (k + 3)),
         "trialp": (lambda: be.gemv_vjp_gemv_t_pending(V, k - 1, c, hh, r, x, V[k], h, st), 8.0 * n * (k + 5)),
     }
