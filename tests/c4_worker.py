@@ -10,11 +10,12 @@ frees its state and rank 0 runs the same solve on one rank over the whole grid. 
   * every rank took identical decisions and holds identical per-iteration scalars;
   * 8 ranks vs 1 rank: nit / nrev / njev / success, per-iteration nfev, basis sizes, stdout identical,
     per-iteration ||r_k|| within north_star's 1e-10 (relative), ||x_k|| within max(1e-10, CANCEL u ||x_0|| /
-    ||x_k||): on this workload the first steps take the iterate from ||x_0|| ~ 3e3 to ||x_k|| ~ 1e-9 .. 1e-5
+    ||x_k||, cycle_spread_k): on this workload the first steps take the iterate from ||x_0|| ~ 3e3 to ||x_k|| ~ 1e-9 .. 1e-5
     (the cancellation of c + d along x_0, ref:gauss_newton_krylow.py:98), so two correctly rounded
     evaluations of the same step already differ by O(u ||x_0||) in x_k -- the floor of any relative
     comparison of ||x_k||, whatever the summation order (at 8192^2 the reference's own reorderings move
-    ||x_1|| by 2e-7: tests/golden/sensitivity.json, head8192).
+    ||x_1|| by 2e-7: tests/golden/sensitivity.json, head8192); the later iterates inherit that absolute
+    difference, so beyond iteration 1 the bound is the pinned 8192^2 cycle's own spread (cycle_spread).
 Memory: ITERS = 6 iterations hold at most 7 basis columns (+ ~9 vectors) x 8.6 GB ~ 140 GB, on 8
 ranks or on one.  (A restart inside the window would make the next step a k = 1 step whose Armijo
 test compares two sums of 1e9 squares differing by less than their rounding: the reference's own
@@ -44,6 +45,17 @@ from tests.transport_shim import StagedTransportComm  # noqa: E402
 TOL = 1e-10
 CANCEL = 16          # roundings of size u ||x_0|| allowed in x_k
 U = np.finfo(np.float64).eps / 2
+
+
+def cycle_spread(n):
+    """2 |exact_k1_i - base_i| / |base_i| of the pinned 8192^2 restart-cycle fixture (tests/golden/
+    make_cycle8192.py, the same workload family and restart): how far the reference's own trajectory
+    moves when only its cancellation-limited k = 1 dot products are rounded differently.  At 32768^2 that
+    cancellation is ~19x deeper (||x_1|| / ||x_0|| = 1.7e-9 vs 3.2e-8), so as a bound here it is conservative."""
+    with open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "large_cycle8192.json")) as f:
+        v = json.load(f)["variants"]
+    b, e = np.array(v["base"]["xnorm"][:n]), np.array(v["exact_k1"]["xnorm"][:n])
+    return 2 * np.abs(e - b) / np.abs(b)
 
 
 def log(msg):
@@ -125,8 +137,8 @@ def main():
         return np.abs(a_ - b_) / np.abs(b_) if len(a_) == len(b_) and len(b_) else np.array([np.inf])
 
     ex, er = rel(mine["xnorm2"], one["xnorm2"]), rel(mine["rsumsq"], one["rsumsq"])
-    xb = np.maximum(TOL, CANCEL * U * one.get("x0norm", 0.0) / np.sqrt(np.array(one["xnorm2"]))) \
-        if len(ex) == len(one["xnorm2"]) else np.array([0.0])
+    xb = np.maximum(np.maximum(TOL, CANCEL * U * one.get("x0norm", 0.0) / np.sqrt(np.array(one["xnorm2"]))),
+                    cycle_spread(len(one["xnorm2"]))) if len(ex) == len(one["xnorm2"]) else np.array([0.0])
     rx, rr = float(np.max(ex)), float(np.max(er))
     ok = bool(ranks_identical and same and np.all(ex <= xb) and rr <= TOL)
     rep = {"ok": ok, "grid": a.grid, "world": world, "restart": a.restart, "iters": a.iters,

@@ -4,7 +4,9 @@
   through slab.Comm's RCCL code paths with a host-staged transport (tests/c4_worker.py,
   tests/transport_shim.py); krylow_restart 20, the first 6 outer iterations; 8 ranks vs 1 rank on the same
   inputs: identical decisions and bookkeeping on every rank and vs one rank, ||r_k|| within 1e-10,
-  ||x_k|| within its cancellation floor (tests/c4_worker.py: x_k ~ 1e-9 .. 1e-5 of ||x_0||).  (The reference itself cannot run at this size; the oracle pins the algorithm at
+  ||x_k|| within its cancellation floor (tests/c4_worker.py: x_k ~ 1e-9 .. 1e-5 of ||x_0||) or the pinned
+  8192^2 restart cycle's own spread under a re-rounded k = 1 step, whichever is larger.  (The reference
+  itself cannot run at this size; the oracle pins the algorithm at
   smaller sizes: tests/test_gpu_multislab.py, tests/test_gpu_baseline_sizes.py.)
 * C5 (configs[4]): Bratu 16384^2 with the basis growing without restart (krylow_restart 100,
   ref:gauss_newton_krylow.py:81-82, ref:krylow.py:72-73) to k = 71 -- through every Gram kernel of
