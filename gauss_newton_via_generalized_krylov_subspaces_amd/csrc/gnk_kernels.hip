@@ -1310,6 +1310,247 @@ constexpr int pair_b(int p, int nb) {
   return a + p;
 }
 
+__device__ __forceinline__ double dpp_row_shr1(double v) {     // lane l <- lane l-1 of its 16-lane row
+  const u2v b = __builtin_bit_cast(u2v, v);
+  u2v o;
+  o.x = unsigned(__builtin_amdgcn_mov_dpp(int(b.x), 0x111, 0xf, 0xf, true));   // bound_ctrl: row edge -> 0
+  o.y = unsigned(__builtin_amdgcn_mov_dpp(int(b.y), 0x111, 0xf, 0xf, true));   // bound_ctrl: row edge -> 0
+  return __builtin_bit_cast(double, o);
+}
+__device__ __forceinline__ double dpp_row_shl1(double v) {     // lane l <- lane l+1 of its 16-lane row
+  const u2v b = __builtin_bit_cast(u2v, v);
+  u2v o;
+  o.x = unsigned(__builtin_amdgcn_mov_dpp(int(b.x), 0x101, 0xf, 0xf, true));   // bound_ctrl: row edge -> 0
+  o.y = unsigned(__builtin_amdgcn_mov_dpp(int(b.y), 0x101, 0xf, 0xf, true));   // bound_ctrl: row edge -> 0
+  return __builtin_bit_cast(double, o);
+}
+
+// Wide Gram pass for 5..7 column blocks (KP = 80..112: k = 64..111 on the GNK path), round 3.
+// k_gram above stages RinvAug (up to 100 KB) in LDS beside its tile, which leaves one 4-wave workgroup
+// per CU: one wave per SIMD runs fill, transform and Gram back to back, so the fp64 pipe idles while a
+// tile loads.  Here one 8-wave workgroup per CU walks a 32-point strip down a row range:
+//  * fill: thread -> (point pair, column phase); every thread marches its columns down the strip with
+//    the centre and south rows in registers (one new 16-B row load per column and step, issued before
+//    the step's MFMAs; the north row is the previous centre), the in-row neighbours by DPP row shifts,
+//    the strip's outer neighbours by its two edge lanes -- each value leaves HBM once;
+//  * transform Y = W P^-1 split over wave pairs by OUTPUT column block (block cb costs cb + 1 k-steps;
+//    a greedy split gives each pair <= 2 blocks and equal cost at 7 blocks), the two waves of a pair
+//    taking the tile's two 16-row groups; RinvAug's B fragments live in VGPRs for the whole launch and
+//    Y goes to a second tile (no in-place hazard);
+//  * Gram: each wave pair owns ceil(P / 4) pair tiles, its two waves the two row halves (summed in a
+//    fixed order at the end);
+//  * jdiag(u) once per point: wave 0 computes the next row's into LDS one step ahead.
+// Strips are XCD-major (consecutive workgroups of one XCD take adjacent strips).
+constexpr int GX_T = 32;      // points per tile (the strip width)
+constexpr int GX_NW = 8;      // waves per workgroup
+constexpr int gx_owner(int nb, int cb) {      // wave pair owning transform block cb (greedy by cost cb + 1)
+  int load[4] = {0, 0, 0, 0};
+  int own = -1;
+  for (int c = nb - 1; c >= 0; --c) {
+    int w = 0;
+    for (int i = 1; i < 4; ++i)
+      if (load[i] < load[w]) w = i;
+    load[w] += c + 1;
+    if (c == cb) own = w;
+  }
+  return own;
+}
+constexpr int gx_cb(int nb, int w, int slot) {    // slot-th (0, 1) transform block of wave pair w
+  int n = 0;
+  for (int cb = nb - 1; cb >= 0; --cb)
+    if (gx_owner(nb, cb) == w) {
+      if (n == slot) return cb;
+      ++n;
+    }
+  return -1;
+}
+
+template <int NB, int WP>
+__device__ __forceinline__ void gram_x_wave(const double* __restrict__ u, const double* __restrict__ V, int64_t ldv,
+                                            int k, const double* __restrict__ rinv, const double* __restrict__ r,
+                                            const Geo& geo, const Coef& c, int64_t rpr, int64_t nitems,
+                                            double* __restrict__ lds, double* __restrict__ partial) {
+  constexpr int TT = GX_T, KP = 16 * NB, S = KP + 1;
+  constexpr int P = NB * (NB + 1) / 2, PPW = (P + 3) / 4;
+  constexpr int CA = gx_cb(NB, WP, 0), CBB = gx_cb(NB, WP, 1);
+  static_assert(gx_cb(NB, WP, 2) == -1, "at most two transform blocks per wave pair");
+  constexpr int NBB = CBB >= 0 ? CBB + 1 : 1;
+  constexpr int NTH = 64 * GX_NW;
+  constexpr int TPR = NTH / (TT / 2);       // 32 threads (column phases) per point pair
+  constexpr int MJ = (KP + TPR - 1) / TPR;  // columns per thread
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int half = (tid >> 6) & 1;          // this wave's row group (transform) / row half (Gram)
+  double* Wt = lds;                         // raw J V (| r) tile, [TT][S]
+  double* Yt = lds + TT * S;                // transformed tile (pass 2); pass 1 reads Wt
+  double* ddb = lds + 2 * TT * S;           // [2][TT]: jdiag of this step's / the next step's row
+  const int64_t N = geo.N;
+  const int64_t nstrips = N / TT;
+  const int nwg = gridDim.x, b = blockIdx.x;
+  const int idx = (nwg % 8 == 0) ? (b % 8) * (nwg / 8) + b / 8 : b;
+
+  // this wave pair's RinvAug B fragments (k-steps of blocks ab <= cb), loaded once
+  double rA[CA + 1][4], rB2[NBB][4];
+  if (rinv) {
+#pragma unroll
+    for (int ab = 0; ab <= CA; ++ab)
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) rA[ab][ks] = rinv[(ab * 16 + ks * 4 + (lane >> 4)) * KP + CA * 16 + (lane & 15)];
+    if (CBB >= 0) {
+#pragma unroll
+      for (int ab = 0; ab < NBB; ++ab)
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks)
+          rB2[ab][ks] = rinv[(ab * 16 + ks * 4 + (lane >> 4)) * KP + CBB * 16 + (lane & 15)];
+    }
+  }
+  d4 acc[PPW];
+#pragma unroll
+  for (int q = 0; q < PPW; ++q) acc[q] = d4{0.0, 0.0, 0.0, 0.0};
+
+  const int pp = tid & (TT / 2 - 1), jh = tid >> 4;
+  const bool ew = pp == 0, ee = pp == TT / 2 - 1;
+  const double* src = rinv ? Yt : Wt;       // what the Gram reads
+  const bool rthr = r && (k % TPR) == jh;   // the threads that stage r (column k)
+
+  for (int64_t item = idx; item < nitems; item += nwg) {   // (row range, strip)
+    const int64_t x0 = (item / nstrips) * rpr;
+    const int64_t x1 = min(geo.nrows, x0 + rpr);
+    const int64_t cs = (item % nstrips) * TT;
+    const int64_t iy = cs + 2 * pp;
+    const bool hw = iy > 0, he = iy + 2 < N;
+    if (x0 >= x1) continue;
+    auto colp = [&](int m, int64_t xr) {
+      return V + int64_t(min(jh + TPR * m, k - 1)) * ldv + (G + xr) * N + iy;
+    };
+    d2 vn[MJ], vc[MJ], vs[MJ];
+    double eo[MJ];                          // edge lanes: the strip's outer neighbour in the centre row
+#pragma unroll
+    for (int m = 0; m < MJ; ++m) {
+      const double* q = colp(m, x0);
+      vn[m] = *reinterpret_cast<const d2*>(q - N);
+      vc[m] = *reinterpret_cast<const d2*>(q);
+      vs[m] = *reinterpret_cast<const d2*>(q + N);
+      eo[m] = ew ? q[hw ? -1 : 0] : (ee ? q[he ? 2 : 1] : 0.0);
+    }
+    d2 rc = {0.0, 0.0};
+    if (rthr) rc = *reinterpret_cast<const d2*>(r + (G + x0) * N + iy);
+    double un = 0.0;                        // threads < TT: u of the next row
+    if (tid < TT) {
+      ddb[tid] = jdiag(c, u[(G + x0) * N + cs + tid]);
+      un = u[(G + x0 + 1) * N + cs + tid];
+    }
+    __syncthreads();
+
+    for (int64_t x = x0; x < x1; ++x) {
+      const int bsel = int((x - x0) & 1);
+      const double dd0 = ddb[bsel * TT + 2 * pp], dd1 = ddb[bsel * TT + 2 * pp + 1];
+#pragma unroll
+      for (int m = 0; m < MJ; ++m) {
+        const double wl = dpp_row_shr1(vc[m].y);   // lane pp-1's second point
+        const double er = dpp_row_shl1(vc[m].x);   // lane pp+1's first point
+        const double w = ew ? eo[m] : wl, e = ee ? eo[m] : er;
+        const double w0 = jvp_pt(c, dd0, vn[m].x, hw ? w : 0.0, hw, vc[m].x, vc[m].y, true, vs[m].x);
+        const double w1 = jvp_pt(c, dd1, vn[m].y, vc[m].x, true, vc[m].y, he ? e : 0.0, he, vs[m].y);
+        if (jh + TPR * m < k) {
+          Wt[(2 * pp) * S + jh + TPR * m] = w0;
+          Wt[(2 * pp + 1) * S + jh + TPR * m] = w1;
+        }
+      }
+      if (rthr) {
+        Wt[(2 * pp) * S + k] = rc.x;
+        Wt[(2 * pp + 1) * S + k] = rc.y;
+      }
+      if (x + 1 < x1) {                      // march: the next step's rows land under this step's MFMAs
+#pragma unroll
+        for (int m = 0; m < MJ; ++m) {
+          vn[m] = vc[m];
+          vc[m] = vs[m];
+          const double* q = colp(m, x + 1);
+          vs[m] = *reinterpret_cast<const d2*>(q + N);
+          eo[m] = ew ? q[hw ? -1 : 0] : (ee ? q[he ? 2 : 1] : 0.0);
+        }
+        if (rthr) rc = *reinterpret_cast<const d2*>(r + (G + x + 1) * N + iy);
+        if (tid < TT) {
+          ddb[(bsel ^ 1) * TT + tid] = jdiag(c, un);
+          un = u[(G + x + 2) * N + cs + tid];
+        }
+      }
+      __syncthreads();
+      if (rinv) {
+        // Y[rows of group `half`, cb block] = W[., :16(cb+1)] RinvAug[:16(cb+1), cb block]
+        const double* arow = Wt + (half * 16 + (lane & 15)) * S + (lane >> 4);
+        d4 qa = d4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int ab = 0; ab <= CA; ++ab)
+#pragma unroll
+          for (int ks = 0; ks < 4; ++ks) qa = mfma64(arow[ab * 16 + ks * 4], rA[ab][ks], qa);
+#pragma unroll
+        for (int ii = 0; ii < 4; ++ii) Yt[(half * 16 + (lane >> 4) + 4 * ii) * S + CA * 16 + (lane & 15)] = qa[ii];
+        if (CBB >= 0) {
+          d4 qb = d4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+          for (int ab = 0; ab < NBB; ++ab)
+#pragma unroll
+            for (int ks = 0; ks < 4; ++ks) qb = mfma64(arow[ab * 16 + ks * 4], rB2[ab][ks], qb);
+#pragma unroll
+          for (int ii = 0; ii < 4; ++ii) Yt[(half * 16 + (lane >> 4) + 4 * ii) * S + CBB * 16 + (lane & 15)] = qb[ii];
+        }
+        __syncthreads();
+      }
+#pragma unroll
+      for (int rr = 0; rr < TT / 2; rr += 4) {
+        const double* row = src + (half * (TT / 2) + rr + (lane >> 4)) * S + (lane & 15);
+#pragma unroll
+        for (int q = 0; q < PPW; ++q) {
+          const int p = WP * PPW + q;
+          if (p < P) acc[q] = mfma64(row[pair_a(p, NB) * 16], row[pair_b(p, NB) * 16], acc[q]);
+        }
+      }
+      if (!rinv) __syncthreads();          // the next fill overwrites the tile this Gram read
+    }
+  }
+  // the pair's two row halves summed in a fixed order (half 0 + half 1) through LDS, then
+  // partial[(block * 4 PPW + pair) * 256 + lane * 4 + i] (k_gram_reduce, one pair group)
+  __syncthreads();
+  double* red = lds + WP * PPW * 256;
+  if (half == 1) {
+#pragma unroll
+    for (int q = 0; q < PPW; ++q)
+#pragma unroll
+      for (int ii = 0; ii < 4; ++ii) red[q * 256 + lane * 4 + ii] = acc[q][ii];
+  }
+  __syncthreads();
+  if (half == 0) {
+#pragma unroll
+    for (int q = 0; q < PPW; ++q) {
+      const int p = WP * PPW + q;
+      if (p < P) {
+#pragma unroll
+        for (int ii = 0; ii < 4; ++ii)
+          partial[(size_t(blockIdx.x) * 4 * PPW + p) * 256 + lane * 4 + ii] = acc[q][ii] + red[q * 256 + lane * 4 + ii];
+      }
+    }
+  }
+}
+
+template <int NB>
+__global__ __launch_bounds__(64 * GX_NW) void k_gram_x(const double* __restrict__ u, const double* __restrict__ V,
+                                                       int64_t ldv, int k, const double* __restrict__ rinv,
+                                                       const double* __restrict__ r, Geo geo, Coef c, int64_t rpr,
+                                                       int64_t nitems, double* __restrict__ partial) {
+  extern __shared__ __attribute__((aligned(16))) double lds[];
+  // padding columns [k(+1), KP) of both tiles stay zero (RinvAug is zero outside its leading block)
+  for (int idx = threadIdx.x; idx < 2 * GX_T * (16 * NB + 1); idx += 64 * GX_NW) lds[idx] = 0.0;
+  __syncthreads();
+  // one code path per wave pair: each knows its transform blocks and pair tiles at compile time
+  switch (__builtin_amdgcn_readfirstlane(threadIdx.x >> 7)) {
+    case 0: gram_x_wave<NB, 0>(u, V, ldv, k, rinv, r, geo, c, rpr, nitems, lds, partial); break;
+    case 1: gram_x_wave<NB, 1>(u, V, ldv, k, rinv, r, geo, c, rpr, nitems, lds, partial); break;
+    case 2: gram_x_wave<NB, 2>(u, V, ldv, k, rinv, r, geo, c, rpr, nitems, lds, partial); break;
+    default: gram_x_wave<NB, 3>(u, V, ldv, k, rinv, r, geo, c, rpr, nitems, lds, partial); break;
+  }
+}
+
 template <int NB, int BC, int CHT>
 __global__ __launch_bounds__(BLOCK) void k_gram_w(const double* __restrict__ u, const double* __restrict__ V,
                                                   int64_t ldv, int k, const double* __restrict__ rinv,
@@ -1470,20 +1711,6 @@ __global__ __launch_bounds__(BLOCK) void k_gram_w(const double* __restrict__ u, 
 // stencil of chunk c and its MFMAs.  k_gram_w waits for each column group's loads in turn (SQ
 // counters at k = 51: waves waiting 51 % of the time, MFMA busy 27 %).  Same FMA order as
 // k_gram_w, so the two kernels give bit-identical Grams.
-__device__ __forceinline__ double dpp_row_shr1(double v) {     // lane l <- lane l-1 of its 16-lane row
-  const u2v b = __builtin_bit_cast(u2v, v);
-  u2v o;
-  o.x = unsigned(__builtin_amdgcn_mov_dpp(int(b.x), 0x111, 0xf, 0xf, true));   // bound_ctrl: row edge -> 0
-  o.y = unsigned(__builtin_amdgcn_mov_dpp(int(b.y), 0x111, 0xf, 0xf, true));   // bound_ctrl: row edge -> 0
-  return __builtin_bit_cast(double, o);
-}
-__device__ __forceinline__ double dpp_row_shl1(double v) {     // lane l <- lane l+1 of its 16-lane row
-  const u2v b = __builtin_bit_cast(u2v, v);
-  u2v o;
-  o.x = unsigned(__builtin_amdgcn_mov_dpp(int(b.x), 0x101, 0xf, 0xf, true));   // bound_ctrl: row edge -> 0
-  o.y = unsigned(__builtin_amdgcn_mov_dpp(int(b.y), 0x101, 0xf, 0xf, true));   // bound_ctrl: row edge -> 0
-  return __builtin_bit_cast(double, o);
-}
 
 template <int NB, int CHT>
 __global__ __launch_bounds__(BLOCK) void k_gram_wp(
@@ -3569,6 +3796,41 @@ int gnk_gram(gnk_ctx* ctx, const double* u, const double* V, int64_t ldv, int k,
     hipLaunchKernelGGL(k_gram_scatter, dim3((P * 256 + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, ctx->stream, red, P, KP,
                        G_out);
     return check_launch(ctx, "gram scatter");
+  }
+  // 5..7 column blocks on a grid of 32-point strips: k_gram_x (RinvAug in VGPRs, two workgroups per CU);
+  // tuning GNK_TUNE_GRAM_WIDE 3 keeps the pair-split k_gram below (tooling A/B)
+  if (nb >= 5 && nb <= 7 && ctx->geo.N % GX_T == 0 && ldv % 2 == 0 && tuning(ctx, GNK_TUNE_GRAM_WIDE) != 3) {
+    // one 8-wave workgroup per CU (the registers of the marching fill, the wave pair's B fragments and
+    // its pair tiles: ~2 waves per SIMD)
+    const size_t ldsx = size_t(2) * GX_T * (KP + 1) * 8 + size_t(2) * GX_T * 8;    // W, Y tiles + jdiag rows
+    if (size_t(4 * ((P + 3) / 4)) * 256 * 8 > ldsx) return fail(ctx, "gram: reduction staging does not fit (x)");
+    const int64_t nstrips = ctx->geo.N / GX_T;
+    const int64_t nrows = ctx->geo.nrows;
+    // a persistent grid of the resident workgroups over (row range, strip) items; items = lcm(strips,
+    // workgroups) when the rows allow, so every workgroup gets the same number
+    const int64_t nwg = int64_t(ctx->num_cus);
+    int64_t gcd = nstrips, bb = nwg;
+    while (bb) { const int64_t t2 = gcd % bb; gcd = bb; bb = t2; }
+    int64_t nranges = std::max<int64_t>(1, std::min<int64_t>(nrows, nwg / gcd));
+    const int64_t rpr = (nrows + nranges - 1) / nranges;
+    nranges = (nrows + rpr - 1) / rpr;
+    const int64_t nitems = nstrips * nranges;
+    const int PGx = 4 * ((P + 3) / 4);
+    if (nwg > (1 << 20) || size_t(nwg) * PGx * 256 > SCRATCH_DOUBLES) return fail(ctx, "gram: scratch too small (x)");
+    const int64_t nown = nrows * ctx->geo.N;
+    TimedLaunch tlx(ctx, GNK_TIMER_GRAM, 8.0 * double(nown) * double(k + 1 + (r ? 1 : 0)));
+#define GRAMX(NBV)                                                                                                \
+  hipLaunchKernelGGL(k_gram_x<NBV>, dim3(unsigned(nwg)), dim3(64 * GX_NW), ldsx, ctx->stream, u, V, ldv, k, rinv, r, \
+                     ctx->geo, ctx->coef, rpr, nitems, ctx->scratch)
+    if (nb == 5) GRAMX(5); else if (nb == 6) GRAMX(6); else GRAMX(7);
+#undef GRAMX
+    tlx.done();
+    int rcx = check_launch(ctx, "gram_x");
+    if (rcx) return rcx;
+    (void)hipMemsetAsync(G_out, 0, size_t(KP) * KP * sizeof(double), ctx->stream);
+    hipLaunchKernelGGL(k_gram_reduce, dim3((P * 256 + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, ctx->stream, ctx->scratch,
+                       int(nwg), P, PGx, KP, G_out);
+    return check_launch(ctx, "gram reduce (x)");
   }
   const int rowsplit = P <= PPW_MAX ? 1 : 0;
   // pair-split: the P pair tiles spread evenly over the 4 waves (PPW = ceil(P / 4), instantiated up

@@ -57,7 +57,8 @@ int gnk_set_reduce_pairs(gnk_ctx* ctx, int on);
  *   GNK_TUNE_GRAM_V1MIN  first k of the one-point VALU Gram kernel (-1: never)
  *   GNK_TUNE_CG_MATVEC   1 = the point-wise normal matvec instead of the row-marching one
  *   GNK_TUNE_VJPG_BLOCKS cap on the blocks of gnk_vjp_gemv_t
- *   GNK_TUNE_GRAM_WIDE   1 = never the prefetching wide Gram kernel, 2 = also for 2..3 column blocks */
+ *   GNK_TUNE_GRAM_WIDE   1 = never the prefetching wide Gram kernel, 2 = also for 2..3 column blocks,
+ *                        3 = the pair-split kernel instead of the VGPR-RinvAug one for 5..7 blocks */
 #define GNK_TUNE_GRAM_PATH 0
 #define GNK_TUNE_GRAM_RING 1
 #define GNK_TUNE_GRAM_V1MIN 2

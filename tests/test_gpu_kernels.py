@@ -260,7 +260,10 @@ def test_cgs_max_propagates_nan():
                                                   (64, 51, True, True), (64, 40, False, True), (96, 22, True, True),
                                                   (130, 33, True, True), (48, 60, True, True), (24, 30, True, False),
                                                   # NB = 4: flattened order (N % 32 != 0) / down-strip walks crossing strips
-                                                  (100, 55, True, True), (96, 50, True, False), (416, 49, True, True)])
+                                                  (100, 55, True, True), (96, 50, True, False), (416, 49, True, True),
+                                                  # NB = 5..7: k_gram_x (N % 32 == 0; 1..5 strips) / k_gram (N = 100)
+                                                  (128, 70, True, True), (96, 90, True, True), (64, 100, True, True),
+                                                  (160, 81, False, True), (32, 64, True, True), (100, 75, True, True)])
 @pytest.mark.parametrize("staged", ["default", "forced", "ring5"])
 def test_gram_mfma(N, k, with_r, with_rinv, staged):
     """W = [J V | r] @ RinvAug on fp64 MFMA vs an fp64 NumPy Gram (host BLAS).  "forced" runs

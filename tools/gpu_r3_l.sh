@@ -1,0 +1,31 @@
+#!/bin/bash
+# Round 3, GPU session L: wide Gram k_gram_x (5..7 column blocks, RinvAug in VGPRs, two workgroups per
+# CU) -- kernel parity, then A/B vs the pair-split k_gram at 8192^2, k = 64..100.
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+O=gpurun_out/r3l
+mkdir -p $O
+export TMPDIR=/tmp
+step() {
+  local name=$1; shift
+  echo "== $name $(date +%T)"
+  "$@"; local rc=$?
+  echo "== $name rc=$rc $(date +%T)"
+  if [ $rc -ge 124 ]; then echo "FATAL at $name"; exit $rc; fi
+  return 0
+}
+step kernels timeout -k 10 400 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_kernels.py -k "gram" > $O/kernels.log 2>&1
+grep -q " passed" $O/kernels.log && ! grep -q "failed" $O/kernels.log || { echo "kernel tests failed"; exit 1; }
+for k in 64 70 80 90 100; do
+  for w in 0 3; do
+    step "wide_${w}_$k" timeout -k 10 150 python -u tools/kbench.py --k $k --reps 5 --kernels gram2 --tune gram_wide=$w > $O/w_${w}_$k.json
+  done
+done
+echo done
+# VALU Gram at k = 8, 9: two points per lane (k_gram_v, default for 8) vs one (k_gram_v1, default for 9)
+for v in 0 8 10; do
+  for k in 8 9; do
+    step "v1min_${v}_$k" timeout -k 10 120 python -u tools/kbench.py --k $k --reps 7 --kernels gram2 --tune gram_v1min=$v > $O/v1_${v}_$k.json
+  done
+done
+echo done2

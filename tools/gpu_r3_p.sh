@@ -1,0 +1,11 @@
+#!/bin/bash
+# Round 3, GPU session P: PMC passes (tools/pmc.sh) over the marching k_gram_x at 8192^2 (k = 64, 80, 100).
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+O=gpurun_out/r3p
+mkdir -p $O
+for k in 64 80 100; do
+  echo "== pmc k=$k $(date +%T)"
+  bash tools/pmc.sh $O/k$k --k $k --reps 3 --kernels gram2 || { echo "pmc k=$k failed rc=$?"; exit 1; }
+done
+echo done
