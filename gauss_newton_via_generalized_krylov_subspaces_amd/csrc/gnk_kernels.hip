@@ -1388,8 +1388,9 @@ __device__ __forceinline__ void gram_x_wave(const double* __restrict__ u, const 
   const int nwg = gridDim.x, b = blockIdx.x;
   const int idx = (nwg % 8 == 0) ? (b % 8) * (nwg / 8) + b / 8 : b;
 
-  // this wave pair's RinvAug B fragments (k-steps of blocks ab <= cb), loaded once
-  double rA[CA + 1][4], rB2[NBB][4];
+  // this wave pair's RinvAug B fragments (k-steps of blocks ab <= cb), loaded once (none: CA = -1, a
+  // pair without transform work at 2..3 column blocks)
+  double rA[CA >= 0 ? CA + 1 : 1][4], rB2[NBB][4];
   if (rinv) {
 #pragma unroll
     for (int ab = 0; ab <= CA; ++ab)
@@ -1479,13 +1480,15 @@ __device__ __forceinline__ void gram_x_wave(const double* __restrict__ u, const 
       if (rinv) {
         // Y[rows of group `half`, cb block] = W[., :16(cb+1)] RinvAug[:16(cb+1), cb block]
         const double* arow = Wt + (half * 16 + (lane & 15)) * S + (lane >> 4);
-        d4 qa = d4{0.0, 0.0, 0.0, 0.0};
+        if constexpr (CA >= 0) {
+          d4 qa = d4{0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-        for (int ab = 0; ab <= CA; ++ab)
+          for (int ab = 0; ab <= CA; ++ab)
 #pragma unroll
-          for (int ks = 0; ks < 4; ++ks) qa = mfma64(arow[ab * 16 + ks * 4], rA[ab][ks], qa);
+            for (int ks = 0; ks < 4; ++ks) qa = mfma64(arow[ab * 16 + ks * 4], rA[ab][ks], qa);
 #pragma unroll
-        for (int ii = 0; ii < 4; ++ii) Yt[(half * 16 + (lane >> 4) + 4 * ii) * S + CA * 16 + (lane & 15)] = qa[ii];
+          for (int ii = 0; ii < 4; ++ii) Yt[(half * 16 + (lane >> 4) + 4 * ii) * S + CA * 16 + (lane & 15)] = qa[ii];
+        }
         if (CBB >= 0) {
           d4 qb = d4{0.0, 0.0, 0.0, 0.0};
 #pragma unroll
@@ -2310,10 +2313,12 @@ __global__ __launch_bounds__(64 * GS_NW) __attribute__((amdgpu_waves_per_eu(WPE)
         if (EB) {
           if (st == 0) {
             dn = __shfl(dnb, 48 + (lane & 15));       // dn(x+1): group 3 of the previous batch
-            // the new batch: group g = dn(x+2+g); u(x+2+g) sits in the slot of row x-1+g (slot g), read
-            // before this step's DMA refills slot 0
+            // the new batch: group g = dn(x+2+g); u(x+2+g) sits in the slot of row x-1+g (slot g).  Every
+            // wave reads it before any wave's DMA below refills slot 0 (one more barrier per 4 rows: the
+            // u row is DMA'd by one wave, read by all)
             double ug = lds[cq * SS + ou];
             asm volatile("" : "+v"(ug));
+            __builtin_amdgcn_s_barrier();
             dnb = -jdiag(cf, ug);
           } else {
             dn = __shfl(dnb, (st - 1) * 16 + (lane & 15));
@@ -2393,8 +2398,8 @@ __device__ __forceinline__ void gram_v_point(const double (&a)[K], double rv, co
 
 constexpr int GV_KMAX = 9;      // VALU Gram pass for k <= GV_KMAX (with r); k = 10 measured slower
                                 // than the staged kernel (2.20 vs 2.08 ms, 256 VGPRs)
-constexpr int GV1_KMIN = 9;     // one point per lane from here (register budget; k = 7, 8 measured
-                                // faster with two points per lane, 16-byte loads)
+constexpr int GV1_KMIN = 8;     // one point per lane from here (register budget: the two-point k = 8
+                                // instance needs 256 VGPRs, one wave per SIMD; 1.40 vs 1.45 ms at 8192^2)
 constexpr int GV_SW = 128;           // strip width: 64 lanes x 2 points
 
 template <int K>
@@ -3064,13 +3069,13 @@ RowLaunch rows(const gnk_ctx* ctx, int64_t lr0, int64_t nlr, int vec, int cap_bl
 // Workgroups (of `block` threads) of `fn` resident on the whole device at once: a persistent
 // grid-stride launch sized to a multiple of it has no partly filled last round (at 8192^2 the trial
 // kernel's former fixed 2048 workgroups were 1.6 rounds at 5 waves per SIMD).
-int resident_blocks(gnk_ctx* ctx, const void* fn, int block = BLOCK) {
+int resident_blocks(gnk_ctx* ctx, const void* fn, int block = BLOCK, size_t lds = 0) {
   int per = 0;
-  const auto it = ctx->resident.find(fn);
+  const auto it = ctx->resident.find(fn);     // (a kernel's dynamic LDS is fixed by its template arguments)
   if (it != ctx->resident.end()) {
     per = it->second;
   } else {
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, fn, block, 0) != hipSuccess || per < 1) per = 1;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, fn, block, lds) != hipSuccess || per < 1) per = 1;
     ctx->resident[fn] = per;
   }
   return per * ctx->num_cus;
@@ -3318,7 +3323,9 @@ int gnk_bratu_residual(gnk_ctx* ctx, const double* x, const double* y, double* r
   if (!y) return fail(ctx, "bratu_residual: y is NULL");
   int64_t lr0, nlr;
   residual_rows(ctx, lr0, nlr);
-  RowLaunch L = rows(ctx, lr0, nlr, vec_of(ctx));
+  // persistent: the resident workgroups walk the rows (one partial per workgroup, not per row chunk)
+  const void* fnr = vec_of(ctx) == 2 ? (const void*)&k_forward<2> : (const void*)&k_forward<1>;
+  RowLaunch L = rows(ctx, lr0, nlr, vec_of(ctx), resident_blocks(ctx, fnr));
   const int nblk = L.grid.x * L.grid.y;
   DISPATCH_VEC(ctx, k_forward, L, 0, x, y, r, ctx->geo, ctx->coef, L.lr0, L.nlr, ctx->scratch);
   int rc = check_launch(ctx, "bratu_residual");
@@ -3456,7 +3463,8 @@ int gnk_basis_gemv_pending(gnk_ctx* ctx, const double* V, int64_t ldv, int k, co
   if (vec_of(ctx) == 2 && (ldv % 2 != 0)) return fail(ctx, "basis_gemv_pending: ldv must be even");
   double* w = const_cast<double*>(V) + int64_t(k) * ldv;
   if (x == w) return fail(ctx, "basis_gemv_pending: x aliases the pending column");
-  RowLaunch L = rows(ctx, 0, ctx->geo.nrows + 2 * G, vec_of(ctx), 2048);
+  const void* fnp = vec_of(ctx) == 2 ? (const void*)&k_gemv_p<2> : (const void*)&k_gemv_p<1>;
+  RowLaunch L = rows(ctx, 0, ctx->geo.nrows + 2 * G, vec_of(ctx), resident_blocks(ctx, fnp));
   const int nblk = L.grid.x * L.grid.y;
   DISPATCH_VEC(ctx, k_gemv_p, L, 0, V, ldv, k, c, hh, w, x, ctx->geo, L.lr0, L.nlr, ctx->scratch);
   int rc = check_launch(ctx, "basis_gemv_pending");
@@ -3669,6 +3677,43 @@ int gnk_gram(gnk_ctx* ctx, const double* u, const double* V, int64_t ldv, int k,
       return check_launch(ctx, "gram scatter (staged)");
     }
   }
+  // 5..7 column blocks on a grid of 32-point strips: k_gram_x (marching, RinvAug in VGPRs); tuning
+  // GNK_TUNE_GRAM_WIDE 3 keeps the pair-split k_gram below (tooling A/B).  At 2..4 blocks (k = 21..63)
+  // the barrier-free chunked / prefetching kernels stay 1.1-1.5x faster (profiles/round3/gram_wide_ab.jsonl)
+  if (nb >= 5 && nb <= 7 && ctx->geo.N % GX_T == 0 && ldv % 2 == 0 && tuning(ctx, GNK_TUNE_GRAM_WIDE) != 3) {
+    const size_t ldsx = size_t(2) * GX_T * (KP + 1) * 8 + size_t(2) * GX_T * 8;    // W, Y tiles + jdiag rows
+    if (size_t(4 * ((P + 3) / 4)) * 256 * 8 > ldsx) return fail(ctx, "gram: reduction staging does not fit (x)");
+    const int64_t nstrips = ctx->geo.N / GX_T;
+    const int64_t nrows = ctx->geo.nrows;
+    // a persistent grid of the resident workgroups over (row range, strip) items; items = lcm(strips,
+    // workgroups) when the rows allow, so every workgroup gets the same number
+    const void* fnx = nb == 5 ? (const void*)&k_gram_x<5> : nb == 6 ? (const void*)&k_gram_x<6>
+                                : (const void*)&k_gram_x<7>;
+    // resident 8-wave workgroups: one per CU (marching rows, B fragments, pair tiles: ~2 waves per SIMD)
+    const int64_t nwg = resident_blocks(ctx, fnx, 64 * GX_NW, ldsx);
+    int64_t gcd = nstrips, bb = nwg;
+    while (bb) { const int64_t t2 = gcd % bb; gcd = bb; bb = t2; }
+    int64_t nranges = std::max<int64_t>(1, std::min<int64_t>(nrows, nwg / gcd));
+    const int64_t rpr = (nrows + nranges - 1) / nranges;
+    nranges = (nrows + rpr - 1) / rpr;
+    const int64_t nitems = nstrips * nranges;
+    const int PGx = 4 * ((P + 3) / 4);
+    if (nwg > (1 << 20) || size_t(nwg) * PGx * 256 > SCRATCH_DOUBLES) return fail(ctx, "gram: scratch too small (x)");
+    const int64_t nown = nrows * ctx->geo.N;
+    TimedLaunch tlx(ctx, GNK_TIMER_GRAM, 8.0 * double(nown) * double(k + 1 + (r ? 1 : 0)));
+#define GRAMX(NBV)                                                                                                \
+  hipLaunchKernelGGL(k_gram_x<NBV>, dim3(unsigned(nwg)), dim3(64 * GX_NW), ldsx, ctx->stream, u, V, ldv, k, rinv, r, \
+                     ctx->geo, ctx->coef, rpr, nitems, ctx->scratch)
+    if (nb == 5) GRAMX(5); else if (nb == 6) GRAMX(6); else GRAMX(7);
+#undef GRAMX
+    tlx.done();
+    int rcx = check_launch(ctx, "gram_x");
+    if (rcx) return rcx;
+    (void)hipMemsetAsync(G_out, 0, size_t(KP) * KP * sizeof(double), ctx->stream);
+    hipLaunchKernelGGL(k_gram_reduce, dim3((P * 256 + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, ctx->stream, ctx->scratch,
+                       int(nwg), P, PGx, KP, G_out);
+    return check_launch(ctx, "gram reduce (x)");
+  }
   if (KP <= 64) {
     // wave-independent streaming kernel
     // chunk height: 64 rows for one column block, 32 rows above (LDS tile 32 x (KP+1) per wave)
@@ -3796,41 +3841,6 @@ int gnk_gram(gnk_ctx* ctx, const double* u, const double* V, int64_t ldv, int k,
     hipLaunchKernelGGL(k_gram_scatter, dim3((P * 256 + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, ctx->stream, red, P, KP,
                        G_out);
     return check_launch(ctx, "gram scatter");
-  }
-  // 5..7 column blocks on a grid of 32-point strips: k_gram_x (RinvAug in VGPRs, two workgroups per CU);
-  // tuning GNK_TUNE_GRAM_WIDE 3 keeps the pair-split k_gram below (tooling A/B)
-  if (nb >= 5 && nb <= 7 && ctx->geo.N % GX_T == 0 && ldv % 2 == 0 && tuning(ctx, GNK_TUNE_GRAM_WIDE) != 3) {
-    // one 8-wave workgroup per CU (the registers of the marching fill, the wave pair's B fragments and
-    // its pair tiles: ~2 waves per SIMD)
-    const size_t ldsx = size_t(2) * GX_T * (KP + 1) * 8 + size_t(2) * GX_T * 8;    // W, Y tiles + jdiag rows
-    if (size_t(4 * ((P + 3) / 4)) * 256 * 8 > ldsx) return fail(ctx, "gram: reduction staging does not fit (x)");
-    const int64_t nstrips = ctx->geo.N / GX_T;
-    const int64_t nrows = ctx->geo.nrows;
-    // a persistent grid of the resident workgroups over (row range, strip) items; items = lcm(strips,
-    // workgroups) when the rows allow, so every workgroup gets the same number
-    const int64_t nwg = int64_t(ctx->num_cus);
-    int64_t gcd = nstrips, bb = nwg;
-    while (bb) { const int64_t t2 = gcd % bb; gcd = bb; bb = t2; }
-    int64_t nranges = std::max<int64_t>(1, std::min<int64_t>(nrows, nwg / gcd));
-    const int64_t rpr = (nrows + nranges - 1) / nranges;
-    nranges = (nrows + rpr - 1) / rpr;
-    const int64_t nitems = nstrips * nranges;
-    const int PGx = 4 * ((P + 3) / 4);
-    if (nwg > (1 << 20) || size_t(nwg) * PGx * 256 > SCRATCH_DOUBLES) return fail(ctx, "gram: scratch too small (x)");
-    const int64_t nown = nrows * ctx->geo.N;
-    TimedLaunch tlx(ctx, GNK_TIMER_GRAM, 8.0 * double(nown) * double(k + 1 + (r ? 1 : 0)));
-#define GRAMX(NBV)                                                                                                \
-  hipLaunchKernelGGL(k_gram_x<NBV>, dim3(unsigned(nwg)), dim3(64 * GX_NW), ldsx, ctx->stream, u, V, ldv, k, rinv, r, \
-                     ctx->geo, ctx->coef, rpr, nitems, ctx->scratch)
-    if (nb == 5) GRAMX(5); else if (nb == 6) GRAMX(6); else GRAMX(7);
-#undef GRAMX
-    tlx.done();
-    int rcx = check_launch(ctx, "gram_x");
-    if (rcx) return rcx;
-    (void)hipMemsetAsync(G_out, 0, size_t(KP) * KP * sizeof(double), ctx->stream);
-    hipLaunchKernelGGL(k_gram_reduce, dim3((P * 256 + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, ctx->stream, ctx->scratch,
-                       int(nwg), P, PGx, KP, G_out);
-    return check_launch(ctx, "gram reduce (x)");
   }
   const int rowsplit = P <= PPW_MAX ? 1 : 0;
   // pair-split: the P pair tiles spread evenly over the 4 waves (PPW = ceil(P / 4), instantiated up
