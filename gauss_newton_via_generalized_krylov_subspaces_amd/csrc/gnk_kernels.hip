@@ -3323,9 +3323,9 @@ int gnk_bratu_residual(gnk_ctx* ctx, const double* x, const double* y, double* r
   if (!y) return fail(ctx, "bratu_residual: y is NULL");
   int64_t lr0, nlr;
   residual_rows(ctx, lr0, nlr);
-  // persistent: the resident workgroups walk the rows (one partial per workgroup, not per row chunk)
-  const void* fnr = vec_of(ctx) == 2 ? (const void*)&k_forward<2> : (const void*)&k_forward<1>;
-  RowLaunch L = rows(ctx, lr0, nlr, vec_of(ctx), resident_blocks(ctx, fnr));
+  // one workgroup per row chunk (a persistent grid of the resident workgroups measured 17 % slower:
+  // 0.37 vs 0.32 ms at 8192^2, profiles/round3/rocprof_window_breakdown.json)
+  RowLaunch L = rows(ctx, lr0, nlr, vec_of(ctx));
   const int nblk = L.grid.x * L.grid.y;
   DISPATCH_VEC(ctx, k_forward, L, 0, x, y, r, ctx->geo, ctx->coef, L.lr0, L.nlr, ctx->scratch);
   int rc = check_launch(ctx, "bratu_residual");

@@ -11,7 +11,7 @@
 * C5 (configs[4]): Bratu 16384^2 with the basis growing without restart (krylow_restart 100,
   ref:gauss_newton_krylow.py:81-82, ref:krylow.py:72-73) to k = 71 -- through every Gram kernel of
   the wide path: the staged MFMA pass (k <= 20), the chunked pass (k_gram_w, 21..47), the prefetching
-  pass (k_gram_wp, 48..63) and the pair-split pass (k_gram, k >= 64).  k = 200 does not fit one GPU
+  pass (k_gram_wp, 48..63) and the marching wide pass (k_gram_x, k >= 64).  k = 200 does not fit one GPU
   (the basis alone is 429 GB); the full-size run is checked by properties:
     - the reference basis (sc_j V_j, krylow.py) is orthonormal: max |V^T V - I| <= ORTH_TOL, computed on
       the device (gnk_flat_gemv_t);
@@ -83,7 +83,7 @@ def test_c5_16384_wide_basis_properties():
     k = b.k
     ks = [t["k"] for t in s.trace]
     print(f"C5 16384^2: nit {book[0]} nrev {book[1]} basis k = {k}, per-step k {ks[0]}..{ks[-1]}")
-    assert book[0] == max_iter - 1 and k >= 70 and max(ks) >= 64          # the pair-split kernel ran
+    assert book[0] == max_iter - 1 and k >= 70 and max(ks) >= 64          # the k_gram_x kernel ran
     # orthonormality of the reference basis, on the device (whole slab: the exterior ghost rows are 0)
     be = dev.backend
     h = be.zeros(k)

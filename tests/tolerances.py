@@ -18,6 +18,9 @@ by its own sensitivity test:
     recurrence ends 2.3e-9 (of max |x|) away from the reference's np.dot recurrence;
   * the converged last outer iteration of the p = 2 Rosenbrock GN runs, whose CG stopping test on a
     2-element residual is a rounding tie (the exactly rounded dot flips one of them, 3 vs 4).
+Bookkeeping is exact everywhere except one recorded rounding tie: the Armijo count of C2 res_old's
+converged last step, where the step is at the noise level -- the reference family's own counts for
+that step span last_nfev_range("c2_res_old") (82..105).
 """
 import json
 import os
@@ -62,3 +65,12 @@ def per_iteration(case, n, key="x"):
 def trajectory_bound(case, key="x"):
     """One bound for a whole trajectory (the multi-slab runs): max(1e-10, max_i envelope_i)."""
     return max(NORTH_STAR, float(envelope(case, key).max()))
+
+
+def last_nfev_range(case):
+    """(min, max) of the last iteration's cumulative nfev over the recorded reordering variants of
+    ``case`` (the reference's own arithmetic, reordered): the spread of a converged step's Armijo
+    count, which is decided by rounding noise."""
+    v = sensitivity()[case]["variants"]
+    last = [int(x["nfev"][-1]) for x in v.values()]
+    return min(last), max(last)

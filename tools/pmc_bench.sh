@@ -1,7 +1,7 @@
 #!/bin/bash
 # HBM traffic of the bench's dominant kernel: two rocprofv3 counter passes (FETCH_SIZE,
-# WRITE_SIZE; --kernel-trace only) over the driver's bench command (--steps 20 --warmup 5, the
-# default repeats), then tools/pmc_summary.py over exactly the timed regions' Gram launches (the
+# WRITE_SIZE; --kernel-trace only) over the driver's bench command (its default steps, warmup and
+# repeats), then tools/pmc_summary.py over exactly the timed regions' Gram launches (the
 # window file bench.py writes).  Extra arguments go to bench.py.
 set -o pipefail
 R="${GRAFT_REPO_ROOT:-$(pwd)}"
@@ -9,7 +9,7 @@ OUT="$R/gpurun_out/pmc_bench"
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
 for c in FETCH_SIZE WRITE_SIZE; do
-  GNK_BENCH_WINDOW_OUT="$OUT/window_$c.json" timeout -k 10 500 rocprofv3 --kernel-trace --pmc $c -d "$OUT/$c" -o run --output-format csv -- python3 "$R/bench.py" --steps 20 --warmup 5 --cpu-seconds 0 --cg-iters 0 --jvp-reps 5 "$@" > "$OUT/$c.log" 2>&1 || exit $?
+  GNK_BENCH_WINDOW_OUT="$OUT/window_$c.json" timeout -k 10 500 rocprofv3 --kernel-trace --pmc $c -d "$OUT/$c" -o run --output-format csv -- python3 "$R/bench.py" --cpu-seconds 0 --cg-iters 0 --jvp-reps 5 "$@" > "$OUT/$c.log" 2>&1 || exit $?
 done
 cmp -s <(python3 -c "import json,sys; d=json.load(open(sys.argv[1])); print(d['gram_launch_offset'], d['launch_bytes'])" "$OUT/window_FETCH_SIZE.json") \
        <(python3 -c "import json,sys; d=json.load(open(sys.argv[1])); print(d['gram_launch_offset'], d['launch_bytes'])" "$OUT/window_WRITE_SIZE.json") \
