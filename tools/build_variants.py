@@ -23,6 +23,24 @@ VARIANTS = {
     # k_gram_s: Gram step replaced by one add (transform + stencil + DMA only)
     "nogram": [("        gram(H, Lx);                                  // row x (its r is in slot x)",
                 "        acc[0] += H[0][0];")],
+    # k_gram_x: the transform's block chains split into two accumulators (even / odd k-steps)
+    "gx2acc": [("""          d4 qa = d4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+          for (int ab = 0; ab <= CA; ++ab)
+#pragma unroll
+            for (int ks = 0; ks < 4; ++ks) qa = mfma64(arow[ab * 16 + ks * 4], rA[ab][ks], qa);
+#pragma unroll
+          for (int ii = 0; ii < 4; ++ii) Yt""", """          d4 qa = d4{0.0, 0.0, 0.0, 0.0}, qz = d4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+          for (int ab = 0; ab <= CA; ++ab)
+#pragma unroll
+            for (int ks = 0; ks < 4; ks += 2) {
+              qa = mfma64(arow[ab * 16 + ks * 4], rA[ab][ks], qa);
+              qz = mfma64(arow[ab * 16 + ks * 4 + 4], rA[ab][ks + 1], qz);
+            }
+          qa = qa + qz;
+#pragma unroll
+          for (int ii = 0; ii < 4; ++ii) Yt""")],
     # k_gram_s: no VALU tail / r sums (MFMA tile only)
     "notail": [("    if (NB == 2) {\n#pragma unroll\n      for (int t = 0; t < TAIL; ++t) {",
                 "    if (false) {\n#pragma unroll\n      for (int t = 0; t < TAIL; ++t) {")],
