@@ -354,8 +354,10 @@ class GNSolver:
 
     def __init__(self, problem, y, tol=1e-8, max_iter=100, cg_preconditioner=False, cg_rtol=1e-4,
                  comm: Optional[Comm] = None, device=None, backend=None, callback: Callable = None,
-                 callback_format="numpy", ops=None, cg_variant="scipy"):
+                 callback_format="numpy", ops=None, cg_variant="scipy", cg_maxiter=None):
+        # cg_maxiter (tooling: bench / full-size tests) caps every CG run below scipy's 10 n
         self.ops = ops if ops is not None else BratuGNOps(problem, y, comm, device, backend)
+        self.cg_maxiter = cg_maxiter
         self.dev = getattr(self.ops, "dev", None)
         self.be = self.ops.be
         self.comm = self.ops.comm
@@ -400,7 +402,7 @@ class GNSolver:
             d = ops.dense_lstsq(x, r, self._dvec())                 # :115-116 (cg_iter keeps its value)
         else:
             d, self.cg_iter = self.cg.solve(x, r, cg_rtol=self.cg_rtol, preconditioner=self.cg_pre,  # :111-114
-                                            variant=self.cg_variant)
+                                            variant=self.cg_variant, maxiter=self.cg_maxiter)
         jdd = ops.jvp_sumsq(x, d)                                    # sum((J d)^2) (ref:armijo_goldstein.py:50)
         xt, rt = self.xb[1 - self.xi], self.rb[1 - self.ri]
         last = {}

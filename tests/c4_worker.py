@@ -16,6 +16,11 @@ frees its state and rank 0 runs the same solve on one rank over the whole grid. 
     comparison of ||x_k||, whatever the summation order (at 8192^2 the reference's own reorderings move
     ||x_1|| by 2e-7: tests/golden/sensitivity.json, head8192); the later iterates inherit that absolute
     difference, so beyond iteration 1 the bound is the pinned 8192^2 cycle's own spread (cycle_spread).
+Then GN + CGLS at the same size and partition ("C3 at 32768^2"; ref:gauss_newton.py:11-60,
+63-138): GN_ITERS outer iterations, Jacobi CGLS at rtol 1e-8 capped at CG_MAXITER iterations per solve,
+8 ranks vs 1 rank.  The CG scalars and ||.||^2 are compensated pairs merged across ranks before one
+rounding (slab.Comm.sum_pairs), so cg_iter, nfev and the per-iteration ||x_k||^2 (the solver's own
+compensated sum) must agree bit for bit; ||r_k||^2 is a plain rank-ordered sum, within 1e-10.
 Memory: ITERS = 6 iterations hold at most 7 basis columns (+ ~9 vectors) x 8.6 GB ~ 140 GB, on 8
 ranks or on one.  (A restart inside the window would make the next step a k = 1 step whose Armijo
 test compares two sums of 1e9 squares differing by less than their rounding: the reference's own
@@ -38,6 +43,7 @@ import torch.distributed as dist
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import gauss_newton_via_generalized_krylov_subspaces_amd as gnk  # noqa: E402
 from gauss_newton_via_generalized_krylov_subspaces_amd._device import BratuDevice  # noqa: E402
+from gauss_newton_via_generalized_krylov_subspaces_amd.gauss_newton import GNSolver  # noqa: E402
 from gauss_newton_via_generalized_krylov_subspaces_amd.inputs import slab_inputs  # noqa: E402
 from gauss_newton_via_generalized_krylov_subspaces_amd.slab import Comm  # noqa: E402
 from tests.transport_shim import StagedTransportComm  # noqa: E402
@@ -98,11 +104,78 @@ def solve(N, comm, restart, iters):
     return out
 
 
+def solve_gn(N, comm, iters, cg_maxiter):
+    prob = gnk.BratuPdeProblem(N + 1, 5, 10)
+    dev = BratuDevice(prob, comm)
+    u0, y, ut = slab_inputs(dev)
+    del ut
+    rec = {"xnorm2": [], "rsumsq": [], "nfev": [], "cg_iter": []}
+
+    def cb(x, nfev, cg_iter):
+        rec["xnorm2"].append(x.ops.sumsq(x.x))                 # compensated, pairs merged across ranks
+        rec["rsumsq"].append(float(x.sumsq))
+        rec["nfev"].append(int(nfev))
+        rec["cg_iter"].append(int(cg_iter))
+        log(f"GN it {len(rec['nfev'])}: cg_iter {cg_iter} nfev {nfev} ||x||^2 {rec['xnorm2'][-1]!r}")
+
+    s = GNSolver(prob, y, max_iter=iters + 1, cg_preconditioner=True, cg_rtol=1e-8, comm=comm,
+                 backend=dev.backend, callback=cb, callback_format="device", cg_maxiter=cg_maxiter)
+    buf = io.StringIO()
+    t0 = time.time()
+    with contextlib.redirect_stdout(buf):
+        s.setup(u0)
+        del u0
+        while not s.step():
+            pass
+        r = s.finish(result_format="torch")
+    torch.cuda.synchronize()
+    out = {"nit": r.nit, "nfev": r.nfev, "njev": r.njev, "success": bool(r.success), **{"it_" + k: v for k, v in rec.items()},
+           "t": [t["t"] for t in s.trace], "stdout": buf.getvalue(), "cg_total": s.cg.total_iters,
+           "seconds": time.time() - t0}
+    del s, r, y, dev
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+    return out
+
+
+def gn_phase(a, comm, rank, world):
+    """GN + CGLS, 8 ranks vs 1 rank (module docstring); returns rank 0's report (None elsewhere)."""
+    log(f"multi-rank GN + CGLS, grid {a.grid}, world {world}, CG capped at {a.cg_maxiter}")
+    mine = solve_gn(a.grid, comm, a.gn_iters, a.cg_maxiter)
+    log(f"multi-rank GN done in {mine['seconds']:.1f} s: cg_iter {mine['it_cg_iter']}")
+    every = [None] * world
+    dist.all_gather_object(every, mine)
+    dist.barrier()
+    if rank != 0:
+        dist.barrier()
+        return None
+    try:
+        one = solve_gn(a.grid, Comm(single=True), a.gn_iters, a.cg_maxiter)
+        log(f"single-rank GN done in {one['seconds']:.1f} s")
+    except Exception as e:
+        log(f"single-rank GN raised {type(e).__name__}: {e}")
+        one = {"error": f"{type(e).__name__}: {e}"}
+    dist.barrier()
+    strip = lambda d: {k: v for k, v in d.items() if k != "seconds"}   # noqa: E731
+    ranks_identical = all(strip(e) == strip(mine) for e in every)
+    exact = ("nit", "nfev", "njev", "success", "it_nfev", "it_cg_iter", "it_xnorm2", "t", "stdout", "cg_total")
+    bit_identical = all(mine[k] == one.get(k) for k in exact)
+    rr = one.get("it_rsumsq", [])
+    rel_r = (float(np.max(np.abs(np.sqrt(mine["it_rsumsq"]) - np.sqrt(rr)) / np.sqrt(rr)))
+             if len(rr) == len(mine["it_rsumsq"]) and rr else float("inf"))
+    ok = bool(ranks_identical and bit_identical and rel_r <= TOL and mine["nit"] == a.gn_iters)
+    return {"ok": ok, "ranks_identical": ranks_identical, "bit_identical": bit_identical, "max_rel_rnorm_diff": rel_r,
+            "gn_iters": a.gn_iters, "cg_maxiter": a.cg_maxiter, "multi": strip(mine), "single": strip(one),
+            "seconds_multi": mine["seconds"], "seconds_single": one.get("seconds")}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--grid", type=int, default=32768)
     ap.add_argument("--restart", type=int, default=20)
     ap.add_argument("--iters", type=int, default=6)
+    ap.add_argument("--gn-iters", type=int, default=2)
+    ap.add_argument("--cg-maxiter", type=int, default=40)
     ap.add_argument("--out", required=True)
     a = ap.parse_args()
     torch.cuda.set_device(0)
@@ -117,6 +190,8 @@ def main():
     dist.barrier()
     if rank != 0:
         dist.barrier()                                      # rank 0's single-rank solve
+        if a.gn_iters > 0:
+            gn_phase(a, comm, rank, world)
         dist.destroy_process_group()
         return 0
     log("single-rank solve over the whole grid")
@@ -145,7 +220,11 @@ def main():
            "ranks_identical": ranks_identical, "bookkeeping_equal": same, "max_rel_xnorm_diff": rx,
            "max_rel_rnorm_diff": rr, "tol": TOL, "rel_xnorm_diff": ex.tolist(), "xnorm_bound": xb.tolist(),
            "x_within_bound": bool(np.all(ex <= xb)) if len(ex) == len(xb) else False, "multi": {k: v for k, v in mine.items() if k != "stdout"},
-           "single": {k: v for k, v in one.items() if k != "stdout"}, "shim_calls": comm.staged_calls}
+           "single": {k: v for k, v in one.items() if k != "stdout"}, "shim_calls": dict(comm.staged_calls)}
+    if a.gn_iters > 0:
+        rep["gn"] = gn_phase(a, comm, rank, world)
+        rep["ok"] = bool(rep["ok"] and rep["gn"]["ok"])
+        rep["shim_calls_total"] = dict(comm.staged_calls)
     with open(a.out, "w") as f:
         json.dump(rep, f, indent=1)
     log(json.dumps({k: rep[k] for k in ("ok", "ranks_identical", "bookkeeping_equal", "max_rel_xnorm_diff",

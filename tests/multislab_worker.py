@@ -121,6 +121,36 @@ def run_oracle(kind, N, **kw):
             "cg_iter": cgs, "norms": norms, "stdout": out.getvalue()}
 
 
+DEFAULT_ITERS = 45
+ORACLE_FIXTURE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "multislab_oracle.json")
+
+
+def case_key(kind, kw):
+    return kind + ":" + json.dumps(kw, sort_keys=True)
+
+
+def cases_for(N, iters):
+    """The solver cases run at grid N (GN unpreconditioned only where its sensitivity evidence exists)."""
+    from tests import tolerances as T
+    cases = [("gnk", dict(krylow_restart=20, max_iter=iters, version=v))
+             for v in ("res_old", "res_new", "jac_old_res_old", "jac_old_res_new")]
+    if f"gn{N}" in T.sensitivity():               # unpreconditioned GN: evidence recorded at grid 256
+        cases.append(("gn", dict(max_iter=4, cg_rtol=1e-4)))
+    cases.append(("gn", dict(max_iter=3, cg_rtol=1e-4, cg_preconditioner=True)))
+    return cases
+
+
+def oracle_result(kind, N, kw):
+    """The oracle's run of a case: from the committed fixture (tests/golden/make_multislab_oracle.py,
+    the same run_oracle) when it holds the case, else computed here."""
+    if os.path.exists(ORACLE_FIXTURE):
+        with open(ORACLE_FIXTURE) as f:
+            got = json.load(f)["grids"].get(str(N), {}).get(case_key(kind, kw))
+        if got is not None:
+            return got
+    return run_oracle(kind, N, **kw)
+
+
 BACKEND = None          # --numpy: the NumPy test double of the C-ABI (CPU rehearsal of this script)
 
 
@@ -177,7 +207,7 @@ def staged_vs_host(prob, y_full, u0_full, comm, steps):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--grid", type=int, default=256)
-    ap.add_argument("--iters", type=int, default=45)
+    ap.add_argument("--iters", type=int, default=DEFAULT_ITERS)
     ap.add_argument("--out", required=True)
     ap.add_argument("--numpy", action="store_true")
     ap.add_argument("--transport", choices=("gloo", "shim"), default="gloo")
@@ -200,12 +230,7 @@ def main():
     one.backend.forward(one.load(prob.u_true), F)
     y = F[one.slab.own].cpu().numpy().copy()
     del one, F
-    cases = [("gnk", dict(krylow_restart=20, max_iter=a.iters, version=v))
-             for v in ("res_old", "res_new", "jac_old_res_old", "jac_old_res_new")]
-    from tests import tolerances as T
-    if f"gn{N}" in T.sensitivity():               # unpreconditioned GN: evidence recorded at grid 256
-        cases.append(("gn", dict(max_iter=4, cg_rtol=1e-4)))
-    cases.append(("gn", dict(max_iter=3, cg_rtol=1e-4, cg_preconditioner=True)))
+    cases = cases_for(N, a.iters)
     if a.transport == "shim":
         from tests.transport_shim import StagedTransportComm
         make_comm = StagedTransportComm
@@ -238,7 +263,7 @@ def main():
                  "ranks_identical": ranks_equal, "bookkeeping_equal": same, "max_rel_norm_diff": rel, "tol": tol,
                  "nit": s["nit"], "nrev": s["nrev"]}
         if a.oracle:
-            o = run_oracle(kind, N, **kw)
+            o = oracle_result(kind, N, kw)
             o_keys = keys if kind == "gn" else ("nit", "nrev", "njev", "success", "nfev", "stdout")
             o_same = all(d[f] == o[f] for f in o_keys)
             o_rel = rel_diff(d["norms"], o["norms"])
