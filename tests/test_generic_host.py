@@ -198,3 +198,49 @@ def test_wide_basis_beyond_63_columns():
 
 def test_dense_lstsq_100_parameters():
     check_dense_100(dict(_backend=NumpyBackend()))
+
+
+def _graded_step(svals, backend_kw, seed=7, m=14):
+    """One GN step on the linear problem y - A x, A = U diag(svals) W^T; (step, svd of A, U^T y)."""
+    rng = np.random.default_rng(seed)
+    p = len(svals)
+    U, _ = np.linalg.qr(rng.standard_normal((m, m)))
+    W, _ = np.linalg.qr(rng.standard_normal((p, p)))
+    A = U[:, :p] @ np.diag(svals) @ W.T
+    y = rng.standard_normal(m)
+    rec = []
+    with contextlib.redirect_stdout(io.StringIO()):
+        try:
+            gnk.gauss_newton(lambda x: y - A @ x, np.zeros(p), lambda x: -A, max_iter=2,
+                             callback=lambda x, nfev, cg_iter: rec.append(x.copy()), **backend_kw)
+        except Exception as e:                      # noqa: BLE001 -- the step is what is checked
+            assert type(e).__name__ == "StepLengthConvergenceError", e
+    assert rec, "no step taken"
+    Us, ss, Vt = np.linalg.svd(A)
+    return rec[0], A, y, ss, Vt, Us[:, :p].T @ y     # linear problem: the full step (t = 1) is accepted
+
+
+def check_graded_spectrum_gn(backend_kw):
+    """dense Jacobians with singular values far below sqrt(eps) sigma_max.  scipy.linalg.lstsq
+    (gelsd, cond = eps) resolves every direction above eps sigma_max; the CholeskyQR solve only sees the
+    Gram, whose shifted factors regularise the directions below ~sqrt(n k eps) sigma_max (documented in
+    lls.CholQR2Solver).  What the step holds to (SVD of the computed A):
+      * one such direction (1, 1e-2, 1e-4, 1e-9): the components along the resolved directions equal the
+        least-squares solution's to 1e-6 (measured 1.5e-7);
+      * a graded tail (1 .. 1e-14, four directions below 1e-8): the step's residual is within 1e-4 of the
+        least-squares optimum (measured 4.5e-5; gelsd's own step, with 1e14-sized coefficients, lands
+        1.6e-4 above it) -- but its components along the resolved directions
+        deviate by up to ~5e-3 (relative) from gelsd's: the band where this branch and gelsd differ."""
+    d, A, y, ss, Vt, uy = _graded_step([1.0, 1e-2, 1e-4, 1e-9], backend_kw)
+    big = ss >= 1e-6 * ss[0]
+    np.testing.assert_allclose(Vt[big] @ d, uy[big] / ss[big], rtol=1e-6)
+    d, A, y, ss, Vt, uy = _graded_step([1.0, 1e-2, 1e-4, 1e-9, 1e-11, 1e-13, 1e-14], backend_kw)
+    r_opt2 = float(y @ y - uy @ uy)                                     # min ||y - A x||^2 (SVD)
+    r_dev2 = float(np.sum((y - A @ d) ** 2))
+    r_ref2 = float(np.sum((y - A @ np.linalg.lstsq(A, y, rcond=None)[0]) ** 2))   # gelsd's step: 1.6e-4 above
+    assert r_opt2 * (1 - 1e-10) <= r_dev2 <= r_opt2 * (1 + 1e-4), (r_dev2, r_opt2)
+    assert r_dev2 <= r_ref2, (r_dev2, r_ref2)
+
+
+def test_graded_spectrum_dense_gn():
+    check_graded_spectrum_gn(dict(_backend=NumpyBackend()))

@@ -177,6 +177,11 @@ def test_rank_deficient_dense_gn_gpu():
     check_rank_deficient_gn({})
 
 
+def test_graded_spectrum_dense_gn_gpu():
+    from tests.test_generic_host import check_graded_spectrum_gn
+    check_graded_spectrum_gn({})
+
+
 def test_rank_deficient_gnk_gpu():
     from tests.test_generic_host import check_rank_deficient_gnk
     check_rank_deficient_gnk({})
