@@ -44,6 +44,11 @@ VARIANTS = {
     # k_gram_s: no VALU tail / r sums (MFMA tile only)
     "notail": [("    if (NB == 2) {\n#pragma unroll\n      for (int t = 0; t < TAIL; ++t) {",
                 "    if (false) {\n#pragma unroll\n      for (int t = 0; t < TAIL; ++t) {")],
+    # k_gram_v1: the next row's V / u / r loads issued one row ahead (software-pipelined march)
+    "v1pf": [("    for (int64_t x = x0; x < x1; ++x, i += N) {\n      double vs[K], eo[K];\n#pragma unroll\n      for (int j = 0; j < K; ++j) {\n        const double* cp = V + j * ldv + i;\n        vs[j] = cp[N];\n        eo[j] = (edge_w || edge_e) ? cp[eoff] : 0.0;     // only the strip's edge lanes load\n      }\n      const double dn = -jdiag(c, u[i]);\n      const double rv = r[i];\n      double a[K];", "    double vs[K], eo[K];\n#pragma unroll\n    for (int j = 0; j < K; ++j) {\n      const double* cp = V + j * ldv + i;\n      vs[j] = cp[N];\n      eo[j] = (edge_w || edge_e) ? cp[eoff] : 0.0;\n    }\n    double uc = u[i], rv = r[i];\n    for (int64_t x = x0; x < x1; ++x, i += N) {\n      // the next row's loads are issued before this row's arithmetic (row G + x + 2 <= the last ghost row)\n      double vs2[K], eo2[K];\n#pragma unroll\n      for (int j = 0; j < K; ++j) {\n        const double* cp = V + j * ldv + i + N;\n        vs2[j] = cp[N];\n        eo2[j] = (edge_w || edge_e) ? cp[eoff] : 0.0;\n      }\n      const double u2 = u[i + N], r2 = r[i + N];\n      const double dn = -jdiag(c, uc);\n      double a[K];"), ('        a[j] = sv;\n        vn[j] = vc[j];\n        vc[j] = vs[j];\n      }\n      gram_v_point<K>(a, rv, T, ldt, acc);\n    }', '        a[j] = sv;\n        vn[j] = vc[j];\n        vc[j] = vs[j];\n      }\n      gram_v_point<K>(a, rv, T, ldt, acc);\n#pragma unroll\n      for (int j = 0; j < K; ++j) {\n        vs[j] = vs2[j];\n        eo[j] = eo2[j];\n      }\n      uc = u2;\n      rv = r2;\n    }')],
+    # k_gram_v1: the transform T staged in LDS (broadcast reads) instead of SGPRs (18 / 52 SGPR spills at K = 8 / 9)
+    "v1lds": [("__global__ __launch_bounds__(BLOCK) void k_gram_v1(",
+               "__global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(2))) void k_gram_v1("), ("  const int eoff = edge_w ? -1 : 1;                 // the edge lanes' outer neighbour (others: unused)\n  double acc[NT];", "  const int eoff = edge_w ? -1 : 1;                 // the edge lanes' outer neighbour (others: unused)\n  __shared__ double Ts[K * K];\n  for (int t = threadIdx.x; t < K * K; t += BLOCK) Ts[t] = T[(t / K) * ldt + t % K];\n  __syncthreads();\n  double acc[NT];"), ('      gram_v_point<K>(a, rv, T, ldt, acc);\n    }\n  }\n#pragma unroll\n  for (int q = 0; q < NT; ++q) {\n    const double sq = wave_sum(acc[q]);\n    if (lane == 0) red[wave][q] = sq;\n  }\n  __syncthreads();\n  for (int q = threadIdx.x; q < NT; q += BLOCK) {\n    double sq = red[0][q];\n    for (int w = 1; w < BLOCK / 64; ++w) sq += red[w][q];\n    partial[size_t(blockIdx.x) * NT + q] = sq;\n  }\n}\n\n// packed upper triangle', '      int z = 0;\n      asm volatile("" : "+s"(z));                   // opaque 0: the LDS reads stay in the row loop\n      gram_v_point<K>(a, rv, Ts + z, K, acc);\n    }\n  }\n#pragma unroll\n  for (int q = 0; q < NT; ++q) {\n    const double sq = wave_sum(acc[q]);\n    if (lane == 0) red[wave][q] = sq;\n  }\n  __syncthreads();\n  for (int q = threadIdx.x; q < NT; q += BLOCK) {\n    double sq = red[0][q];\n    for (int w = 1; w < BLOCK / 64; ++w) sq += red[w][q];\n    partial[size_t(blockIdx.x) * NT + q] = sq;\n  }\n}\n\n// packed upper triangle')],
 }
 
 
