@@ -49,6 +49,10 @@ VARIANTS = {
     # k_gram_v1: the transform T staged in LDS (broadcast reads) instead of SGPRs (18 / 52 SGPR spills at K = 8 / 9)
     "v1lds": [("__global__ __launch_bounds__(BLOCK) void k_gram_v1(",
                "__global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(2))) void k_gram_v1("), ("  const int eoff = edge_w ? -1 : 1;                 // the edge lanes' outer neighbour (others: unused)\n  double acc[NT];", "  const int eoff = edge_w ? -1 : 1;                 // the edge lanes' outer neighbour (others: unused)\n  __shared__ double Ts[K * K];\n  for (int t = threadIdx.x; t < K * K; t += BLOCK) Ts[t] = T[(t / K) * ldt + t % K];\n  __syncthreads();\n  double acc[NT];"), ('      gram_v_point<K>(a, rv, T, ldt, acc);\n    }\n  }\n#pragma unroll\n  for (int q = 0; q < NT; ++q) {\n    const double sq = wave_sum(acc[q]);\n    if (lane == 0) red[wave][q] = sq;\n  }\n  __syncthreads();\n  for (int q = threadIdx.x; q < NT; q += BLOCK) {\n    double sq = red[0][q];\n    for (int w = 1; w < BLOCK / 64; ++w) sq += red[w][q];\n    partial[size_t(blockIdx.x) * NT + q] = sq;\n  }\n}\n\n// packed upper triangle', '      int z = 0;\n      asm volatile("" : "+s"(z));                   // opaque 0: the LDS reads stay in the row loop\n      gram_v_point<K>(a, rv, Ts + z, K, acc);\n    }\n  }\n#pragma unroll\n  for (int q = 0; q < NT; ++q) {\n    const double sq = wave_sum(acc[q]);\n    if (lane == 0) red[wave][q] = sq;\n  }\n  __syncthreads();\n  for (int q = threadIdx.x; q < NT; q += BLOCK) {\n    double sq = red[0][q];\n    for (int w = 1; w < BLOCK / 64; ++w) sq += red[w][q];\n    partial[size_t(blockIdx.x) * NT + q] = sq;\n  }\n}\n\n// packed upper triangle')],
+    # k_jvp: non-temporal stores of J v / a grid of the resident workgroups (row-strided) / both
+    "jvpnt": [('      o.y = jvp_pt(c, d1, vn.y, vc.x, true, vc.y, ve, he, vs.y);\n    }\n    *reinterpret_cast<d2*>(out + li) = o;', '      o.y = jvp_pt(c, d1, vn.y, vc.x, true, vc.y, ve, he, vs.y);\n    }\n    __builtin_nontemporal_store(o, reinterpret_cast<d2*>(out + li));')],
+    "jvpres": [('  RowLaunch L = rows(ctx, G, ctx->geo.nrows, vec_of(ctx), 1 << 30);\n  TimedLaunch tl(ctx, GNK_TIMER_JVP, 24.0 * double(ctx->geo.nrows) * double(ctx->geo.N));\n  DISPATCH_VEC(ctx, k_jvp, L, 0, u, v, out, ctx->geo, ctx->coef, L.lr0, L.nlr, 0);', '  RowLaunch L = rows(ctx, G, ctx->geo.nrows, vec_of(ctx), resident_blocks(ctx, (const void*)&k_jvp<2>));\n  TimedLaunch tl(ctx, GNK_TIMER_JVP, 24.0 * double(ctx->geo.nrows) * double(ctx->geo.N));\n  DISPATCH_VEC(ctx, k_jvp, L, 0, u, v, out, ctx->geo, ctx->coef, L.lr0, L.nlr, 0);')],
+    "jvpntres": [('      o.y = jvp_pt(c, d1, vn.y, vc.x, true, vc.y, ve, he, vs.y);\n    }\n    *reinterpret_cast<d2*>(out + li) = o;', '      o.y = jvp_pt(c, d1, vn.y, vc.x, true, vc.y, ve, he, vs.y);\n    }\n    __builtin_nontemporal_store(o, reinterpret_cast<d2*>(out + li));'), ('  RowLaunch L = rows(ctx, G, ctx->geo.nrows, vec_of(ctx), 1 << 30);\n  TimedLaunch tl(ctx, GNK_TIMER_JVP, 24.0 * double(ctx->geo.nrows) * double(ctx->geo.N));\n  DISPATCH_VEC(ctx, k_jvp, L, 0, u, v, out, ctx->geo, ctx->coef, L.lr0, L.nlr, 0);', '  RowLaunch L = rows(ctx, G, ctx->geo.nrows, vec_of(ctx), resident_blocks(ctx, (const void*)&k_jvp<2>));\n  TimedLaunch tl(ctx, GNK_TIMER_JVP, 24.0 * double(ctx->geo.nrows) * double(ctx->geo.N));\n  DISPATCH_VEC(ctx, k_jvp, L, 0, u, v, out, ctx->geo, ctx->coef, L.lr0, L.nlr, 0);')],
 }
 
 
