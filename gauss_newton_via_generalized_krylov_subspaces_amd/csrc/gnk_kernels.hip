@@ -308,6 +308,144 @@ __global__ __launch_bounds__(BLOCK) void k_forward(const double* __restrict__ x,
   if (partial) block_sum_store<1>(acc, 1, partial + (blockIdx.y * gridDim.x + blockIdx.x), sh);
 }
 
+// Two grid rows per pass (rows lr, lr + 1; VEC 2 and N % 512 == 0, so every lane of every block holds
+// two points of the row -- no lanes past its end): the centre and south rows of the stencil vector serve both output rows, 4 row loads
+// per 2 output rows instead of 6.  The per-point arithmetic is k_jvp's / k_forward's, bit for bit.
+// 8192^2 JVP 0.319 -> 0.271 ms (5.05 -> 5.94 TB/s), 16384^2 5.6 -> 6.05 TB/s
+// (profiles/round3/jvp2_ab.jsonl).  Launched with gridDim.y = ceil(nlr / 2): one pass per block.
+constexpr int ROWS2_ALIGN = 2 * BLOCK;
+
+// J(u) v (TR false) / J(u)^T w (TR true)
+template <bool TR>
+__global__ __launch_bounds__(BLOCK) void k_jvp2(const double* __restrict__ u, const double* __restrict__ v,
+                                                double* __restrict__ out, Geo geo, Coef c, int64_t lr0, int64_t nlr) {
+  const int lane = threadIdx.x & 63;
+  const int64_t N = geo.N;
+  const int64_t iy = (int64_t(blockIdx.x) * BLOCK + threadIdx.x) * 2;
+  const bool hw = iy > 0, he = iy + 2 < N;
+  for (int64_t p = blockIdx.y; 2 * p < nlr; p += gridDim.y) {
+    const int64_t lr = lr0 + 2 * p;
+    const bool two = 2 * p + 1 < nlr;               // block-uniform
+    const int64_t li = lr * N + iy;
+    const d2 vn = *reinterpret_cast<const d2*>(v + li - N);
+    const d2 vc = *reinterpret_cast<const d2*>(v + li);
+    const d2 vs = *reinterpret_cast<const d2*>(v + li + N);
+    const d2 u0 = *reinterpret_cast<const d2*>(u + li);
+    d2 vss = {0.0, 0.0}, u1 = {0.0, 0.0};
+    if (two) {
+      vss = *reinterpret_cast<const d2*>(v + li + 2 * N);
+      u1 = *reinterpret_cast<const d2*>(u + li + N);
+    }
+    double vw0 = __shfl_up(vc.y, 1), ve0 = __shfl_down(vc.x, 1);
+    double vw1 = __shfl_up(vs.y, 1), ve1 = __shfl_down(vs.x, 1);
+    if (lane == 0) {
+      vw0 = hw ? v[li - 1] : 0.0;
+      vw1 = hw ? v[li + N - 1] : 0.0;
+    }
+    if (lane == 63) {
+      ve0 = he ? v[li + 2] : 0.0;
+      ve1 = he ? v[li + N + 2] : 0.0;
+    }
+    const double d00 = jdiag(c, u0.x), d01 = jdiag(c, u0.y);
+    d2 o;
+    if (TR) {
+      o.x = vjp_pt(c, d00, vn.x, vw0, hw, vc.x, vc.y, true, vs.x);
+      o.y = vjp_pt(c, d01, vn.y, vc.x, true, vc.y, ve0, he, vs.y);
+    } else {
+      o.x = jvp_pt(c, d00, vn.x, vw0, hw, vc.x, vc.y, true, vs.x);
+      o.y = jvp_pt(c, d01, vn.y, vc.x, true, vc.y, ve0, he, vs.y);
+    }
+    *reinterpret_cast<d2*>(out + li) = o;
+    if (two) {
+      const double d10 = jdiag(c, u1.x), d11 = jdiag(c, u1.y);
+      if (TR) {
+        o.x = vjp_pt(c, d10, vc.x, vw1, hw, vs.x, vs.y, true, vss.x);
+        o.y = vjp_pt(c, d11, vc.y, vs.x, true, vs.y, ve1, he, vss.y);
+      } else {
+        o.x = jvp_pt(c, d10, vc.x, vw1, hw, vs.x, vs.y, true, vss.x);
+        o.y = jvp_pt(c, d11, vc.y, vs.x, true, vs.y, ve1, he, vss.y);
+      }
+      *reinterpret_cast<d2*>(out + li + N) = o;
+    }
+  }
+}
+
+// out = pde_operator(x) (y == nullptr) or y - pde_operator(x).  partial (residual): the sum of out^2 over
+// each owned row's 512-point segment at [row offset * gridDim.x + blockIdx.x] -- exactly k_forward's
+// partials when that kernel runs one row per block (same per-thread order, same block reduction)
+__global__ __launch_bounds__(BLOCK) void k_forward2(const double* __restrict__ x, const double* __restrict__ y,
+                                                    double* __restrict__ out, Geo geo, Coef c, int64_t lr0,
+                                                    int64_t nlr, double* __restrict__ partial) {
+  __shared__ double sh[2][BLOCK / 64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int64_t N = geo.N;
+  const int64_t iy = (int64_t(blockIdx.x) * BLOCK + threadIdx.x) * 2;
+  const bool hw = iy > 0, he = iy + 2 < N;
+  for (int64_t p = blockIdx.y; 2 * p < nlr; p += gridDim.y) {
+    const int64_t lr = lr0 + 2 * p;
+    const bool two = 2 * p + 1 < nlr;               // block-uniform
+    const int64_t li = lr * N + iy;
+    const d2 xn = *reinterpret_cast<const d2*>(x + li - N);
+    const d2 xc = *reinterpret_cast<const d2*>(x + li);
+    const d2 xs = *reinterpret_cast<const d2*>(x + li + N);
+    d2 xss = {0.0, 0.0};
+    if (two) xss = *reinterpret_cast<const d2*>(x + li + 2 * N);
+    double xw0 = __shfl_up(xc.y, 1), xe0 = __shfl_down(xc.x, 1);
+    double xw1 = __shfl_up(xs.y, 1), xe1 = __shfl_down(xs.x, 1);
+    if (lane == 0) {
+      xw0 = hw ? x[li - 1] : 0.0;
+      xw1 = hw ? x[li + N - 1] : 0.0;
+    }
+    if (lane == 63) {
+      xe0 = he ? x[li + 2] : 0.0;
+      xe1 = he ? x[li + N + 2] : 0.0;
+    }
+    double acc0 = 0.0, acc1 = 0.0;
+    d2 f;
+    f.x = fwd_pt(c, xn.x, xw0, hw, xc.x, xc.y, true, xs.x);
+    f.y = fwd_pt(c, xn.y, xc.x, true, xc.y, xe0, he, xs.y);
+    if (y) {
+      const d2 yy = *reinterpret_cast<const d2*>(y + li);
+      f.x = yy.x - f.x;
+      f.y = yy.y - f.y;
+    }
+    *reinterpret_cast<d2*>(out + li) = f;
+    if (lr >= G && lr < G + geo.nrows) {
+      acc0 += f.x * f.x;
+      acc0 += f.y * f.y;
+    }
+    if (two) {
+      f.x = fwd_pt(c, xc.x, xw1, hw, xs.x, xs.y, true, xss.x);
+      f.y = fwd_pt(c, xc.y, xs.x, true, xs.y, xe1, he, xss.y);
+      if (y) {
+        const d2 yy = *reinterpret_cast<const d2*>(y + li + N);
+        f.x = yy.x - f.x;
+        f.y = yy.y - f.y;
+      }
+      *reinterpret_cast<d2*>(out + li + N) = f;
+      if (lr + 1 >= G && lr + 1 < G + geo.nrows) {
+        acc1 += f.x * f.x;
+        acc1 += f.y * f.y;
+      }
+    }
+    if (partial) {
+      const double s0 = wave_sum(acc0), s1 = wave_sum(acc1);
+      if (lane == 0) {
+        sh[0][wave] = s0;
+        sh[1][wave] = s1;
+      }
+      __syncthreads();
+      if (threadIdx.x < (two ? 2 : 1)) {
+        const int q = threadIdx.x;
+        double t = sh[q][0];
+        for (int w = 1; w < BLOCK / 64; ++w) t += sh[q][w];
+        partial[(2 * p + q) * int64_t(gridDim.x) + blockIdx.x] = t;
+      }
+      __syncthreads();
+    }
+  }
+}
+
 template <int VEC>
 __global__ __launch_bounds__(BLOCK) void k_diag_jtj(const double* __restrict__ u, double* __restrict__ out,
                                                     Geo geo, Coef c, int64_t lr0, int64_t nlr, int recip) {
@@ -3083,6 +3221,14 @@ int resident_blocks(gnk_ctx* ctx, const void* fn, int block = BLOCK, size_t lds 
 
 int vec_of(const gnk_ctx* ctx) { return (ctx->geo.N % 2 == 0) ? 2 : 1; }
 
+// k_jvp2 / k_forward2 apply (whole waves of two-point lanes, one block per row segment): turn L (a
+// one-pass row launch) into their grid of row pairs; false leaves L as it was
+bool rows2(const gnk_ctx* ctx, RowLaunch& L) {
+  if (ctx->geo.N % ROWS2_ALIGN != 0 || L.nlr < 1) return false;
+  L.grid.y = unsigned(std::min<int64_t>((L.nlr + 1) / 2, 65535));
+  return true;
+}
+
 int64_t owned_lr0() { return G; }
 
 // local rows of the residual: owned +- 1 clipped to the domain
@@ -3298,7 +3444,10 @@ int gnk_bratu_jvp(gnk_ctx* ctx, const double* u, const double* v, double* out) {
   if (!ready(ctx)) return -1;
   RowLaunch L = rows(ctx, G, ctx->geo.nrows, vec_of(ctx), 1 << 30);
   TimedLaunch tl(ctx, GNK_TIMER_JVP, 24.0 * double(ctx->geo.nrows) * double(ctx->geo.N));
-  DISPATCH_VEC(ctx, k_jvp, L, 0, u, v, out, ctx->geo, ctx->coef, L.lr0, L.nlr, 0);
+  if (rows2(ctx, L))
+    hipLaunchKernelGGL(k_jvp2<false>, L.grid, dim3(BLOCK), 0, ctx->stream, u, v, out, ctx->geo, ctx->coef, L.lr0, L.nlr);
+  else
+    DISPATCH_VEC(ctx, k_jvp, L, 0, u, v, out, ctx->geo, ctx->coef, L.lr0, L.nlr, 0);
   tl.done();
   return check_launch(ctx, "bratu_jvp");
 }
@@ -3306,15 +3455,22 @@ int gnk_bratu_jvp(gnk_ctx* ctx, const double* u, const double* v, double* out) {
 int gnk_bratu_vjp(gnk_ctx* ctx, const double* u, const double* w, double* out) {
   if (!ready(ctx)) return -1;
   RowLaunch L = rows(ctx, G, ctx->geo.nrows, vec_of(ctx), 1 << 30);
-  DISPATCH_VEC(ctx, k_jvp, L, 0, u, w, out, ctx->geo, ctx->coef, L.lr0, L.nlr, 1);
+  if (rows2(ctx, L))
+    hipLaunchKernelGGL(k_jvp2<true>, L.grid, dim3(BLOCK), 0, ctx->stream, u, w, out, ctx->geo, ctx->coef, L.lr0, L.nlr);
+  else
+    DISPATCH_VEC(ctx, k_jvp, L, 0, u, w, out, ctx->geo, ctx->coef, L.lr0, L.nlr, 1);
   return check_launch(ctx, "bratu_vjp");
 }
 
 int gnk_bratu_forward(gnk_ctx* ctx, const double* x, double* F) {
   if (!ready(ctx)) return -1;
   RowLaunch L = rows(ctx, G, ctx->geo.nrows, vec_of(ctx), 1 << 30);
-  DISPATCH_VEC(ctx, k_forward, L, 0, x, (const double*)nullptr, F, ctx->geo, ctx->coef, L.lr0, L.nlr,
-               (double*)nullptr);
+  if (rows2(ctx, L))
+    hipLaunchKernelGGL(k_forward2, L.grid, dim3(BLOCK), 0, ctx->stream, x, (const double*)nullptr, F, ctx->geo,
+                       ctx->coef, L.lr0, L.nlr, (double*)nullptr);
+  else
+    DISPATCH_VEC(ctx, k_forward, L, 0, x, (const double*)nullptr, F, ctx->geo, ctx->coef, L.lr0, L.nlr,
+                 (double*)nullptr);
   return check_launch(ctx, "bratu_forward");
 }
 
@@ -3327,7 +3483,12 @@ int gnk_bratu_residual(gnk_ctx* ctx, const double* x, const double* y, double* r
   // 0.37 vs 0.32 ms at 8192^2, profiles/round3/rocprof_window_breakdown.json)
   RowLaunch L = rows(ctx, lr0, nlr, vec_of(ctx));
   const int nblk = L.grid.x * L.grid.y;
-  DISPATCH_VEC(ctx, k_forward, L, 0, x, y, r, ctx->geo, ctx->coef, L.lr0, L.nlr, ctx->scratch);
+  // two rows per block where k_forward runs one row per block (its partials, bit for bit)
+  if (int64_t(L.grid.y) == L.nlr && rows2(ctx, L))
+    hipLaunchKernelGGL(k_forward2, L.grid, dim3(BLOCK), 0, ctx->stream, x, y, r, ctx->geo, ctx->coef, L.lr0, L.nlr,
+                       ctx->scratch);
+  else
+    DISPATCH_VEC(ctx, k_forward, L, 0, x, y, r, ctx->geo, ctx->coef, L.lr0, L.nlr, ctx->scratch);
   int rc = check_launch(ctx, "bratu_residual");
   if (rc) return rc;
   if (norm2_out) return reduce(ctx, ctx->scratch, nblk, 1, 1, nullptr, norm2_out);
