@@ -55,6 +55,8 @@ VARIANTS = {
     "jvpntres": [('      o.y = jvp_pt(c, d1, vn.y, vc.x, true, vc.y, ve, he, vs.y);\n    }\n    *reinterpret_cast<d2*>(out + li) = o;', '      o.y = jvp_pt(c, d1, vn.y, vc.x, true, vc.y, ve, he, vs.y);\n    }\n    __builtin_nontemporal_store(o, reinterpret_cast<d2*>(out + li));'), ('  RowLaunch L = rows(ctx, G, ctx->geo.nrows, vec_of(ctx), 1 << 30);\n  TimedLaunch tl(ctx, GNK_TIMER_JVP, 24.0 * double(ctx->geo.nrows) * double(ctx->geo.N));\n  DISPATCH_VEC(ctx, k_jvp, L, 0, u, v, out, ctx->geo, ctx->coef, L.lr0, L.nlr, 0);', '  RowLaunch L = rows(ctx, G, ctx->geo.nrows, vec_of(ctx), resident_blocks(ctx, (const void*)&k_jvp<2>));\n  TimedLaunch tl(ctx, GNK_TIMER_JVP, 24.0 * double(ctx->geo.nrows) * double(ctx->geo.N));\n  DISPATCH_VEC(ctx, k_jvp, L, 0, u, v, out, ctx->geo, ctx->coef, L.lr0, L.nlr, 0);')],
     # k_jvp2: two grid rows per lane pass (4 v row loads per 2 output rows instead of 6)
     "jvp2r": [('template <int VEC>\n__global__ __launch_bounds__(BLOCK) void k_forward(', '// J(u) v for two grid rows per lane pass (rows lr, lr + 1; N % 128 == 0): the centre and south v rows\n// serve both outputs, so 4 v row loads per 2 output rows instead of 6; same per-point arithmetic as k_jvp\n__global__ __launch_bounds__(BLOCK) void k_jvp2(const double* __restrict__ u, const double* __restrict__ v,\n                                                double* __restrict__ out, Geo geo, Coef c, int64_t lr0, int64_t nlr) {\n  const int lane = threadIdx.x & 63;\n  const int64_t N = geo.N;\n  const int64_t iy = (int64_t(blockIdx.x) * BLOCK + threadIdx.x) * 2;\n  const bool hw = iy > 0, he = iy + 2 < N;\n  for (int64_t p = blockIdx.y; 2 * p < nlr; p += gridDim.y) {\n    const int64_t lr = lr0 + 2 * p;\n    const bool two = 2 * p + 1 < nlr;\n    const int64_t li = lr * N + iy;\n    const d2 vn = *reinterpret_cast<const d2*>(v + li - N);\n    const d2 vc = *reinterpret_cast<const d2*>(v + li);\n    const d2 vs = *reinterpret_cast<const d2*>(v + li + N);\n    const d2 vss = *reinterpret_cast<const d2*>(v + li + 2 * N);     // row lr + 2 <= the last ghost row\n    const d2 u0 = *reinterpret_cast<const d2*>(u + li);\n    const d2 u1 = *reinterpret_cast<const d2*>(u + li + N);\n    double vw0 = __shfl_up(vc.y, 1), ve0 = __shfl_down(vc.x, 1);\n    double vw1 = __shfl_up(vs.y, 1), ve1 = __shfl_down(vs.x, 1);\n    if (lane == 0) {\n      vw0 = hw ? v[li - 1] : 0.0;\n      vw1 = hw ? v[li + N - 1] : 0.0;\n    }\n    if (lane == 63) {\n      ve0 = he ? v[li + 2] : 0.0;\n      ve1 = he ? v[li + N + 2] : 0.0;\n    }\n    d2 o0, o1;\n    o0.x = jvp_pt(c, jdiag(c, u0.x), vn.x, vw0, hw, vc.x, vc.y, true, vs.x);\n    o0.y = jvp_pt(c, jdiag(c, u0.y), vn.y, vc.x, true, vc.y, ve0, he, vs.y);\n    *reinterpret_cast<d2*>(out + li) = o0;\n    if (two) {\n      o1.x = jvp_pt(c, jdiag(c, u1.x), vc.x, vw1, hw, vs.x, vs.y, true, vss.x);\n      o1.y = jvp_pt(c, jdiag(c, u1.y), vc.y, vs.x, true, vs.y, ve1, he, vss.y);\n      *reinterpret_cast<d2*>(out + li + N) = o1;\n    }\n  }\n}\n\ntemplate <int VEC>\n__global__ __launch_bounds__(BLOCK) void k_forward('), ('  RowLaunch L = rows(ctx, G, ctx->geo.nrows, vec_of(ctx), 1 << 30);\n  TimedLaunch tl(ctx, GNK_TIMER_JVP, 24.0 * double(ctx->geo.nrows) * double(ctx->geo.N));\n  DISPATCH_VEC(ctx, k_jvp, L, 0, u, v, out, ctx->geo, ctx->coef, L.lr0, L.nlr, 0);', '  RowLaunch L = rows(ctx, G, ctx->geo.nrows, vec_of(ctx), 1 << 30);\n  TimedLaunch tl(ctx, GNK_TIMER_JVP, 24.0 * double(ctx->geo.nrows) * double(ctx->geo.N));\n  if (ctx->geo.N % 128 == 0) {\n    L.grid.y = unsigned(std::min<int64_t>((L.nlr + 1) / 2, 65535));\n    hipLaunchKernelGGL(k_jvp2, L.grid, dim3(BLOCK), 0, ctx->stream, u, v, out, ctx->geo, ctx->coef, L.lr0, L.nlr);\n  } else\n  DISPATCH_VEC(ctx, k_jvp, L, 0, u, v, out, ctx->geo, ctx->coef, L.lr0, L.nlr, 0);')],
+    # k_gemv_vjpg: one workgroup per row segment (as k_jvp2) instead of the resident persistent grid
+    "vjpgrow": [('  RowLaunch L = rows(ctx, 0, ctx->geo.nrows + 2 * G, vec_of(ctx), resident_blocks(ctx, fn));', '  RowLaunch L = rows(ctx, 0, ctx->geo.nrows + 2 * G, vec_of(ctx), 1 << 30);')],
 }
 
 
