@@ -35,7 +35,7 @@ def close(a, b, scale=None, rtol=1e-13):
     np.testing.assert_allclose(a, b, rtol=0, atol=rtol * max(scale, 1e-300))
 
 
-@pytest.mark.parametrize("N", [8, 25, 64, 1024])
+@pytest.mark.parametrize("N", [8, 25, 64, 512, 1024])     # N % 512 == 0: the two-row k_jvp2 / k_forward2
 @pytest.mark.parametrize("lam", [10.0, 0.0])
 def test_operators_match_oracle(N, lam):
     prob, dev, ref = make(N, lam)
@@ -64,17 +64,21 @@ def test_operators_match_oracle(N, lam):
     np.testing.assert_allclose(n2.item(), np.sum(r_ref ** 2), rtol=1e-12)
 
 
-def test_jvp_bitwise_vs_oracle_small():
+@pytest.mark.parametrize("N", [64, 512])     # k_jvp (one row per pass) / k_jvp2 (two rows, N % 512 == 0)
+def test_jvp_bitwise_vs_oracle_small(N):
     """With the CSR summation order and no FMA contraction the stencil is bit-exact vs the oracle
     except where exp() differs by an ulp (lambda = 0 removes exp)."""
-    prob, dev, ref = make(64, lam=0.0)
+    prob, dev, ref = make(N, lam=0.0)
     rng = np.random.default_rng(7)
-    v = rng.standard_normal(64 * 64)
+    v = rng.standard_normal(N * N)
     out = dev.vec()
-    dev.backend.jvp(dev.load(np.zeros(64 * 64)), dev.load(v), out)
-    np.testing.assert_array_equal(own(dev, out), ref.jvp(np.zeros(64 * 64), v))
-    dev.backend.vjp(dev.load(np.zeros(64 * 64)), dev.load(v), out)
-    np.testing.assert_array_equal(own(dev, out), ref.vjp(np.zeros(64 * 64), v))
+    dev.backend.jvp(dev.load(np.zeros(N * N)), dev.load(v), out)
+    np.testing.assert_array_equal(own(dev, out), ref.jvp(np.zeros(N * N), v))
+    dev.backend.vjp(dev.load(np.zeros(N * N)), dev.load(v), out)
+    np.testing.assert_array_equal(own(dev, out), ref.vjp(np.zeros(N * N), v))
+    x = rng.standard_normal(N * N)
+    dev.backend.forward(dev.load(x), out)
+    close(own(dev, out), ref.pde_operator(x), rtol=1e-14)
 
 
 @pytest.mark.parametrize("N,k", [(24, 1), (24, 7), (100, 33), (1024, 20), (25, 5)])
