@@ -43,7 +43,7 @@ def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--repeats", type=int, default=3, help="timed regions of --steps each; value = median")
     ap.add_argument("--grid", type=int, default=8192, help="interior points per side N")
     ap.add_argument("--restart", type=int, default=20)
@@ -268,23 +268,53 @@ def c2_gpu(args, comm, device, grid=1024):
             "note": "GPU, second restart cycle (k = 1..20) of the same C2 run"}
 
 
-def pmc_traffic(config_key, window):
-    """HBM bytes per Gram launch from a committed rocprofv3 PMC summary (tools/pmc_summary.py) of this
-    configuration AND this timed window: same warmup / steps / repeats and the same algorithmic bytes
-    per launch (so the same basis sizes).  Otherwise (None, None): the line reports traffic null."""
+def pmc_traffic(config_key, window, section=None):
+    """HBM bytes per launch from a committed rocprofv3 PMC summary (tools/pmc_summary.py) of this
+    configuration AND this timed window: same warmup / steps / repeats / launch count and the same
+    algorithmic bytes per launch (so the same basis sizes).  section None: the Gram pass; "trial": the
+    first-trial kernel.  Otherwise (None, None): the line reports traffic null."""
+    count = "trial_launches" if section == "trial" else "gram_launches"
     for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "pmc_summary*.json")), reverse=True):
         try:
             with open(path) as f:
                 d = json.load(f)
         except (OSError, ValueError):
             continue
+        if d.get("config") != config_key:
+            continue
+        if section:
+            d = d.get(section) or {}
         w = d.get("window") or {}
-        if (d.get("config") == config_key and d.get("traffic_bytes_per_launch")
-                and all(w.get(k) == window[k] for k in ("warmup", "steps", "repeats", "gram_launches"))
+        if (d.get("traffic_bytes_per_launch")
+                and all(w.get(k) == window[k] for k in ("warmup", "steps", "repeats", count))
                 and abs(w.get("algorithmic_bytes_per_launch", 0.0) - window["algorithmic_bytes_per_launch"])
                 <= 1e-9 * window["algorithmic_bytes_per_launch"]):
             return d["traffic_bytes_per_launch"], os.path.relpath(path, ROOT)
     return None, None
+
+
+def stream_floor(be, n, device, reps):
+    """Measured HBM streaming floor on this box (gnk_probe_stream, HIP events): triad a = b + s c
+    (24 n bytes), read-only (8 n) and copy (16 n) over n doubles, the median of reps launches each --
+    what a perfectly coalesced kernel of that access mix reaches, the yardstick for the HBM-bound
+    kernels beside the 8 TB/s spec peak."""
+    from gauss_newton_via_generalized_krylov_subspaces_amd import _native
+    a = torch.empty(n, dtype=torch.float64, device=device)
+    b = torch.ones(n, dtype=torch.float64, device=device)
+    c = torch.ones(n, dtype=torch.float64, device=device)
+    out = {}
+    for name, mode in (("triad", 0), ("read", 1), ("copy", 2)):
+        for _ in range(3):
+            be.probe_stream(a, b, c, 0.5, n, mode)
+        be.timer_start(_native.TIMER_PROBE, reps)
+        for _ in range(reps):
+            be.probe_stream(a, b, c, 0.5, n, mode)
+        got = be.timer_collect(reps)
+        ms = float(np.median([m for m, _ in got]))
+        out[name] = {"ms": ms, "GBs": got[0][1] / (ms * 1e-3) / 1e9, "bytes": got[0][1]}
+    del a, b, c
+    out["kernel"] = "k_probe_stream (16-B accesses, 4 in flight per lane, one pass over n doubles)"
+    return out
 
 
 def main():
@@ -327,6 +357,11 @@ def main():
     solver.setup(u0)
     be = solver.be
     warm_s = []                 # per-step times of the warm-up steps (k = 1..warmup), synchronised each
+    # the warm-up's launches are counted (not timed into the result) so the PMC / trace tools can find
+    # the timed regions' launches of each kernel class among all bench-grid launches
+    wcap = 8 * (args.warmup + 1)
+    be.timer_start(_native.TIMER_GRAM, wcap)
+    be.timer_add(_native.TIMER_TRIAL)
     with contextlib.redirect_stdout(io.StringIO()):
         for _ in range(args.warmup):
             torch.cuda.synchronize()
@@ -334,15 +369,18 @@ def main():
             solver.step()
             torch.cuda.synchronize()
             warm_s.append(time.perf_counter() - t0)
+    wl = be.timer_collect_ids(wcap)
+    gram_offset = sum(1 for i, _, _ in wl if i == _native.TIMER_GRAM)    # bench-grid launches before the
+    trial_offset = sum(1 for i, _, _ in wl if i == _native.TIMER_TRIAL)  # first timed region
     # --repeats timed regions of exactly --steps outer iterations each (with the default 20 steps one
     # region is one whole restart cycle, k = 1..20); value = the median region's rate
-    cap = 4 * (args.steps + 1)
+    cap = 8 * (args.steps + 1)
     k_trace0 = len(solver.trace)
     passes0 = solver.lls.passes
-    gram_offset = solver.lls.passes            # bench-grid Gram launches before the first timed region
-    regions, launches = [], []
+    regions, launches, tlaunches = [], [], []
     for _ in range(args.repeats):
         be.timer_start(_native.TIMER_GRAM, cap)
+        be.timer_add(_native.TIMER_TRIAL)
         tr0 = len(solver.trace)
         comm.barrier()
         torch.cuda.synchronize()
@@ -354,7 +392,9 @@ def main():
         torch.cuda.synchronize()
         comm.barrier()
         el = time.perf_counter() - t0
-        launches += be.timer_collect(cap)
+        got = be.timer_collect_ids(cap)
+        launches += [(m, b) for i, m, b in got if i == _native.TIMER_GRAM]
+        tlaunches += [(m, b) for i, m, b in got if i == _native.TIMER_TRIAL]
         if world > 1:
             t = torch.tensor([el], dtype=torch.float64, device=device)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -380,11 +420,21 @@ def main():
     g_gbs = g_avg_bytes / (g_avg_ms * 1e-3) / 1e9 if g_ms else float("nan")
     window = {"warmup": args.warmup, "steps": args.steps, "repeats": args.repeats, "gram_launch_offset": gram_offset,
               "gram_launches": len(g_ms), "algorithmic_bytes_per_launch": g_avg_bytes}
+    # the first Armijo trial + update products (k_gemv_vjpg), the largest kernel by time
+    t_ms = [m for m, _ in tlaunches]
+    t_by = [b for _, b in tlaunches]
+    t_avg_ms = float(np.mean(t_ms)) if t_ms else float("nan")
+    t_avg_bytes = float(np.mean(t_by)) if t_by else float("nan")
+    t_gbs = t_avg_bytes / (t_avg_ms * 1e-3) / 1e9 if t_ms else float("nan")
+    twindow = {"warmup": args.warmup, "steps": args.steps, "repeats": args.repeats,
+               "trial_launch_offset": trial_offset, "trial_launches": len(t_ms),
+               "algorithmic_bytes_per_launch": t_avg_bytes}
     if os.environ.get("GNK_BENCH_WINDOW_OUT") and rank == 0:
-        # the Gram launches of the timed regions, for tools/pmc_summary.py (the PMC pass runs this same
-        # command under rocprofv3 and keeps exactly these launches)
+        # the Gram and first-trial launches of the timed regions, for tools/pmc_summary.py and
+        # tools/rocprof_window.py (they run this same command under rocprofv3 and keep exactly these)
         with open(os.environ["GNK_BENCH_WINDOW_OUT"], "w") as f:
-            json.dump({**window, "grid": N, "launch_bytes": g_by}, f)
+            json.dump({**window, "grid": N, "launch_bytes": g_by,
+                       "trial": {**twindow, "launch_bytes": t_by}}, f)
     gram_share = sum(g_ms) * 1e-3 / elapsed_all if g_ms else float("nan")
     # per basis size: columns = bytes / (8 n_rank) - 2 (V, u, r); kernel as gnk_gram dispatches a pass
     # with P^-1 and r: VALU k <= 9 (one point per lane from 8), staged k <= 20 (N % 128 == 0), chunked
@@ -422,6 +472,10 @@ def main():
     jl = be.timer_collect(args.jvp_reps)
     j_ms = float(np.median([m for m, _ in jl]))
     j_gbs = jl[0][1] / (j_ms * 1e-3) / 1e9
+    stream = stream_floor(be, n_rank, device, args.jvp_reps)
+    trial_by_k = {}
+    for m, b in tlaunches:
+        trial_by_k.setdefault(int(round(b / (8.0 * n_rank))), []).append(m)
 
     spec_stats = dict(solver.spec_stats)
     del solver, v, out, uu                      # free the GNK state (the basis) before the CG line
@@ -430,6 +484,7 @@ def main():
 
     config_key = f"bratu{N}_gnk_restart{args.restart}_{args.version}_ranks{world}"
     traffic, traffic_src = pmc_traffic(config_key, window)
+    t_traffic, t_traffic_src = pmc_traffic(config_key, twindow, section="trial")
     result = {
         "metric": "GN-Krylov outer iters/sec + JVP HBM GB/s, Bratu 8192² fp64, 1/2/4/8 GPUs",
         "value": steps_done / elapsed,
@@ -455,7 +510,21 @@ def main():
                      "traffic": traffic, "traffic_source": traffic_src,
                      "traffic_over_algorithmic": (traffic / g_avg_bytes) if traffic else None, "window": window,
                      "avg_launch_ms": g_avg_ms, "algorithmic_bytes_per_launch": g_avg_bytes,
-                     "launches": len(g_ms), "share_of_step_time": gram_share, "by_k": gram_by_k},
+                     "launches": len(g_ms), "share_of_step_time": gram_share, "by_k": gram_by_k,
+                     "trial": {"kernel": "k_gemv_vjpg (first Armijo trial x = V c, g = -J(x)^T r_old, h = V^T g; "
+                                         "pending column w = g - V hh materialised), one launch per step",
+                               "bound": "hbm", "achieved": t_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                               "frac": t_gbs / HBM_PEAK_GBS, "traffic": t_traffic, "traffic_source": t_traffic_src,
+                               "traffic_over_algorithmic": (t_traffic / t_avg_bytes) if t_traffic else None,
+                               "avg_launch_ms": t_avg_ms, "algorithmic_bytes_per_launch": t_avg_bytes,
+                               "bytes_model": "8 n (k + 3 + 2 [pending]): k settled columns, r in, x, g out, w r/w",
+                               "launches": len(t_ms), "window": twindow,
+                               "share_of_step_time": sum(t_ms) * 1e-3 / elapsed_all if t_ms else None,
+                               "frac_of_stream_floor": {m: t_gbs / stream[m]["GBs"] for m in ("read", "triad")},
+                               "by_vectors": {str(kk): {"ms": float(np.mean(v)),
+                                                        "GBs": 8.0 * n_rank * kk / (np.mean(v) * 1e-3) / 1e9}
+                                              for kk, v in sorted(trial_by_k.items())}}},
+        "stream_floor": stream,
         "jvp": {"kernel": "k_jvp (J(u) v, 5-point stencil)", "grid": N, "median_ms": j_ms, "GBs": j_gbs,
                 "frac_of_peak": j_gbs / HBM_PEAK_GBS, "algorithmic_bytes": jl[0][1]},
         "repeats": [{"steps": st, "seconds": el, "outer_iters_per_s": st / el} for st, el in regions],

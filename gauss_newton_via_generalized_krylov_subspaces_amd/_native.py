@@ -18,8 +18,8 @@ import torch
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("GNK_LIB", os.path.join(_HERE, "libgnk.so"))
 GHOST = 2  # GNK_GHOST_ROWS
-TIMER_GRAM, TIMER_JVP, TIMER_CG_MATVEC = 1, 2, 3  # GNK_TIMER_*
-ABI_VERSION = 3  # GNK_ABI_VERSION
+TIMER_GRAM, TIMER_JVP, TIMER_CG_MATVEC, TIMER_TRIAL, TIMER_PROBE = 1, 2, 3, 4, 5  # GNK_TIMER_*
+ABI_VERSION = 4  # GNK_ABI_VERSION
 # GNK_TUNE_* keys of gnk_set_tuning (tests / A/B tooling only; the solver never sets them)
 TUNE = {"gram_path": 0, "gram_ring": 1, "gram_v1min": 2, "cg_matvec": 3, "vjpg_blocks": 4, "gram_wide": 5}
 
@@ -80,8 +80,12 @@ SIGNATURES = {
     "gnk_lls_next": (_c_int, [_c_vp, _c_int, _c_int, _c_vp, _c_vp, _c_vp, _c_vp, _c_int, _c_vp, _c_vp, _c_vp, _c_vp,
                               _c_vp, _c_vp]),
     "gnk_probe_mfma_f64": (_c_int, [_c_vp, _c_vp, _c_int, _c_int]),
+    "gnk_probe_stream": (_c_int, [_c_vp, _c_vp, _c_vp, _c_vp, _c_dbl, _c_i64, _c_int]),
     "gnk_timer_start": (_c_int, [_c_vp, _c_int, _c_int]),
+    "gnk_timer_add": (_c_int, [_c_vp, _c_int]),
     "gnk_timer_collect": (_c_int, [_c_vp, ctypes.POINTER(_c_dbl), ctypes.POINTER(_c_dbl), _c_int]),
+    "gnk_timer_collect_ids": (_c_int, [_c_vp, ctypes.POINTER(_c_dbl), ctypes.POINTER(_c_dbl),
+                                       ctypes.POINTER(ctypes.c_int), _c_int]),
 }
 
 _LIB = None
@@ -357,6 +361,23 @@ class HipBackend:
         if n < 0:
             self._chk(n, "timer_collect")
         return [(ms[i], by[i]) for i in range(n)]
+
+    def timer_add(self, kernel_id):
+        """Also time the launches of another kernel class in the window timer_start opened."""
+        self._chk(self.lib.gnk_timer_add(self.ctx, int(kernel_id)), "timer_add")
+
+    def timer_collect_ids(self, capacity):
+        """-> list of (kernel class id, ms, algorithmic bytes) for each timed launch, in launch order."""
+        ms = (_c_dbl * capacity)()
+        by = (_c_dbl * capacity)()
+        ids = (ctypes.c_int * capacity)()
+        n = self.lib.gnk_timer_collect_ids(self.ctx, ms, by, ids, int(capacity))
+        if n < 0:
+            self._chk(n, "timer_collect_ids")
+        return [(ids[i], ms[i], by[i]) for i in range(n)]
+
+    def probe_stream(self, a, b, c, s, n, mode):
+        self._call("gnk_probe_stream", _p(a), _p(b), _p(c), float(s), int(n), int(mode))
 
     def probe_mfma(self, out, blocks, iters):
         self._call("gnk_probe_mfma_f64", _p(out), int(blocks), int(iters))

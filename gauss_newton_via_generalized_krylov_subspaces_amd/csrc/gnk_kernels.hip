@@ -3144,6 +3144,40 @@ __global__ void k_probe_mfma(double* out, int iters) {
   if (s[0] == 12345.0) out[threadIdx.x] = s[1] + s[2] + s[3];
 }
 
+// HBM streaming floor (tooling): mode 0 triad a = b + s c (2 reads, 1 write), 1 read-only (sum of b,
+// one partial per workgroup), 2 copy a = b.  16-B accesses, 4 independent ones per lane in flight.
+__global__ __launch_bounds__(BLOCK) void k_probe_stream(double* __restrict__ a, const double* __restrict__ b,
+                                                       const double* __restrict__ c, double s, int64_t n2, int mode,
+                                                       double* __restrict__ part) {
+  constexpr int U = 4;
+  const int64_t base = int64_t(blockIdx.x) * BLOCK * U + threadIdx.x;
+  const d2* B = reinterpret_cast<const d2*>(b);
+  const d2* C = reinterpret_cast<const d2*>(c);
+  d2* A = reinterpret_cast<d2*>(a);
+  d2 acc = {0.0, 0.0};
+  d2 vb[U], vc[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int64_t i = base + int64_t(u) * BLOCK;
+    vb[u] = i < n2 ? B[i] : d2{0.0, 0.0};
+    vc[u] = (mode == 0 && i < n2) ? C[i] : d2{0.0, 0.0};
+  }
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int64_t i = base + int64_t(u) * BLOCK;
+    if (mode == 1) {
+      acc += vb[u];
+    } else if (i < n2) {
+      A[i] = mode == 0 ? vb[u] + s * vc[u] : vb[u];
+    }
+  }
+  if (mode == 1) {
+    double t = acc[0] + acc[1];
+    for (int o = 32; o > 0; o >>= 1) t += __shfl_xor(t, o);
+    if ((threadIdx.x & 63) == 0) part[blockIdx.x * (BLOCK / 64) + threadIdx.x / 64] = t;
+  }
+}
+
 }  // namespace
 
 // ======================================================================== C-ABI
@@ -3162,10 +3196,11 @@ struct gnk_ctx {
   // gnk_set_tuning (tooling A/B of kernel choices; 0 = the product's choice)
   int tune[GNK_TUNE_COUNT] = {};
   // per-launch timer (tooling, see gnk_timer_start)
-  int timer_kernel = 0;
+  unsigned timer_mask = 0;     // bit id: kernel class id is timed
   int timer_count = 0;
   std::vector<hipEvent_t> timer_ev;
   std::vector<double> timer_bytes;
+  std::vector<int> timer_ids;
 };
 
 namespace {
@@ -3246,9 +3281,10 @@ struct TimedLaunch {
   gnk_ctx* ctx;
   int slot = -1;
   TimedLaunch(gnk_ctx* c, int kernel_id, double bytes) : ctx(c) {
-    if (c->timer_kernel == kernel_id && c->timer_count < int(c->timer_bytes.size())) {
+    if ((c->timer_mask >> kernel_id & 1u) && c->timer_count < int(c->timer_bytes.size())) {
       slot = c->timer_count++;
       c->timer_bytes[slot] = bytes;
+      c->timer_ids[slot] = kernel_id;
       (void)hipEventRecord(c->timer_ev[2 * slot], c->stream);
     }
   }
@@ -3594,7 +3630,10 @@ static int gemv_vjpg_launch(gnk_ctx* ctx, const char* what, const double* V, int
   Coef coef = ctx->coef;
   double* part = ctx->scratch;
   void* args[] = {&V, &ldv, &k, &c, &hh, &wcol, &r, &x, &g, &geo, &coef, &L.lr0, &L.nlr, &part, &spart};
+  // algorithmic bytes (owned rows): the k settled columns, r in, x and g out; pending: w read + written
+  TimedLaunch tl(ctx, GNK_TIMER_TRIAL, 8.0 * double(ctx->geo.nrows) * double(ctx->geo.N) * double(k + 3 + (pend ? 2 : 0)));
   (void)hipLaunchKernel(fn, L.grid, dim3(BLOCK), args, 0, ctx->stream);
+  tl.done();
   int rc = check_launch(ctx, what);
   if (rc) return rc;
   rc = wreduce(ctx, ctx->scratch, nblk, kk, kct, kct, int64_t(nblk) * kct, nullptr, h_out);
@@ -4302,18 +4341,28 @@ int gnk_cg_update_p(gnk_ctx* ctx, double beta, int first, const double* z, doubl
 int gnk_timer_start(gnk_ctx* ctx, int kernel_id, int capacity) {
   if (!ctx) return -1;
   if (capacity < 0) return fail(ctx, "timer_start: capacity < 0");
+  if (kernel_id < 1 || kernel_id > 30) return fail(ctx, "timer_start: kernel_id out of range");
   while (int(ctx->timer_ev.size()) < 2 * capacity) {
     hipEvent_t e;
     if (hipEventCreate(&e) != hipSuccess) return fail(ctx, "timer_start: hipEventCreate failed", -2);
     ctx->timer_ev.push_back(e);
   }
   ctx->timer_bytes.assign(capacity, 0.0);
-  ctx->timer_kernel = kernel_id;
+  ctx->timer_ids.assign(capacity, 0);
+  ctx->timer_mask = 1u << kernel_id;
   ctx->timer_count = 0;
   return 0;
 }
 
-int gnk_timer_collect(gnk_ctx* ctx, double* ms_out, double* bytes_out, int capacity) {
+int gnk_timer_add(gnk_ctx* ctx, int kernel_id) {
+  if (!ctx) return -1;
+  if (kernel_id < 1 || kernel_id > 30) return fail(ctx, "timer_add: kernel_id out of range");
+  if (!ctx->timer_mask) return fail(ctx, "timer_add: no timer started");
+  ctx->timer_mask |= 1u << kernel_id;
+  return 0;
+}
+
+int gnk_timer_collect_ids(gnk_ctx* ctx, double* ms_out, double* bytes_out, int* ids_out, int capacity) {
   if (!ctx) return -1;
   const int n = std::min(capacity, ctx->timer_count);
   for (int i = 0; i < n; ++i) {
@@ -4323,10 +4372,15 @@ int gnk_timer_collect(gnk_ctx* ctx, double* ms_out, double* bytes_out, int capac
       return fail(ctx, "timer_collect: elapsed", -2);
     ms_out[i] = ms;
     bytes_out[i] = ctx->timer_bytes[i];
+    if (ids_out) ids_out[i] = ctx->timer_ids[i];
   }
-  ctx->timer_kernel = 0;
+  ctx->timer_mask = 0;
   ctx->timer_count = 0;
   return n;
+}
+
+int gnk_timer_collect(gnk_ctx* ctx, double* ms_out, double* bytes_out, int capacity) {
+  return gnk_timer_collect_ids(ctx, ms_out, bytes_out, nullptr, capacity);
 }
 
 int gnk_rank_sum(gnk_ctx* ctx, const double* parts, int world, int64_t n, double* out) {
@@ -4365,6 +4419,22 @@ int gnk_lls_solve(gnk_ctx* ctx, const double* Gm, int kp, int k, const double* P
 }
 
 // tooling: fp64 MFMA issue-rate probe (not part of the solver)
+int gnk_probe_stream(gnk_ctx* ctx, double* a, const double* b, const double* c, double s, int64_t n, int mode) {
+  if (!ctx) return -1;
+  if (mode < 0 || mode > 2 || n < 2 || n % 2 != 0) return fail(ctx, "probe_stream: mode in 0..2, n even >= 2");
+  if (!b || (mode != 1 && !a) || (mode == 0 && !c)) return fail(ctx, "probe_stream: NULL argument");
+  const int64_t n2 = n / 2;
+  const int64_t blocks = (n2 + BLOCK * 4 - 1) / (BLOCK * 4);
+  if (blocks > (1 << 30) || (mode == 1 && blocks * (BLOCK / 64) > int64_t(SCRATCH_DOUBLES)))
+    return fail(ctx, "probe_stream: n too large");
+  const double bytes = 8.0 * double(n) * (mode == 0 ? 3.0 : mode == 1 ? 1.0 : 2.0);
+  TimedLaunch tl(ctx, GNK_TIMER_PROBE, bytes);
+  hipLaunchKernelGGL(k_probe_stream, dim3(unsigned(blocks)), dim3(BLOCK), 0, ctx->stream, a, b, c, s, n2, mode,
+                     ctx->scratch);
+  tl.done();
+  return check_launch(ctx, "probe_stream");
+}
+
 int gnk_probe_mfma_f64(gnk_ctx* ctx, double* out, int blocks, int iters) {
   if (!ctx) return -1;
   hipLaunchKernelGGL(k_probe_mfma, dim3(blocks), dim3(BLOCK), 0, ctx->stream, out, iters);

@@ -33,7 +33,7 @@ extern "C" {
 #endif
 
 #define GNK_GHOST_ROWS 2
-#define GNK_ABI_VERSION 3
+#define GNK_ABI_VERSION 4
 
 typedef struct gnk_ctx gnk_ctx;
 
@@ -248,18 +248,27 @@ int gnk_flat_gram(gnk_ctx* ctx, const double* W, int64_t ldw, int k, const doubl
                   const double* r, int64_t m, double* G_out);
 
 /* ---- tooling (not on the solver path) ----------------------------------- */
-/* Per-launch HIP-event timer for one kernel class (bench roofline): after
- * gnk_timer_start, the next `capacity` launches of that kernel are bracketed by
- * an event pair on the context's stream; gnk_timer_collect synchronises them and
- * returns the count, the milliseconds and the algorithmic bytes of each launch. */
+/* Per-launch HIP-event timer for kernel classes (bench roofline): after
+ * gnk_timer_start (one class; gnk_timer_add puts more classes in the same
+ * window), the next `capacity` launches of those kernels are bracketed by an
+ * event pair on the context's stream; gnk_timer_collect(_ids) synchronises them
+ * and returns the count, the milliseconds, the algorithmic bytes (and the class)
+ * of each launch in launch order. */
 #define GNK_TIMER_GRAM 1
 #define GNK_TIMER_JVP 2
 #define GNK_TIMER_CG_MATVEC 3
+#define GNK_TIMER_TRIAL 4   /* first Armijo trial + update products, k_gemv_vjpg */
+#define GNK_TIMER_PROBE 5   /* gnk_probe_stream */
 int gnk_timer_start(gnk_ctx* ctx, int kernel_id, int capacity);
+int gnk_timer_add(gnk_ctx* ctx, int kernel_id);
 int gnk_timer_collect(gnk_ctx* ctx, double* ms_out, double* bytes_out, int capacity);
+int gnk_timer_collect_ids(gnk_ctx* ctx, double* ms_out, double* bytes_out, int* ids_out, int capacity);
 /* back-to-back v_mfma_f64_16x16x4_f64 issue-rate probe: blocks x 256 threads,
  * 4 independent accumulators per wave, iters x 4 MFMAs per wave */
 int gnk_probe_mfma_f64(gnk_ctx* ctx, double* out, int blocks, int iters);
+/* HBM streaming floor: mode 0 triad a = b + s c, 1 read-only (sum of b into scratch), 2 copy a = b;
+ * n doubles (even), 16-B accesses; timed as GNK_TIMER_PROBE with 24 n / 8 n / 16 n bytes */
+int gnk_probe_stream(gnk_ctx* ctx, double* a, const double* b, const double* c, double s, int64_t n, int mode);
 
 #ifdef __cplusplus
 }

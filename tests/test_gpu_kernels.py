@@ -245,7 +245,7 @@ def test_cgs_max_propagates_nan():
     assert np.isnan(st[1].item()) and np.isnan(st[0].item())
 
 
-@pytest.mark.parametrize("N,k,with_r,with_rinv", [(24, 1, False, False), (24, 5, True, True), (100, 20, False, False),
+GRAM_CASES = [(24, 1, False, False), (24, 5, True, True), (100, 20, False, False),
                                                   (100, 20, True, True), (64, 47, True, True), (64, 70, True, False),
                                                   (1024, 20, True, True),
                                                   # marching kernel (N % 64 == 0): NB = 1 both passes, NB = 2 pass 1
@@ -267,14 +267,22 @@ def test_cgs_max_propagates_nan():
                                                   (100, 55, True, True), (96, 50, True, False), (416, 49, True, True),
                                                   # NB = 5..7: k_gram_x (N % 32 == 0; 1..5 strips) / k_gram (N = 100)
                                                   (128, 70, True, True), (96, 90, True, True), (64, 100, True, True),
-                                                  (160, 81, False, True), (32, 64, True, True), (100, 75, True, True)])
-@pytest.mark.parametrize("staged", ["default", "forced", "ring5"])
+                                                  (160, 81, False, True), (32, 64, True, True), (100, 75, True, True),
+                                                  # k_gram_x plain passes (RinvAug = identity, Gram straight from W)
+                                                  (128, 70, True, False), (96, 90, False, False),
+                                                  # pair-split k_gram, k >= 112 (C5's range on 8 GPUs)
+                                                  (64, 112, True, True), (96, 150, True, False), (64, 200, True, True),
+                                                  (32, 130, False, False)]
+# "forced" / "ring5" only where the staged kernel applies (N % 128 == 0, k <= 20)
+GRAM_PARAMS = [(N, k, r, ri, st) for (N, k, r, ri) in GRAM_CASES
+               for st in (("default", "forced", "ring5") if N % 128 == 0 and k <= 20 else ("default",))]
+
+
+@pytest.mark.parametrize("N,k,with_r,with_rinv,staged", GRAM_PARAMS)
 def test_gram_mfma(N, k, with_r, with_rinv, staged):
     """W = [J V | r] @ RinvAug on fp64 MFMA vs an fp64 NumPy Gram (host BLAS).  "forced" runs
     the staged LDS-DMA kernel for every pass it supports (N % 128 == 0, k <= 20) with its default
     4-slot ring (jdiag batched over 4 rows); "ring5" forces the 5-slot ring (one jdiag per row step)."""
-    if staged != "default" and (N % 128 or k > 20):
-        pytest.skip("staged kernel does not cover this shape")
     prob, dev, ref = make(N)
     be = dev.backend
     if staged != "default":
@@ -549,3 +557,27 @@ def test_rank_sum_matches_host_order(world, n):
     for p in range(1, world):
         s = s + parts[p]
     np.testing.assert_array_equal(out.cpu().numpy(), s)
+
+
+def test_timer_classes_and_stream_probe():
+    """The bench's per-launch timer with two classes in one window (Gram + first trial), launch order
+    and class ids kept; the streaming-floor probe computes triad / copy / read exactly."""
+    prob, dev, ref = make(1024)
+    be = dev.backend
+    n = 1 << 20
+    a = be.zeros(n)
+    b = torch.arange(n, dtype=torch.float64, device=a.device)
+    c = torch.full((n,), 3.0, dtype=torch.float64, device=a.device)
+    be.timer_start(_native.TIMER_PROBE, 8)
+    be.timer_add(_native.TIMER_JVP)
+    be.probe_stream(a, b, c, 0.5, n, 0)
+    torch.testing.assert_close(a, b + 1.5, rtol=0, atol=0)
+    be.probe_stream(a, c, None, 0.0, n, 2)
+    torch.testing.assert_close(a, c, rtol=0, atol=0)
+    be.probe_stream(None, b, None, 0.0, n, 1)
+    u = dev.load(np.zeros(1024 * 1024))
+    be.jvp(u, u, dev.vec())
+    got = be.timer_collect_ids(8)
+    assert [i for i, _, _ in got] == [_native.TIMER_PROBE] * 3 + [_native.TIMER_JVP]
+    assert [by for _, _, by in got] == [24.0 * n, 16.0 * n, 8.0 * n, 24.0 * 1024 * 1024]
+    assert all(ms > 0 for _, ms, _ in got)

@@ -9,7 +9,7 @@ OUT="$R/gpurun_out/pmc_bench"
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
 for c in FETCH_SIZE WRITE_SIZE; do
-  GNK_BENCH_WINDOW_OUT="$OUT/window_$c.json" timeout -k 10 500 rocprofv3 --kernel-trace --pmc $c -d "$OUT/$c" -o run --output-format csv -- python3 "$R/bench.py" --cpu-seconds 0 --cg-iters 0 --jvp-reps 5 "$@" > "$OUT/$c.log" 2>&1 || exit $?
+  GNK_BENCH_WINDOW_OUT="$OUT/window_$c.json" timeout -k 10 500 rocprofv3 --kernel-trace --pmc $c -d "$OUT/$c" -o run --output-format csv -- python3 "$R/bench.py" --gpus 1 --steps 20 --warmup 5 --cpu-seconds 0 --cg-iters 0 --jvp-reps 5 "$@" > "$OUT/$c.log" 2>&1 || exit $?
 done
 cmp -s <(python3 -c "import json,sys; d=json.load(open(sys.argv[1])); print(d['gram_launch_offset'], d['launch_bytes'])" "$OUT/window_FETCH_SIZE.json") \
        <(python3 -c "import json,sys; d=json.load(open(sys.argv[1])); print(d['gram_launch_offset'], d['launch_bytes'])" "$OUT/window_WRITE_SIZE.json") \

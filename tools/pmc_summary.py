@@ -20,6 +20,7 @@ import sys
 from collections import defaultdict
 
 GRAM = re.compile(r"k_gram_(?:[smw]p?|v1?)<")    # every Gram-pass kernel (staged / marching / chunked / VALU)
+TRIAL = re.compile(r"k_gemv_vjpg<")                # the first Armijo trial + update products
 BENCH_GRID_MIN = 50e6                              # bytes: launches on the bench grid (not the 256^2 pre-warm)
 
 
@@ -35,6 +36,29 @@ def load(d, counter):
     for v in vals.values():
         v.sort()
     return vals
+
+
+def section(f, w, pat, win, off_key, cnt_key):
+    """Launches of the kernels matching pat on the bench grid, in dispatch order across those kernels;
+    with a window: exactly the timed regions' launches, their traffic and the window's algorithmic bytes."""
+    gf = sorted((did, v) for name, lst in f.items() if pat.search(name) for did, v in lst if v > BENCH_GRID_MIN)
+    gw = dict((did, v) for name, lst in w.items() if pat.search(name) for did, v in lst)
+    seq = [(did, 2 * v + gw.get(did, 0.0)) for did, v in gf]
+    out = {}
+    if win:
+        lo, cnt = win[off_key], win[cnt_key]
+        sel = seq[lo:lo + cnt]
+        if len(sel) != cnt:
+            raise SystemExit(f"window {lo}+{cnt} outside the {len(seq)} bench-grid launches of {pat.pattern}")
+        alg = win["launch_bytes"]
+        out["window"] = {k: win[k] for k in ("warmup", "steps", "repeats", off_key, cnt_key,
+                                             "algorithmic_bytes_per_launch")}
+        out["traffic_bytes_per_launch"] = sum(t for _, t in sel) / cnt
+        out["traffic_over_algorithmic"] = sum(t for _, t in sel) / sum(alg)
+        out["per_launch"] = [{"algorithmic": a, "traffic": t} for a, (_, t) in zip(alg, sel)]
+    elif seq:
+        out["traffic_bytes_per_launch"] = sum(t for _, t in seq) / len(seq)
+    return out
 
 
 def main(d, config=None, window_path=None):
@@ -55,26 +79,14 @@ def main(d, config=None, window_path=None):
                                 "write_bytes": wm, "traffic_bytes_per_launch": 2 * fm + wm}
     if config:
         out["config"] = config
-    # Gram launches on the bench grid, in dispatch order across all Gram kernels
-    gf = sorted((did, v) for name, lst in f.items() if GRAM.search(name) for did, v in lst if v > BENCH_GRID_MIN)
-    gw = dict((did, v) for name, lst in w.items() if GRAM.search(name) for did, v in lst)
-    seq = [(did, 2 * v + gw.get(did, 0.0)) for did, v in gf]
-    out["gram_kernels"] = sorted(k for k in out["kernels"] if GRAM.search(k))
+    win = None
     if window_path:
         with open(window_path) as fh:
             win = json.load(fh)
-        lo, cnt = win["gram_launch_offset"], win["gram_launches"]
-        sel = seq[lo:lo + cnt]
-        if len(sel) != cnt:
-            raise SystemExit(f"window {lo}+{cnt} outside the {len(seq)} bench-grid Gram launches")
-        alg = win["launch_bytes"]
-        out["window"] = {k: win[k] for k in ("warmup", "steps", "repeats", "gram_launch_offset", "gram_launches",
-                                             "algorithmic_bytes_per_launch")}
-        out["traffic_bytes_per_launch"] = sum(t for _, t in sel) / cnt
-        out["traffic_over_algorithmic"] = sum(t for _, t in sel) / sum(alg)
-        out["per_launch"] = [{"algorithmic": a, "traffic": t} for a, (_, t) in zip(alg, sel)]
-    elif seq:
-        out["traffic_bytes_per_launch"] = sum(t for _, t in seq) / len(seq)
+    out["gram_kernels"] = sorted(k for k in out["kernels"] if GRAM.search(k))
+    out.update(section(f, w, GRAM, win, "gram_launch_offset", "gram_launches"))
+    if win and "trial" in win:
+        out["trial"] = section(f, w, TRIAL, win["trial"], "trial_launch_offset", "trial_launches")
     print(json.dumps(out, indent=1))
 
 

@@ -7,5 +7,5 @@ R="${GRAFT_REPO_ROOT:-$(pwd)}"
 OUT="$R/gpurun_out/prof_bench"
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
-GNK_BENCH_WINDOW_OUT="$OUT/window.json" timeout -k 10 900 rocprofv3 --kernel-trace --stats -d "$OUT" -o run --output-format csv -- python3 "$R/bench.py" --gpus 1 > "$OUT/bench.json" 2> "$OUT/bench.err" || exit $?
+GNK_BENCH_WINDOW_OUT="$OUT/window.json" timeout -k 10 900 rocprofv3 --kernel-trace --stats -d "$OUT" -o run --output-format csv -- python3 "$R/bench.py" --gpus 1 --steps 20 --warmup 5 "$@" > "$OUT/bench.json" 2> "$OUT/bench.err" || exit $?
 python3 "$R/tools/rocprof_window.py" "$(ls "$OUT"/*kernel_trace.csv "$OUT"/*/*kernel_trace.csv 2>/dev/null | head -1)" "$OUT/window.json" > "$OUT/window_avg.json"

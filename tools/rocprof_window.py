@@ -12,23 +12,33 @@ import re
 import sys
 
 GRAM = re.compile(r"k_gram_(?:[smw]p?|v1?)<")
+TRIAL = re.compile(r"k_gemv_vjpg<")
 
 
-def main(trace, window):
-    win = json.load(open(window))
+def window_avg(trace, pat, lo, cnt):
     rows = []
     for r in csv.DictReader(open(trace)):
-        if GRAM.search(r["Kernel_Name"]):
+        if pat.search(r["Kernel_Name"]):
             rows.append((int(r.get("Dispatch_Id") or r["Correlation_Id"]), int(r["End_Timestamp"]) - int(r["Start_Timestamp"]),
                          r["Kernel_Name"]))
     rows.sort()
     # the pre-warm cycle runs the same kernels on a 256^2 grid first: its launches are ~100x shorter
     big = [r for r in rows if r[1] > 50_000]
-    lo, cnt = win["gram_launch_offset"], win["gram_launches"]
     sel = big[lo:lo + cnt]
-    avg_ms = sum(d for _, d, _ in sel) / len(sel) / 1e6
-    print(json.dumps({"gram_launches": len(sel), "avg_launch_ms": avg_ms, "first": sel[0][2].split("(")[0],
-                      "bench_window": win}))
+    return {"launches": len(sel), "avg_launch_ms": sum(d for _, d, _ in sel) / len(sel) / 1e6,
+            "first": sel[0][2].split("(")[0]}
+
+
+def main(trace, window):
+    win = json.load(open(window))
+    g = window_avg(trace, GRAM, win["gram_launch_offset"], win["gram_launches"])
+    out = {"gram_launches": g["launches"], "avg_launch_ms": g["avg_launch_ms"], "first": g["first"]}
+    if "trial" in win:
+        t = win["trial"]
+        out["trial"] = window_avg(trace, TRIAL, t["trial_launch_offset"], t["trial_launches"])
+        win = {k: v for k, v in win.items() if k != "trial"} | {"trial": {k: v for k, v in t.items() if k != "launch_bytes"}}
+    out["bench_window"] = {k: v for k, v in win.items() if k != "launch_bytes"}
+    print(json.dumps(out))
 
 
 if __name__ == "__main__":
