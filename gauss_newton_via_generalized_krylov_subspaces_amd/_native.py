@@ -163,9 +163,22 @@ class HipBackend:
         self._chk(getattr(self.lib, name)(self.ctx, *args), name)
 
     def set_reduce_pairs(self, on: bool):
-        """Compensated reductions return unevaluated (s, c) pairs (gnk_set_reduce_pairs)."""
+        """Compensated reductions return unevaluated (s, c) pairs (gnk_set_reduce_pairs).  The
+        methods below that reduce take the mode per call (``pairs=``) and switch the context only
+        when it differs, so one backend can serve a pair-mode solver (Bratu GN / CGLS) and a plain one
+        (GNK, generic problems) in any order."""
         self._chk(self.lib.gnk_set_reduce_pairs(self.ctx, int(bool(on))), "set_reduce_pairs")
         self.pairs = bool(on)
+
+    def _mode(self, pairs, out, plain_len, pair_len, what):
+        """Set the context's reduction mode for one call and check the output buffer holds what that
+        mode writes (plain_len / pair_len doubles): a too-small buffer would be a device OOB write."""
+        need = pair_len if pairs else plain_len
+        if out is None or out.numel() < need:
+            raise ValueError(f"{what}: output buffer holds {0 if out is None else out.numel()} doubles, "
+                             f"{'pair' if pairs else 'plain'} mode writes {need}")
+        if bool(pairs) != self.pairs:
+            self.set_reduce_pairs(pairs)
 
     def set_tuning(self, key: str, value: int):
         """Kernel-choice override for tests / A/B tooling (gnk_set_tuning; 0 restores the default)."""
@@ -266,10 +279,12 @@ class HipBackend:
     def flat_cgs_update(self, V, k, h, g, stats):
         self._call("gnk_flat_cgs_update", _p(V), V.stride(0), int(k), _p(h), _p(g), g.numel(), _p(stats))
 
-    def flat_stats(self, x, stats):
+    def flat_stats(self, x, stats, pairs=False):
+        self._mode(pairs, stats, 2, 3, "flat_stats")
         self._call("gnk_flat_stats", _p(x), x.numel(), _p(stats))
 
-    def flat_dot(self, a, b, out):
+    def flat_dot(self, a, b, out, pairs=False):
+        self._mode(pairs, out, 1, 2, "flat_dot")
         self._call("gnk_flat_dot", _p(a), _p(b), a.numel(), _p(out))
 
     def flat_div(self, src, denom, dst):
@@ -278,7 +293,8 @@ class HipBackend:
     def flat_axpy(self, x, alpha, d, out):
         self._call("gnk_flat_axpy", _p(x), float(alpha), _p(d), _p(out), x.numel())
 
-    def flat_cg_update_xr(self, alpha, p, q, x, r, dinv, z, out):
+    def flat_cg_update_xr(self, alpha, p, q, x, r, dinv, z, out, pairs=False):
+        self._mode(pairs, out, 2, 4, "flat_cg_update_xr")
         self._call("gnk_flat_cg_update_xr", float(alpha), _p(p), _p(q), _p(x), _p(r), _p(dinv), _p(z), x.numel(),
                    _p(out))
 
@@ -296,7 +312,8 @@ class HipBackend:
     def cgs_update(self, V, k, h, g, stats):
         self._call("gnk_cgs_update", _p(V), V.stride(0), int(k), _p(h), _p(g), _p(stats))
 
-    def vec_stats(self, x, stats):
+    def vec_stats(self, x, stats, pairs=False):
+        self._mode(pairs, stats, 2, 3, "vec_stats")
         self._call("gnk_vec_stats", _p(x), _p(stats))
 
     def vec_div(self, src, denom, dst, full_slab):
@@ -337,14 +354,17 @@ class HipBackend:
         self._call("gnk_gram", _p(u), _p(V), V.stride(0), int(k), _p(rinv), kp, _p(r), _p(G))
 
     # --- CG ------------------------------------------------------------------------
-    def cg_matvec(self, d, p, q, pq):
+    def cg_matvec(self, d, p, q, pq, pairs=False):
+        self._mode(pairs, pq, 1, 2, "cg_matvec")
         self._call("gnk_cg_normal_matvec", _p(d), _p(p), _p(q), _p(pq))
 
-    def cg_step_matvec(self, d, z, p_in, p_out, q, beta, first, x, xalpha, pq):
+    def cg_step_matvec(self, d, z, p_in, p_out, q, beta, first, x, xalpha, pq, pairs=False):
+        self._mode(pairs, pq, 1, 2, "cg_step_matvec")
         self._call("gnk_cg_step_matvec", _p(d), _p(z), _p(p_in), _p(p_out), _p(q), float(beta), int(bool(first)),
                    _p(x), float(xalpha), _p(pq))
 
-    def cg_update_xr(self, alpha, p, q, x, r, dinv, z, out):
+    def cg_update_xr(self, alpha, p, q, x, r, dinv, z, out, pairs=False):
+        self._mode(pairs, out, 2, 4, "cg_update_xr")
         self._call("gnk_cg_update_xr", float(alpha), _p(p), _p(q), _p(x), _p(r), _p(dinv), _p(z), _p(out))
 
     def cg_update_p(self, beta, first, z, p):

@@ -68,13 +68,11 @@ class _DeviceTraces:
         self.s = self.dev.scalar(3)
 
     def error(self, x) -> float:
-        """||u_true - x|| (ref:bratu_pde_problem.py:98-99) over owned rows, summed in rank order (the
-        backend may be shared with a GN solver, whose context returns compensated pairs)."""
+        """||u_true - x|| (ref:bratu_pde_problem.py:98-99) over owned rows: the compensated sum of
+        squares as (s, c) pairs merged in rank order (the same value on any rank count)."""
         self.be.vec_axpy(x, -1.0, self.u_true, self.tmp, False)
-        self.be.vec_stats(self.tmp, self.s)
-        if getattr(self.be, "pairs", False):
-            return math.sqrt(self.comm.sum_pairs(self.s, 1)[0])
-        return math.sqrt(self.comm.sum_max(self.s[:2])[0])
+        self.be.vec_stats(self.tmp, self.s, pairs=True)
+        return math.sqrt(self.comm.sum_pairs(self.s, 1)[0])
 
     def sumsq_residual(self, x) -> float:
         self.be.residual(x, self.y, self.tmp, self.s[0:1])

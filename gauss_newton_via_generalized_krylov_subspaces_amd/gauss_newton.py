@@ -41,7 +41,7 @@ class BratuGNOps:
     the fused 13-point J^T J p stencil, the closed-form diag(J^T J), halos of p.
 
     The CG scalars (p.q, r.r, r.z) and the squared norms are compensated (Dot2) sums on the device;
-    this rank's context returns them as unevaluated (s, c) pairs (gnk_set_reduce_pairs) and the ranks'
+    this rank's context returns them as unevaluated (s, c) pairs (``pairs=True`` per call) and the ranks'
     pairs are merged with TwoSum in rank order (slab.Comm.sum_pairs) before rounding, so a multi-rank
     CG runs on the same exactly rounded scalars as a single rank (ref:gauss_newton.py:11-60)."""
 
@@ -53,7 +53,6 @@ class BratuGNOps:
         self.comm = self.dev.comm
         self.n_global = self.dev.slab.n_global
         self.y = None if y is None else self.dev.load(y)
-        self.be.set_reduce_pairs(True)
         self._n1 = self.dev.scalar(1)              # residual sum of squares (plain reduction)
         self._s1 = self.dev.scalar(2)              # one compensated pair
         self._s2 = self.dev.scalar(4)              # two compensated pairs
@@ -95,7 +94,7 @@ class BratuGNOps:
         self.be.vec_axpy(x, t, d, out, True)                         # x + t d (whole slab)
 
     def sumsq(self, v) -> float:
-        self.be.vec_stats(v, self._st)
+        self.be.vec_stats(v, self._st, pairs=True)
         return float(self.comm.sum_pairs(self._st, 1)[0])
 
     # CG pieces
@@ -111,11 +110,11 @@ class BratuGNOps:
     def cg_normal_matvec(self, p, q) -> float:
         sl = self.dev.slab
         self.comm.halo(p, sl.N, sl.nrows)
-        self.be.cg_matvec(self.dvec, p, q, self._s1)
+        self.be.cg_matvec(self.dvec, p, q, self._s1, pairs=True)
         return float(self.comm.sum_pairs(self._s1, 1)[0])
 
     def cg_update_xr(self, alpha, p, q, x, r, dinv, z):
-        self.be.cg_update_xr(alpha, p, q, x, r, dinv, z, self._s2)
+        self.be.cg_update_xr(alpha, p, q, x, r, dinv, z, self._s2, pairs=True)
         rr, rz = self.comm.sum_pairs(self._s2, 2)
         return float(rr), float(rz)
 
@@ -137,11 +136,11 @@ class BratuGNOps:
         self.comm.halo(z, sl.N, sl.nrows)
 
     def cg_step_matvec(self, z, p_in, p_out, q, beta, first, x, xalpha) -> float:
-        self.be.cg_step_matvec(self.dvec, z, p_in, p_out, q, beta, first, x, xalpha, self._s1)
+        self.be.cg_step_matvec(self.dvec, z, p_in, p_out, q, beta, first, x, xalpha, self._s1, pairs=True)
         return float(self.comm.sum_pairs(self._s1, 1)[0])
 
     def cg_update_rz(self, alpha, q, r, dinv, z):
-        self.be.cg_update_xr(alpha, None, q, None, r, dinv, z, self._s2)
+        self.be.cg_update_xr(alpha, None, q, None, r, dinv, z, self._s2, pairs=True)
         rr, rz = self.comm.sum_pairs(self._s2, 2)
         return float(rr), float(rz)
 
@@ -162,9 +161,9 @@ class BratuGNOps:
         if self.cg_fused:
             if getattr(self, "_sr_p", None) is None:
                 self._sr_p = self.dev.vec()
-            self.be.cg_step_matvec(self.dvec, u, u, self._sr_p, w, 0.0, True, None, 0.0, out)
+            self.be.cg_step_matvec(self.dvec, u, u, self._sr_p, w, 0.0, True, None, 0.0, out, pairs=True)
         else:
-            self.be.cg_matvec(self.dvec, u, w, out)
+            self.be.cg_matvec(self.dvec, u, w, out, pairs=True)
 
     def cg_sr_read(self, buf):
         parts = self.comm._gather(buf)                  # per rank [r.u, r.r, s(u.w), c(u.w)]

@@ -73,7 +73,6 @@ class BratuOps:
         self.comm = self.dev.comm
         self.n_global = self.dev.slab.n_global
         self.y = self.dev.load(y)
-        self.be.set_reduce_pairs(False)             # the GNK scalars are plain doubles (lls.py, krylow.py)
         self._n2 = self.dev.scalar(1)
 
     def vec(self):

@@ -25,6 +25,13 @@ class NumpyBackend:
         """gnk_set_reduce_pairs: compensated results as (s, c) pairs; the double's c is 0."""
         self.pairs = bool(on)
 
+    def _mode(self, pairs, out, plain_len, pair_len, what):
+        """As HipBackend._mode: the reduction mode per call, checked against the output's size."""
+        need = pair_len if pairs else plain_len
+        if out is None or out.numel() < need:
+            raise ValueError(f"{what}: output buffer too small for {'pair' if pairs else 'plain'} mode")
+        self.pairs = bool(pairs)
+
     def set_tuning(self, key, value):
         pass
 
@@ -251,12 +258,14 @@ class NumpyBackend:
         stats[0] = float(np.sum(G * G))
         stats[1] = float(np.max(np.abs(G)))
 
-    def flat_stats(self, x, stats):
+    def flat_stats(self, x, stats, pairs=False):
+        self._mode(pairs, stats, 2, 3, 'flat_stats')
         o = x.numpy()
         stats[0] = float(np.sum(o * o))
         stats[1] = float(np.max(np.abs(o)))
 
-    def flat_dot(self, a, b, out):
+    def flat_dot(self, a, b, out, pairs=False):
+        self._mode(pairs, out, 1, 2, 'flat_dot')
         out[0] = float(np.dot(a.numpy(), b.numpy()))
 
     def flat_div(self, src, denom, dst):
@@ -265,7 +274,8 @@ class NumpyBackend:
     def flat_axpy(self, x, alpha, d, out):
         out.numpy()[:] = x.numpy() + alpha * d.numpy()
 
-    def flat_cg_update_xr(self, alpha, p, q, x, r, dinv, z, out):
+    def flat_cg_update_xr(self, alpha, p, q, x, r, dinv, z, out, pairs=False):
+        self._mode(pairs, out, 2, 4, 'flat_cg_update_xr')
         X, R = x.numpy(), r.numpy()
         X[:] = X + alpha * p.numpy()
         R[:] = R - alpha * q.numpy()
@@ -328,7 +338,8 @@ class NumpyBackend:
         stats[0] = float(np.sum(o * o))
         stats[1] = float(np.max(np.abs(o))) if not np.isnan(o).any() else float("nan")
 
-    def vec_stats(self, x, stats):
+    def vec_stats(self, x, stats, pairs=False):
+        self._mode(pairs, stats, 2, 3, 'vec_stats')
         own = slice(GHOST * self.N, (GHOST + self.nrows) * self.N)
         o = x.numpy()[own]
         self._put(stats, [np.sum(o * o)], [np.max(np.abs(o))])
@@ -365,7 +376,8 @@ class NumpyBackend:
         G.numpy()[:kp * kp] = (W.T @ W).reshape(-1)
 
     # -- CG ------------------------------------------------------------------------------
-    def cg_matvec(self, d, p, q, pq):
+    def cg_matvec(self, d, p, q, pq, pairs=False):
+        self._mode(pairs, pq, 1, 2, 'cg_matvec')
         # t = J p on owned +-1 rows (inside the domain), then q = J^T t
         lo, hi = GHOST, GHOST + self.nrows
         P = self._m(p)
@@ -380,7 +392,8 @@ class NumpyBackend:
         own = slice(GHOST * self.N, (GHOST + self.nrows) * self.N)
         self._put(pq, [np.dot(p.numpy()[own], q.numpy()[own])])
 
-    def cg_step_matvec(self, d, z, p_in, p_out, q, beta, first, x, xalpha, pq):
+    def cg_step_matvec(self, d, z, p_in, p_out, q, beta, first, x, xalpha, pq, pairs=False):
+        self._mode(pairs, pq, 1, 2, 'cg_step_matvec')
         # p_out on every slab row (owned + ghost, as the kernel's boundary ranges), lagged x update
         own = slice(GHOST * self.N, (GHOST + self.nrows) * self.N)
         pi, pv, zv = p_in.numpy(), p_out.numpy(), z.numpy()
@@ -390,7 +403,8 @@ class NumpyBackend:
             xv[own] = xv[own] + xalpha * pi[own]
         self.cg_matvec(d, p_out, q, pq)
 
-    def cg_update_xr(self, alpha, p, q, x, r, dinv, z, out):
+    def cg_update_xr(self, alpha, p, q, x, r, dinv, z, out, pairs=False):
+        self._mode(pairs, out, 2, 4, 'cg_update_xr')
         own = slice(GHOST * self.N, (GHOST + self.nrows) * self.N)
         xv, rv = (x.numpy() if x is not None else None), r.numpy()
         if xv is not None:

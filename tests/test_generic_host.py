@@ -244,3 +244,44 @@ def check_graded_spectrum_gn(backend_kw):
 
 def test_graded_spectrum_dense_gn():
     check_graded_spectrum_gn(dict(_backend=NumpyBackend()))
+
+
+def test_shared_backend_across_pair_and_plain_solvers():
+    """one backend serves a Bratu GN (compensated reductions as (s, c) pairs) and generic
+    solvers (plain reductions) in any order -- the mode is set per call and checked against each
+    output buffer's size, so neither run writes past a buffer or reads the other's layout."""
+    be = NumpyBackend()
+    res, jac = O.rosenbrock(1000)
+    x0 = 2 * np.ones(1000)
+    prob, y, u0 = O.bratu_workload(24)
+
+    def bratu_gn(backend):
+        p = gnk.BratuPdeProblem(25, 5, 10)
+        with contextlib.redirect_stdout(io.StringIO()):
+            return gnk.gauss_newton(p.make_res(y), u0, p.make_jac(), max_iter=4, _backend=backend)
+
+    def generic(backend, method, **kw):
+        with contextlib.redirect_stdout(io.StringIO()):
+            return method(res, x0, jac, max_iter=6, _backend=backend, **kw)
+
+    ref_gn = bratu_gn(NumpyBackend())
+    ref_gen = generic(NumpyBackend(), gnk.gauss_newton)
+    ref_gnk = generic(NumpyBackend(), gnk.gauss_newton_krylow, version="res_old")
+    a = bratu_gn(be)
+    assert be.pairs                                       # the Bratu GN left the context in pair mode
+    b = generic(be, gnk.gauss_newton)
+    c = generic(be, gnk.gauss_newton_krylow, version="res_old")
+    d = bratu_gn(be)
+    for got, ref in ((a, ref_gn), (b, ref_gen), (c, ref_gnk), (d, ref_gn)):
+        assert (got.nit, got.nrev, got.njev) == (ref.nit, ref.nrev, ref.njev)
+        np.testing.assert_array_equal(got.x, ref.x)
+
+
+def test_reduction_buffer_checked_against_mode():
+    import torch
+    be = NumpyBackend()
+    x = torch.ones(8, dtype=torch.float64)
+    with pytest.raises(ValueError):
+        be.flat_stats(x, torch.zeros(2, dtype=torch.float64), pairs=True)     # pair mode writes 3
+    with pytest.raises(ValueError):
+        be.flat_dot(x, x, torch.zeros(1, dtype=torch.float64), pairs=True)   # pair mode writes 2
