@@ -237,6 +237,12 @@ class HostCallableOps:
     def vjp(self, u, w, out, negate=False):
         self._jac_of(u).rmatvec(w, out, negate)
 
+    def max_arena_k(self, with_r=True) -> int:
+        """The largest basis size ``gram`` accepts: kp = gram_dim(k, with_r) (k (+ r) rounded up to 16)
+        either <= 64 (MFMA tiles, no arena) or with kp * m <= scratch (the wide pass's Y)."""
+        kp_max = max(64, (self.be.scratch_doubles() // self.m) // 16 * 16)
+        return min(FLAT_GRAM_KMAX, kp_max - (1 if with_r else 0))
+
     def gram(self, u, V, k, rinv, r, G):
         """Gram of [J(u) V RinvAug | r]: k JVPs into a device W, then gnk_flat_gram."""
         if k > FLAT_GRAM_KMAX:
@@ -247,7 +253,7 @@ class HostCallableOps:
             # the wide pass materialises Y = W RinvAug (m x kp) in the library's scratch arena
             raise NotImplementedError(f"generic problems: a {k}-column basis over {self.m} residuals exceeds the "
                                       f"wide Gram's arena ({self.be.scratch_doubles()} doubles; use krylow_restart "
-                                      f"<= {max(1, self.be.scratch_doubles() // self.m - 1)})")
+                                      f"<= {self.max_arena_k(r is not None)})")
         if self._W is None or self._W.shape[0] < k:
             self._W = self.be.zeros(max(k, 8), self.m)
         J = self._jac_of(u)

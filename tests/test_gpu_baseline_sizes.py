@@ -74,9 +74,10 @@ def test_c2_full_run_vs_reference(version):
     m = n - 1 if last_tie else n
     assert rec["nfev"][:m] == ref["nfev"][:m]
     if last_tie:                   # the converged step's Armijo count is a rounding tie
-        lo, hi = T.last_nfev_range(f"c2_{version}")
-        print(f"C2 {version}: last step nfev {rec['nfev'][-1]} (reference {ref['nfev'][-1]}, its reorderings {lo}..{hi})")
-        assert lo <= rec["nfev"][-1] <= hi and out.nrev - rec["nfev"][-1] == case["nrev"] - ref["nfev"][-1]
+        seen = T.last_nfev_values(f"c2_{version}")
+        print(f"C2 {version}: last step nfev {rec['nfev'][-1]} (reference {ref['nfev'][-1]}, its reorderings {seen})")
+        # one of the counts the reference family itself produced (not just inside their range)
+        assert rec["nfev"][-1] in seen and out.nrev - rec["nfev"][-1] == case["nrev"] - ref["nfev"][-1]
     else:
         assert out.nrev == case["nrev"]
     tol = T.per_iteration(f"c2_{version}", n)

@@ -200,5 +200,13 @@ def test_generic_wide_gram_arena_guard():
 
     ops = HostCallableOps(lambda x: x, lambda x: np.eye(x.size), 4, backend=SmallArena())
     ops.m = 2000
-    with pytest.raises(NotImplementedError, match="krylow_restart"):
+    with pytest.raises(NotImplementedError, match="krylow_restart <= 63") as ei:
         ops.gram(None, None, 70, None, ops.be.zeros(2000), ops.be.zeros(96 * 96))
+    # the suggested bound is the real limit: kp = gram_dim(k, r) rounds k + 1 up to 16, and
+    # kp <= 64 needs no arena
+    kb = int(str(ei.value).rsplit("<= ", 1)[1].rstrip(")"))
+    assert ops.be.gram_dim(kb, True) <= 64
+    assert ops.be.gram_dim(kb + 1, True) * ops.m > ops.be.scratch_doubles()
+    ops.m = 500                                       # arena 80 000 / 500 -> kp 160: k <= 159
+    assert ops.max_arena_k(True) == 159
+    assert ops.be.gram_dim(159, True) * ops.m <= ops.be.scratch_doubles() < ops.be.gram_dim(160, True) * ops.m

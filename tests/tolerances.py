@@ -71,6 +71,12 @@ def last_nfev_range(case):
     """(min, max) of the last iteration's cumulative nfev over the recorded reordering variants of
     ``case`` (the reference's own arithmetic, reordered): the spread of a converged step's Armijo
     count, which is decided by rounding noise."""
-    v = sensitivity()[case]["variants"]
-    last = [int(x["nfev"][-1]) for x in v.values()]
+    last = last_nfev_values(case)
     return min(last), max(last)
+
+
+def last_nfev_values(case):
+    """The last iteration's cumulative nfev of every recorded reordering variant of ``case`` (sorted,
+    distinct): the counts the reference family actually produced, so drift inside the range shows."""
+    v = sensitivity()[case]["variants"]
+    return sorted({int(x["nfev"][-1]) for x in v.values()})
