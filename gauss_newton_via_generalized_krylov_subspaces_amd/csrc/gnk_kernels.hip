@@ -3747,7 +3747,8 @@ int gnk_gram(gnk_ctx* ctx, const double* u, const double* V, int64_t ldv, int k,
     const int64_t nrows = ctx->geo.nrows;
     // about 8 waves per CU, whole row ranges per strip
     int64_t nranges = std::max<int64_t>(1, std::min<int64_t>(nrows, int64_t(ctx->num_cus) * 8 / nstrips));
-    const int64_t rpr = (nrows + nranges - 1) / nranges;
+    const int rpr_t = tuning(ctx, GNK_TUNE_GRAM_RPR);
+    const int64_t rpr = rpr_t > 0 ? int64_t(rpr_t) : (nrows + nranges - 1) / nranges;
     nranges = (nrows + rpr - 1) / rpr;
     const int64_t nwaves = nstrips * nranges;
     const int64_t nblk = (nwaves + BLOCK / 64 - 1) / (BLOCK / 64);
@@ -3823,7 +3824,8 @@ int gnk_gram(gnk_ctx* ctx, const double* u, const double* V, int64_t ldv, int k,
       const int64_t nstrips = ctx->geo.N / GS_SW;
       const int64_t nrows = ctx->geo.nrows;
       int64_t nranges = std::max<int64_t>(1, std::min<int64_t>(nrows, int64_t(ctx->num_cus) * wgpc / nstrips));
-      const int64_t rpr = (nrows + nranges - 1) / nranges;
+      const int rpr_t = tuning(ctx, GNK_TUNE_GRAM_RPR);
+      const int64_t rpr = rpr_t > 0 ? int64_t(rpr_t) : (nrows + nranges - 1) / nranges;
       nranges = (nrows + rpr - 1) / rpr;
       const int64_t nwg = nstrips * nranges;
       if (nwg > (1 << 20) || size_t(nwg) * PL > SCRATCH_DOUBLES - size_t(PL))

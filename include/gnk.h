@@ -58,14 +58,17 @@ int gnk_set_reduce_pairs(gnk_ctx* ctx, int on);
  *   GNK_TUNE_CG_MATVEC   1 = the point-wise normal matvec instead of the row-marching one
  *   GNK_TUNE_VJPG_BLOCKS cap on the blocks of gnk_vjp_gemv_t
  *   GNK_TUNE_GRAM_WIDE   1 = never the prefetching wide Gram kernel, 2 = also for 2..3 column blocks,
- *                        3 = the pair-split kernel instead of the VGPR-RinvAug one for 5..7 blocks */
+ *                        3 = the pair-split kernel instead of the VGPR-RinvAug one for 5..7 blocks
+ *   GNK_TUNE_GRAM_RPR    > 0: grid rows per row range of the staged / VALU Gram kernels (a finer,
+ *                        fixed decomposition; A/B of what rank-count-independent partials cost) */
 #define GNK_TUNE_GRAM_PATH 0
 #define GNK_TUNE_GRAM_RING 1
 #define GNK_TUNE_GRAM_V1MIN 2
 #define GNK_TUNE_CG_MATVEC 3
 #define GNK_TUNE_VJPG_BLOCKS 4
 #define GNK_TUNE_GRAM_WIDE 5
-#define GNK_TUNE_COUNT 6
+#define GNK_TUNE_GRAM_RPR 6
+#define GNK_TUNE_COUNT 7
 int gnk_set_tuning(gnk_ctx* ctx, int key, int value);
 /* doubles in the context's scratch arena (bounds the wide generic Gram: kp * m <= this) */
 int64_t gnk_scratch_doubles(void);

@@ -74,10 +74,14 @@ def test_c2_full_run_vs_reference(version):
     m = n - 1 if last_tie else n
     assert rec["nfev"][:m] == ref["nfev"][:m]
     if last_tie:                   # the converged step's Armijo count is a rounding tie
+        lo, hi = T.last_nfev_range(f"c2_{version}")
         seen = T.last_nfev_values(f"c2_{version}")
-        print(f"C2 {version}: last step nfev {rec['nfev'][-1]} (reference {ref['nfev'][-1]}, its reorderings {seen})")
-        # one of the counts the reference family itself produced (not just inside their range)
-        assert rec["nfev"][-1] in seen and out.nrev - rec["nfev"][-1] == case["nrev"] - ref["nfev"][-1]
+        tracked = T.DEVICE_LAST_NFEV[f"c2_{version}"]
+        print(f"C2 {version}: last step nfev {rec['nfev'][-1]} (reference {ref['nfev'][-1]}, its reorderings {seen}; "
+              f"tracked device value {tracked})")
+        assert lo <= rec["nfev"][-1] <= hi and out.nrev - rec["nfev"][-1] == case["nrev"] - ref["nfev"][-1]
+        # drift inside the band must show -- the device's own count is tracked
+        assert rec["nfev"][-1] == tracked, "the converged step's Armijo count moved inside the band: re-check, update"
     else:
         assert out.nrev == case["nrev"]
     tol = T.per_iteration(f"c2_{version}", n)
