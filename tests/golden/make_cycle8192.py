@@ -16,10 +16,19 @@ process's anonymous memory stays ~ 25 GB -- at k = 17 an all-anonymous run reach
   base      the oracle's arithmetic (numpy dot products, LAPACK Householder QR);
   exact_k1  the one-column steps (k = 1) with exactly rounded sums (math.fsum) -- the cancellation-
             limited step the device's compensated k = 1 path computes (tests/golden/make_sensitivity.py).
+  cholqr    the device's least-squares arithmetic (lls.CholQR2Solver._passes) instead of Householder:
+            the exact k = 1 step, then for k >= 2 preconditioned CholeskyQR -- P = blockdiag(R_prev, 1),
+            Y = (J V) P^-1 (fp64 BLAS), the Gram of [Y | r] in extended precision (x87 80-bit products
+            and sums over 64 Ki-row chunks, the chunk sums kept as double-double pairs and added exactly
+            by math.fsum: ~1e-19 relative, orders below an fp64 Gram), the new column rescaled by
+            sqrt(G_kk), another pass with P = R_Y P while cond(R_Y) > 30, R = R_Y P, d = -R^-1 R_Y^-T Y^T r,
+            and Armijo's jdd = ||R d||^2 (the device's).  Everything else -- the basis update, the
+            trials -- is the base arithmetic, so |cholqr - base| is the move of the reference's
+            trajectory under an equally valid factorisation, and |device - cholqr| what is left.
 The GPU test (tests/test_gpu_baseline_sizes.py) asserts base within max(1e-10, |exact_k1 - base|,
 the head8192 envelope), and the bookkeeping exactly.
 
-Usage:  python tests/golden/make_cycle8192.py [base|exact_k1 ...]   (merges into large_cycle8192.json)
+Usage:  python tests/golden/make_cycle8192.py [base|exact_k1|cholqr ...]   (merges into large_cycle8192.json)
 """
 import contextlib
 import io
@@ -99,6 +108,98 @@ def lls_inplace(A, y, exact_k1):
     return scipy.linalg.solve_triangular(r, q.T @ y)
 
 
+def _gram_ext(Y, r):
+    """[Y | r]^T [Y | r] (F-order Y, n x k) with x87 80-bit products / sums per 64 Ki-row chunk, the
+    chunk sums split into double-double (hi, lo) and summed exactly (math.fsum), rounded once."""
+    n, k = Y.shape
+    CH = 1 << 16
+    m = k + 1
+    parts = [[[] for _ in range(m)] for _ in range(m)]
+    Z = np.empty((CH, m), dtype=np.longdouble, order="F")
+    for lo in range(0, n, CH):
+        hi = min(n, lo + CH)
+        L = hi - lo
+        for j in range(k):
+            Z[:L, j] = Y[lo:hi, j]
+        Z[:L, k] = r[lo:hi]
+        for i in range(m):
+            zi = Z[:L, i]
+            for j in range(i, m):
+                sv = np.dot(zi, Z[:L, j])
+                h = float(sv)
+                parts[i][j] += [h, float(sv - np.longdouble(h))]
+    G = np.empty((m, m))
+    for i in range(m):
+        for j in range(i, m):
+            G[i, j] = G[j, i] = math.fsum(parts[i][j])
+    return G
+
+
+class CholQRLS:
+    """lls.CholQR2Solver._passes (host form) on the fp64 J V of the reference basis."""
+    COND_ACCEPT = 30.0
+
+    def __init__(self):
+        self.R_prev = None
+        self.passes = []
+
+    def restart(self):
+        self.R_prev = None
+
+    def solve(self, JV, Ybuf, r):
+        import scipy.linalg as sl
+        k = JV.shape[1]
+        if k == 1 or self.R_prev is None:
+            a = JV[:, 0] if k == 1 else None
+            if k != 1:
+                raise RuntimeError("no preconditioner at k > 1: not the bench trajectory")
+            # the exact k = 1 step (the device's compensated one-column pass): G = [||Jv||^2, Jv.r]
+            g00 = math.fsum(a * a)
+            g01 = math.fsum(a * r)
+            s = math.sqrt(g00)
+            R = np.array([[s]])
+            d = np.array([-(g01 / s) / s])
+            self.R_prev = R
+            self.passes.append((k, 1, [1.0]))
+            return d, R
+        P = np.zeros((k, k))
+        P[:k - 1, :k - 1] = self.R_prev
+        P[k - 1, k - 1] = 1.0
+        conds = []
+        for it in range(4):
+            T = sl.solve_triangular(P, np.eye(k), lower=False)
+            Y = Ybuf[:, :k]
+            np.matmul(JV, T, out=Y)
+            G = _gram_ext(Y, r)
+            if it == 0:
+                s = math.sqrt(G[k - 1, k - 1])
+                G[k - 1, :] /= s
+                G[:, k - 1] /= s
+                P[k - 1, k - 1] = s
+            Ry = sl.cholesky(G[:k, :k], lower=False)
+            sv = np.linalg.svd(Ry, compute_uv=False)
+            conds.append(float(sv[0] / sv[-1]))
+            if conds[-1] <= self.COND_ACCEPT or it == 3:
+                z = sl.solve_triangular(Ry, G[:k, k], trans="T", lower=False)
+                R = Ry @ P
+                break
+            P = Ry @ P
+        d = -sl.solve_triangular(R, z, lower=False)
+        self.R_prev = R                       # the next step's preconditioner (blockdiag(R, scale))
+        self.passes.append((k, len(conds), conds))
+        return d, R
+
+
+class _Rd:
+    """Armijo's jac_ev @ d with the device's jdd = ||R d||^2 (lls.py)."""
+
+    def __init__(self, R):
+        self.R = R
+
+    def __matmul__(self, d):
+        return self.R @ d
+
+
 class _JVd:
     def __init__(self, JV):
         self.JV = JV
@@ -109,6 +210,7 @@ class _JVd:
 
 def run(variant):
     exact_k1 = variant == "exact_k1"
+    chol = CholQRLS() if variant == "cholqr" else None
     prob, y, u0 = O.bratu_workload(N)
     res = prob.make_res(y)
     jac = prob.make_jac()
@@ -128,10 +230,16 @@ def run(variant):
         JV, A = JVbuf[:, :k], Abuf[:, :k]
         for j in range(k):
             JV[:, j] = J @ kr.buf[:, j]
-            np.multiply(JV[:, j], -1, out=A[:, j])
+            if chol is None:
+                np.multiply(JV[:, j], -1, out=A[:, j])
         r_old = res_new
-        d = lls_inplace(A, r_old, exact_k1)
-        t, res_new, dn = O.armijo_goldstein(lambda cc: res(kr.x(cc)), c, r_old, _JVd(JV), (), d)
+        if chol is None:
+            d = lls_inplace(A, r_old, exact_k1)
+            jv = _JVd(JV)
+        else:
+            d, R = chol.solve(JV, Abuf, r_old)
+            jv = _Rd(R)
+        t, res_new, dn = O.armijo_goldstein(lambda cc: res(kr.x(cc)), c, r_old, jv, (), d)
         nfev += dn
         s = np.sum(c ** 2)
         c += t * d
@@ -152,7 +260,11 @@ def run(variant):
             print(f"Generalized krylow subspace breakdown at iteration = {it}, basis.shape = {kr.basis.shape}")
         if it % RESTART == 0:
             c = kr.start(kr.x(c))
+            if chol is not None:
+                chol.restart()
     rec["seconds"] = time.time() - t0
+    if chol is not None:
+        rec["ls_passes"] = chol.passes
     return rec
 
 
