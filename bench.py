@@ -51,6 +51,8 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=20.0, help="CPU oracle sample budget (0 = skip)")
     ap.add_argument("--jvp-reps", type=int, default=20)
     ap.add_argument("--cg-iters", type=int, default=200, help="CGLS iterations of the C3 line (0 = skip)")
+    ap.add_argument("--segments", choices=("auto", "on", "off"), default="auto",
+                    help="rank-count-independent reductions (slab.reduction_segments): auto = on for N > 1")
     return ap.parse_args()
 
 
@@ -345,7 +347,7 @@ def main():
 
     N = args.grid
     n = N * N
-    comm = Comm()
+    comm = Comm(segments={"auto": None, "on": True, "off": False}[args.segments])
     prewarm(args, comm, device)
     prob = gnk.BratuPdeProblem(N + 1, 5, 10)
     # this rank's slabs of u0 and y = F(u_true) (ref:bratu_pde_test.py:22-36), built per rank: no
@@ -378,6 +380,7 @@ def main():
     k_trace0 = len(solver.trace)
     passes0 = solver.lls.passes
     regions, launches, tlaunches = [], [], []
+    comm0 = dict(comm.counters)
     for _ in range(args.repeats):
         be.timer_start(_native.TIMER_GRAM, cap)
         be.timer_add(_native.TIMER_TRIAL)
@@ -400,6 +403,8 @@ def main():
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             el = t.item()
         regions.append((len(solver.trace) - tr0, el))
+    comm_steps = max(1, sum(st for st, _ in regions))
+    comm_per_step = {key: (comm.counters[key] - comm0[key]) / comm_steps for key in comm0}
     rates = [st / el for st, el in regions]
     imed = int(np.argsort(rates)[len(rates) // 2])
     steps_done, elapsed = regions[imed]
@@ -503,7 +508,8 @@ def main():
                    "basis_k_range": [min(s["k"] for s in tr), max(s["k"] for s in tr)] if tr else None,
                    "armijo_trials": int(sum(s["trials"] for s in tr)),
                    "parallelism": f"slab{world}",
-                   "transport": (dist.get_backend() if world > 1 else "none")},
+                   "transport": (dist.get_backend() if world > 1 else "none"),
+                   "reduction_segments": int(getattr(solver.dev, "seg_rows", 0))},
         "roofline": {"kernel": "Gram pass of the CholeskyQR solve, J V T on the fly (k_gram_v: VALU, k <= 9; "
                                "k_gram_s: staged fp64 MFMA, k > 9)", "bound": "hbm",
                      "achieved": g_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": g_gbs / HBM_PEAK_GBS,
@@ -530,6 +536,7 @@ def main():
         "repeats": [{"steps": st, "seconds": el, "outer_iters_per_s": st / el} for st, el in regions],
         "step_algorithmic_GBs": total_bytes / elapsed_all / 1e9,
         "gram_passes_per_step": ppi,
+        "comm_per_step": comm_per_step,
         "speculated_solves": spec_stats,
     }
     if cg_line is not None:

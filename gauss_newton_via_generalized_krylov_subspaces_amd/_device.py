@@ -4,7 +4,7 @@ from __future__ import annotations
 import torch
 
 from ._native import HipBackend
-from .slab import Comm, Slab
+from .slab import Comm, Slab, reduction_segments
 
 
 def default_device():
@@ -30,6 +30,10 @@ class BratuDevice:
                                problem.ALPHA, problem.LAMBDA)
         if self.backend.slab_len() != self.slab.length:
             raise RuntimeError("slab length mismatch between host and libgnk")
+        # rank-count-independent reductions (slab.reduction_segments; on by default for several ranks)
+        self.seg_rows = reduction_segments(problem.N, self.comm.world, getattr(self.comm, "segments", None))
+        if hasattr(self.backend, "set_segments"):
+            self.backend.set_segments(self.seg_rows)
         if self.comm.world > 1 and not self.comm.stage and hasattr(self.backend, "rank_sum"):
             self.comm.device_rank_sum = self.backend.rank_sum
 

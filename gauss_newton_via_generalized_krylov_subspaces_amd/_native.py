@@ -19,7 +19,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("GNK_LIB", os.path.join(_HERE, "libgnk.so"))
 GHOST = 2  # GNK_GHOST_ROWS
 TIMER_GRAM, TIMER_JVP, TIMER_CG_MATVEC, TIMER_TRIAL, TIMER_PROBE = 1, 2, 3, 4, 5  # GNK_TIMER_*
-ABI_VERSION = 4  # GNK_ABI_VERSION
+ABI_VERSION = 5  # GNK_ABI_VERSION
 # GNK_TUNE_* keys of gnk_set_tuning (tests / A/B tooling only; the solver never sets them)
 TUNE = {"gram_path": 0, "gram_ring": 1, "gram_v1min": 2, "cg_matvec": 3, "vjpg_blocks": 4, "gram_wide": 5, "gram_rpr": 6}
 
@@ -33,6 +33,7 @@ SIGNATURES = {
     "gnk_last_error": (ctypes.c_char_p, [_c_vp]),
     "gnk_set_stream": (_c_int, [_c_vp, _c_vp]),
     "gnk_set_reduce_pairs": (_c_int, [_c_vp, _c_int]),
+    "gnk_set_segments": (_c_int, [_c_vp, _c_i64]),
     "gnk_set_tuning": (_c_int, [_c_vp, _c_int, _c_int]),
     "gnk_scratch_doubles": (_c_i64, []),
     "gnk_set_bratu": (_c_int, [_c_vp, _c_i64, _c_i64, _c_i64, _c_dbl, _c_dbl, _c_dbl]),
@@ -191,6 +192,12 @@ class HipBackend:
     def set_bratu(self, N, row0, nrows, h, alpha, lam):
         self._chk(self.lib.gnk_set_bratu(self.ctx, N, row0, nrows, float(h), float(alpha), float(lam)), "set_bratu")
 
+    def set_segments(self, seg_rows: int):
+        """Rank-count-independent reductions over fixed global row segments of ``seg_rows`` rows
+        (gnk_set_segments; 0 = off).  Call after set_bratu, which resets it."""
+        self._chk(self.lib.gnk_set_segments(self.ctx, int(seg_rows)), "set_segments")
+        self.seg_rows = int(seg_rows)
+
     def slab_len(self):
         return int(self.lib.gnk_slab_len(self.ctx))
 
@@ -330,7 +337,8 @@ class HipBackend:
                    _p(dinv), _p(u), _p(out))
 
     def rank_sum(self, parts, world, out):
-        """out = rank-ordered sum of parts (world x n, contiguous) on the device, one launch."""
+        """out = the ranks' parts (world x n, contiguous) summed on the device in slab.tree_sum's order
+        (pairwise, fixed), one launch."""
         n = out.numel()
         self._call("gnk_rank_sum", _p(parts), int(world), int(n), _p(out))
         return out

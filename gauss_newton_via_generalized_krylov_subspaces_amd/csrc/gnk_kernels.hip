@@ -215,6 +215,27 @@ struct RowLaunch {
 
 #define ROW_LOOP_END }}
 
+// Row loop of the persistent reduction kernels with segments (gnk_set_segments): grid.z = nseg + 1 slices,
+// slice z < nseg the owned rows of segment z (block row y taking rows y, y + gridDim.y, .. counted from the
+// segment's first row: a block's rows in a segment do not depend on where the slab starts), slice nseg the
+// rest of [lr0, lr0 + nlr) (ghost rows, no partial contributions).  seg == 0: one slice, [lr0, lr0 + nlr) as
+// ROW_LOOP.  One loop around one copy of the body, as ROW_LOOP (a loop over segments with a partial store
+// per segment in the kernel raised the trial kernel's VGPRs to 256).
+#define ZSEG_ROW_LOOP_BEGIN(VEC)                                                                        \
+  const int64_t N = geo.N;                                                                             \
+  const int zs = blockIdx.z;                                                                           \
+  const bool ghost_slice = seg > 0 && zs == nseg;                                                      \
+  const int64_t gbelow = max(int64_t(0), G - lr0);             /* ghost rows before the owned ones */  \
+  const int64_t za = seg == 0 ? lr0 : (ghost_slice ? lr0 : G + int64_t(zs) * seg);                     \
+  const int64_t zcnt = seg == 0 ? nlr : (ghost_slice ? nlr - geo.nrows : seg);                         \
+  for (int64_t t = blockIdx.y; t < zcnt; t += gridDim.y) {                                             \
+    const int64_t lr = (ghost_slice && t >= gbelow) ? G + geo.nrows + (t - gbelow) : za + t;           \
+    for (int64_t iy = (int64_t(blockIdx.x) * BLOCK + threadIdx.x) * (VEC); iy < N;                     \
+         iy += int64_t(gridDim.x) * BLOCK * (VEC)) {                                                   \
+      const int64_t li = lr * N + iy;
+
+#define ZSEG_ROW_LOOP_END }}
+
 // ---------------------------------------------------------------- operator kernels
 template <int VEC>
 __global__ __launch_bounds__(BLOCK) void k_jvp(const double* __restrict__ u, const double* __restrict__ v,
@@ -520,10 +541,11 @@ template <int VEC>
 __global__ __launch_bounds__(BLOCK) void k_gemv_p(const double* __restrict__ V, int64_t ldv, int k,
                                                   const double* __restrict__ cvec, const double* __restrict__ hh,
                                                   double* __restrict__ w, double* __restrict__ x, Geo geo,
-                                                  int64_t lr0, int64_t nlr, double* __restrict__ partial) {
+                                                  int64_t lr0, int64_t nlr, double* __restrict__ partial,
+                                                  int64_t seg, int nseg) {
   double ss = 0.0, mx = 0.0;
   const double ck = cvec[k];
-  ROW_LOOP_BEGIN(VEC)
+  ZSEG_ROW_LOOP_BEGIN(VEC)
   const bool owned = lr >= G && lr < G + geo.nrows;       // block-uniform
   if (VEC == 2 && iy + 1 < N) {
     d2 acc = {0.0, 0.0}, s = {0.0, 0.0};
@@ -565,8 +587,8 @@ __global__ __launch_bounds__(BLOCK) void k_gemv_p(const double* __restrict__ V, 
       }
     }
   }
-  ROW_LOOP_END
-  block_sum_max_store(ss, mx, partial);
+  ZSEG_ROW_LOOP_END
+  block_sum_max_store(ss, mx, partial + 2 * size_t(blockIdx.z) * gridDim.x * gridDim.y);
 }
 
 // g = -(J^T r) on owned rows (chunk 0 stores it), h[j0 + j] partial = V_j . g.
@@ -644,7 +666,7 @@ __global__ __launch_bounds__(BLOCK) void k_gemv_vjpg(const double* __restrict__ 
                                                      double* __restrict__ wcol, const double* __restrict__ r,
                                                      double* __restrict__ x, double* __restrict__ g, Geo geo, Coef c,
                                                      int64_t lr0, int64_t nlr, double* __restrict__ partial,
-                                                     double* __restrict__ spart) {
+                                                     double* __restrict__ spart, int64_t seg, int nseg) {
   __shared__ double sh[(BLOCK / 64) * KCT];
   __shared__ __attribute__((aligned(16))) double cl[2 * KCT];   // [c_0 .. c_{KCT-1} | hh_0 .. hh_{KCT-1}]
   const int lane = threadIdx.x & 63;
@@ -659,7 +681,7 @@ __global__ __launch_bounds__(BLOCK) void k_gemv_vjpg(const double* __restrict__ 
 #pragma unroll
   for (int j = 0; j < KCT; ++j) acc[j] = 0.0;
   double ss = 0.0, mx = 0.0;
-  ROW_LOOP_BEGIN(VEC)
+  ZSEG_ROW_LOOP_BEGIN(VEC)
   const bool owned = lr >= G && lr < G + geo.nrows;       // block-uniform
   if (VEC == 2 && iy + 1 < N) {
     // column j of this grid row: a wave-uniform base (SGPRs) + this lane's 32-bit byte offset
@@ -758,9 +780,11 @@ __global__ __launch_bounds__(BLOCK) void k_gemv_vjpg(const double* __restrict__ 
       }
     }
   }
-  ROW_LOOP_END
-  block_sum_store<KCT>(acc, kk, partial + size_t(blockIdx.y * gridDim.x + blockIdx.x) * KCT, sh);
-  if (PEND) block_sum_max_store(ss, mx, spart);
+  ZSEG_ROW_LOOP_END
+  // slice z's partials at z * nblk + blk (segments; z = 0 otherwise)
+  const size_t zb = size_t(blockIdx.z) * gridDim.x * gridDim.y;
+  block_sum_store<KCT>(acc, kk, partial + (zb + size_t(blockIdx.y) * gridDim.x + blockIdx.x) * KCT, sh);
+  if (PEND) block_sum_max_store(ss, mx, spart + 2 * zb);
 }
 
 // g -= V[:, :k] @ h ; partial {sum g^2, max|g|}
@@ -1149,13 +1173,31 @@ __global__ __launch_bounds__(BLOCK) void k_cg_p(double beta, int first, const do
 }
 
 // ---------------------------------------------------------------- deterministic partial reduction
-// rank-ordered sum of all-gathered per-rank partials: out[j] = ((p_0[j] + p_1[j]) + p_2[j]) + ...,
-// the host's order (slab.Comm), in one launch instead of world - 1 elementwise adds
+// sum of all-gathered per-rank partials in the fixed pairwise order of the host (slab.tree_sum) and of
+// gnk_set_segments' segment fold: the ranks' values are merged like a binary counter (a new value of
+// size 1 merges with the top of the stack while their sizes match, each merge (left) + (right)), then the
+// stack folds right to left -- equal to the bottom-up pairwise order v[i] += v[i + w], w = 1, 2, 4, ..
+// One launch instead of world - 1 elementwise adds.
 __global__ __launch_bounds__(BLOCK) void k_rank_sum(const double* __restrict__ parts, int world, int64_t n,
                                                     double* __restrict__ out) {
   for (int64_t j = int64_t(blockIdx.x) * BLOCK + threadIdx.x; j < n; j += int64_t(gridDim.x) * BLOCK) {
-    double s = parts[j];
-    for (int p = 1; p < world; ++p) s = s + parts[int64_t(p) * n + j];
+    double sv[32];
+    int sz[32];
+    int top = 0;
+    for (int p = 0; p < world; ++p) {
+      double v = parts[int64_t(p) * n + j];
+      int z = 1;
+      while (top > 0 && sz[top - 1] == z) {
+        v = sv[top - 1] + v;
+        z *= 2;
+        --top;
+      }
+      sv[top] = v;
+      sz[top] = z;
+      ++top;
+    }
+    double s = sv[--top];
+    while (top > 0) s = sv[--top] + s;
     out[j] = s;
   }
 }
@@ -1164,13 +1206,28 @@ __global__ __launch_bounds__(BLOCK) void k_rank_sum(const double* __restrict__ p
 // Output j reads partial[base(j) + b * sb] for b in [split * span, min(nblk, (split+1) * span)),
 // base(j) = (j / cw) * cs + (j % cw).  Lane l folds b = l, l + 64, ... with 8 independent
 // (clamped, branch-free) loads in flight, then a fixed xor-tree.  out[j * nsplit + split].
+// segblk > 0 (segment reductions, gnk_set_segments): the blocks come in segments of segblk and no
+// split crosses a segment -- split q covers blocks seg * segblk + sub * span .. of segment seg = q / nsps,
+// sub = q % nsps (nsps = ceil(segblk / span) splits per segment).
+__device__ __forceinline__ void seg_split_range(int split, int span, int nblk, int segblk, int& b0, int& b1) {
+  if (segblk > 0) {
+    const int nsps = (segblk + span - 1) / span, sg = split / nsps, sub = split % nsps;
+    b0 = sg * segblk + sub * span;
+    b1 = min(b0 + span, (sg + 1) * segblk);
+  } else {
+    b0 = split * span;
+    b1 = min(nblk, b0 + span);
+  }
+}
+
 __global__ __launch_bounds__(64) void k_wave_reduce(const double* __restrict__ partial, int nblk, int span, int64_t sb,
                                                     int cw, int64_t cs, const int* __restrict__ is_max,
-                                                    double* __restrict__ out) {
+                                                    double* __restrict__ out, int segblk = 0) {
   const int j = blockIdx.x, split = blockIdx.y, nsplit = gridDim.y, lane = threadIdx.x;
   const bool mx = is_max ? is_max[j] != 0 : false;
   const double* src = partial + int64_t(j / cw) * cs + (j % cw);
-  const int b0 = split * span, b1 = min(nblk, b0 + span);
+  int b0, b1;
+  seg_split_range(split, span, nblk, segblk, b0, b1);
   double s = mx ? -1.0 : 0.0;    // identity (max is taken over |x| >= 0)
   for (int b = b0 + lane; b < b1; b += 64 * 8) {
     double v[8];
@@ -1192,10 +1249,11 @@ __global__ __launch_bounds__(64) void k_wave_reduce(const double* __restrict__ p
 // [split * span, min(nblk, (split+1) * span)) with comp_merge in a fixed order; final != 0 writes
 // s + c to out[j * nsplit + split], else the pair to out[2 (j * nsplit + split) + {0, 1}].
 __global__ __launch_bounds__(64) void k_wave_reduce2(const double* __restrict__ partial, int nblk, int span, int64_t sb,
-                                                     int64_t cs, int final, double* __restrict__ out) {
+                                                     int64_t cs, int final, double* __restrict__ out, int segblk = 0) {
   const int j = blockIdx.x, split = blockIdx.y, nsplit = gridDim.y, lane = threadIdx.x;
   const double* src = partial + int64_t(j) * cs;
-  const int b0 = split * span, b1 = min(nblk, b0 + span);
+  int b0, b1;
+  seg_split_range(split, span, nblk, segblk, b0, b1);
   double s = 0.0, c = 0.0;
   for (int b = b0 + lane; b < b1; b += 64) comp_merge(s, c, src[int64_t(b) * sb], src[int64_t(b) * sb + 1]);
   wave_sum2(s, c);
@@ -1204,6 +1262,25 @@ __global__ __launch_bounds__(64) void k_wave_reduce2(const double* __restrict__ 
     if (final) out[o] = s + c;
     else { out[2 * o] = s; out[2 * o + 1] = c; }
   }
+}
+
+// Segment values -> one value per output, in the fixed pairwise order of gnk.h's gnk_set_segments
+// (bottom-up: v[i] += v[i + w] for w = 1, 2, 4, ..., i a multiple of 2w with i + w < n): for a power-of-two
+// n this is the balanced binary tree, so a rank holding segments [a, a + n / w) of n folds them into the
+// subtree value slab.Comm's rank combine expects.  in[j * nseg + s] -> out[j]; is_max[j]: NaN-propagating max.
+constexpr int SEG_MAX = 64;
+__device__ __forceinline__ double seg_tree_fold(double (&v)[SEG_MAX], int n, bool mx) {
+  for (int w = 1; w < n; w *= 2)
+    for (int i = 0; i + w < n; i += 2 * w) v[i] = mx ? nan_max(v[i], v[i + w]) : v[i] + v[i + w];
+  return v[0];
+}
+__global__ __launch_bounds__(64) void k_seg_fold(const double* __restrict__ in, int nseg, int len,
+                                                 const int* __restrict__ is_max, double* __restrict__ out) {
+  const int j = blockIdx.x * 64 + threadIdx.x;
+  if (j >= len) return;
+  double v[SEG_MAX];
+  for (int sgi = 0; sgi < nseg; ++sgi) v[sgi] = in[int64_t(j) * nseg + sgi];
+  out[j] = seg_tree_fold(v, nseg, is_max ? is_max[j] != 0 : false);
 }
 
 // out[j] = sum over b of partial[b * stride + j] (mode is_max[j]: NaN-propagating max).
@@ -2225,7 +2302,7 @@ template <int NB, int L, int KSL, int TAIL, int R, int WPE>
 __global__ __launch_bounds__(64 * GS_NW) __attribute__((amdgpu_waves_per_eu(WPE))) void k_gram_s(const double* __restrict__ u, const double* __restrict__ V,
                                                        int64_t ldv, int k, const double* __restrict__ rinv,
                                                        int ldr, const double* __restrict__ r, Geo geo, Coef cf,
-                                                       int64_t rpr, double* __restrict__ partial) {
+                                                       int64_t rpr, double* __restrict__ partial, int plog) {
   constexpr int NACC = gs_nacc(NB, KSL);
   constexpr int TMAX = NB == 2 ? 4 * KSL : 0;             // tail accumulator slots of this instance
   constexpr int ER = NB * TMAX, RR = ER + NB;             // accumulator slots of r . Y and r . r
@@ -2500,8 +2577,24 @@ __global__ __launch_bounds__(64 * GS_NW) __attribute__((amdgpu_waves_per_eu(WPE)
     }
     __syncthreads();
   }
-  double* out = partial + size_t(blockIdx.x) * PL;
-  for (int t = tid; t < PL; t += blockDim.x) out[t] = red[t];
+  double* out = partial + size_t(plog ? idx : b) * PL;     // plog (segments): the logical tile's slot
+  if (!plog) {
+    for (int t = tid; t < PL; t += blockDim.x) out[t] = red[t];
+    return;
+  }
+  // segments: the scatter's sum over the four lane groups (k_gram_scatter_s, lsum: ((g0 + g1) + g2) + g3)
+  // happens here, per workgroup, before any reduction over workgroups, segments or ranks -- summed after
+  // them it would not commute with the rank combine.  Group 0's slot gets the sum, groups 1..3 zeros
+  // (the scatter's sum then returns it unchanged)
+  for (int t = tid; t < PL; t += blockDim.x) {
+    if (t < 256) {
+      out[t] = red[t];
+    } else {
+      const int ln = (t - 256) / NACC, q = (t - 256) % NACC, col = ln & 15;
+      const double* e = red + 256 + q;
+      out[t] = (ln >> 4) ? 0.0 : ((e[col * NACC] + e[(16 + col) * NACC]) + e[(32 + col) * NACC]) + e[(48 + col) * NACC];
+    }
+  }
 }
 
 // ---------------------------------------------------------------- VALU Gram pass (k <= 8, with r)
@@ -3193,6 +3286,9 @@ struct gnk_ctx {
   std::string err;
   // gnk_set_reduce_pairs: compensated reductions written as unevaluated (s, c) pairs
   int pairs = 0;
+  // gnk_set_segments: reduction segment rows (0: off) and this slab's segment count
+  int64_t seg = 0;
+  int nseg = 1;
   // gnk_set_tuning (tooling A/B of kernel choices; 0 = the product's choice)
   int tune[GNK_TUNE_COUNT] = {};
   // per-launch timer (tooling, see gnk_timer_start)
@@ -3266,6 +3362,21 @@ bool rows2(const gnk_ctx* ctx, RowLaunch& L) {
 
 int64_t owned_lr0() { return G; }
 
+// Segment reductions (gnk_set_segments) over one-row-per-block launches: a row launch whose partials are
+// one block row per grid row (grid.y == nlr), so the partials of owned row m sit at (G - lr0 + m) * grid.x
+// and a segment's rows are seg * grid.x consecutive blocks whatever the slab.  cap for rows().
+int seg_row_cap(const gnk_ctx* ctx, int cap = MAX_RED_BLOCKS) { return ctx->seg > 0 ? (1 << 30) : cap; }
+
+// Rows per range of a (range, strip) Gram grid under segments: the range count the kernel would take for a
+// slab of one segment (nr_seg), rounded so that ranges tile every segment (rpr | seg) and a segment's units
+// (ranges x strips) fill whole blocks of `unit` (BLOCK / 64 waves of the VALU kernels, 1 workgroup of
+// the staged one).  A function of N and seg only, so every slab decomposes its segments the same way.  0: none fits.
+int64_t seg_rpr(int64_t seg, int64_t nr_seg, int64_t nstrips, int64_t unit) {
+  for (int64_t rpr = (seg + nr_seg - 1) / nr_seg; rpr >= 1; --rpr)
+    if (seg % rpr == 0 && ((seg / rpr) * nstrips) % unit == 0) return rpr;
+  return 0;
+}
+
 // local rows of the residual: owned +- 1 clipped to the domain
 void residual_rows(const gnk_ctx* ctx, int64_t& lr0, int64_t& nlr) {
   const Geo& g = ctx->geo;
@@ -3320,13 +3431,77 @@ int reduce(gnk_ctx* ctx, const double* partial, int nblk, int len, int stride, c
   return wreduce(ctx, partial, nblk, len, stride, len, 0, is_max, out);
 }
 
+// Segment reductions (gnk_set_segments): the partials of ctx->nseg segments, segblk blocks each
+// (segment s = blocks s * segblk .. (s + 1) * segblk - 1), are reduced per segment exactly as a slab of one
+// segment reduces its segblk blocks (the same split and wave tree: the result depends on segblk only), then
+// the segment values are folded in the fixed tree order (k_seg_fold).  The two workspaces sit below the last
+// 512 Ki doubles of the arena (callers' outputs live there); partials must end before SEG_WS.
+constexpr size_t SEG_WS = SCRATCH_DOUBLES - (size_t(1) << 21);
+constexpr size_t SEG_WS2 = SCRATCH_DOUBLES - (size_t(1) << 20);
+constexpr size_t SEG_WS_END = SCRATCH_DOUBLES - (size_t(1) << 19);
+bool seg_on(const gnk_ctx* ctx) { return ctx->seg > 0; }
+
+int sreduce(gnk_ctx* ctx, const double* partial, int segblk, int len, int64_t sb, int cw, int64_t cs,
+            const int* is_max, double* out) {
+  if (!seg_on(ctx)) return wreduce(ctx, partial, segblk, len, sb, cw, cs, is_max, out);
+  constexpr int SPAN = 4096;
+  const int nseg = ctx->nseg;
+  const int span = std::min(SPAN, std::max(1, segblk));
+  const int nsps = (std::max(1, segblk) + span - 1) / span;
+  double* t1 = ctx->scratch + SEG_WS;
+  double* t2 = ctx->scratch + SEG_WS2;
+  if (size_t(len) * nseg * nsps > SEG_WS2 - SEG_WS || size_t(len) * nseg > SEG_WS_END - SEG_WS2)
+    return fail(ctx, "segment reduction: workspace too small");
+  hipLaunchKernelGGL(k_wave_reduce, dim3(len, nseg * nsps), dim3(64), 0, ctx->stream, partial, nseg * segblk, span,
+                     sb, cw, cs, is_max, t1, segblk);
+  int rc = check_launch(ctx, "segment reduce");
+  if (rc) return rc;
+  if (nsps > 1) {
+    hipLaunchKernelGGL(k_wave_reduce, dim3(len, nseg), dim3(64), 0, ctx->stream, t1, nseg * nsps, nsps, int64_t(1), 1,
+                       int64_t(nseg) * nsps, is_max, t2, 0);
+    rc = check_launch(ctx, "segment reduce stage 2");
+    if (rc) return rc;
+    t1 = t2;
+  }
+  hipLaunchKernelGGL(k_seg_fold, dim3((len + 63) / 64), dim3(64), 0, ctx->stream, t1, nseg, len, is_max, out);
+  return check_launch(ctx, "segment fold");
+}
+
+// reduce() with segments: nblk partial blocks of `stride` doubles per segment
+int sreduce_rows(gnk_ctx* ctx, const double* partial, int segblk, int len, int stride, const int* is_max, double* out) {
+  return sreduce(ctx, partial, segblk, len, stride, len, 0, is_max, out);
+}
+
 // Compensated reduction of nblk blocks of (s, c) pairs: quantity j of block b at
 // partial[2 j + b * sb + {0, 1}] -> out[j] = s + c (k_wave_reduce2; two stages above 4096 blocks).
 // With ctx->pairs the result stays the unevaluated pair: out[2 j] = s_j, out[2 j + 1] = c_j (the
 // caller merges ranks' pairs, slab.Comm.sum_pairs).
-int wreduce2(gnk_ctx* ctx, const double* partial, int nblk, int len, int64_t sb, double* out) {
+int wreduce2(gnk_ctx* ctx, const double* partial, int nblk, int len, int64_t sb, double* out, int segblk = 0) {
   constexpr int SPAN = 4096;
   const int final = ctx->pairs ? 0 : 1;
+  if (segblk > 0 && seg_on(ctx) && !ctx->pairs) {
+    // per segment: the compensated sum of its blocks (rounded once), then the tree fold (plain)
+    const int nseg = ctx->nseg;
+    const int span = std::min(SPAN, segblk);
+    const int nsps = (segblk + span - 1) / span;
+    double* t1 = ctx->scratch + SEG_WS;
+    double* t2 = ctx->scratch + SEG_WS2;
+    if (size_t(2) * len * nseg * nsps > SEG_WS2 - SEG_WS || size_t(len) * nseg > SEG_WS_END - SEG_WS2)
+      return fail(ctx, "segment reduction (compensated): workspace too small");
+    hipLaunchKernelGGL(k_wave_reduce2, dim3(len, nseg * nsps), dim3(64), 0, ctx->stream, partial, nseg * segblk, span,
+                       sb, int64_t(2), nsps > 1 ? 0 : 1, nsps > 1 ? t1 : t2, segblk);
+    int rc = check_launch(ctx, "segment reduce2");
+    if (rc) return rc;
+    if (nsps > 1) {
+      hipLaunchKernelGGL(k_wave_reduce2, dim3(len, nseg), dim3(64), 0, ctx->stream, t1, nseg * nsps, nsps, int64_t(2),
+                         int64_t(2) * nseg * nsps, 1, t2, 0);
+      rc = check_launch(ctx, "segment reduce2 stage 2");
+      if (rc) return rc;
+    }
+    hipLaunchKernelGGL(k_seg_fold, dim3((len + 63) / 64), dim3(64), 0, ctx->stream, t2, nseg, len, nullptr, out);
+    return check_launch(ctx, "segment fold (compensated)");
+  }
+  if (segblk > 0 && seg_on(ctx)) nblk = segblk * ctx->nseg;     // pairs: every block, one rank-level pair
   if (nblk <= SPAN) {
     hipLaunchKernelGGL(k_wave_reduce2, dim3(len, 1), dim3(64), 0, ctx->stream, partial, nblk, nblk, sb, int64_t(2),
                        final, out);
@@ -3352,11 +3527,13 @@ const int* sum_max_flags() {
   return static_cast<const int*>(p);
 }
 
-// {sum x^2, max |x|} of k_stats partials ([s, c, max] per block); ctx->pairs: {s, c, max |x|}
+// {sum x^2, max |x|} of k_stats partials ([s, c, max] per block); ctx->pairs: {s, c, max |x|}.
+// Segments: nblk blocks per segment.
 int reduce_stats(gnk_ctx* ctx, const double* partial, int nblk, double* stats_out) {
-  int rc = wreduce2(ctx, partial, nblk, 1, 3, stats_out);
+  const bool sg = seg_on(ctx);
+  int rc = wreduce2(ctx, partial, nblk, 1, 3, stats_out, sg ? nblk : 0);
   if (rc) return rc;
-  return wreduce(ctx, partial + 2, nblk, 1, 3, 1, 0, sum_max_flags() + 1, stats_out + (ctx->pairs ? 2 : 1));
+  return sreduce(ctx, partial + 2, nblk, 1, 3, 1, 0, sum_max_flags() + 1, stats_out + (ctx->pairs ? 2 : 1));
 }
 
 int tuning(const gnk_ctx* ctx, int key) { return ctx->tune[key]; }
@@ -3446,6 +3623,8 @@ int gnk_set_bratu(gnk_ctx* ctx, int64_t N, int64_t row0, int64_t nrows, double h
   if (N < 2 || nrows < 1 || row0 < 0 || row0 + nrows > N) return fail(ctx, "gnk_set_bratu: bad slab geometry");
   if (nrows < G && nrows != N) return fail(ctx, "gnk_set_bratu: slab must own >= GNK_GHOST_ROWS rows");
   ctx->geo = Geo{N, row0, nrows};
+  ctx->seg = 0;                                     // segments belong to one slab geometry
+  ctx->nseg = 1;
   Coef c;
   // identical float expressions to ref:bratu_pde_problem.py:58,67 (h ** -2, h ** -1)
   const double hm2 = std::pow(h, -2.0);
@@ -3460,6 +3639,23 @@ int gnk_set_bratu(gnk_ctx* ctx, int64_t N, int64_t row0, int64_t nrows, double h
   c.lam = lambda;
   c.lam_zero = (lambda == 0.0) ? 1 : 0;
   ctx->coef = c;
+  return 0;
+}
+
+int gnk_set_segments(gnk_ctx* ctx, int64_t seg_rows) {
+  if (!ready(ctx)) return -1;
+  if (seg_rows == 0) {
+    ctx->seg = 0;
+    ctx->nseg = 1;
+    return 0;
+  }
+  const Geo& g = ctx->geo;
+  if (seg_rows < 1 || g.row0 % seg_rows != 0 || g.nrows % seg_rows != 0)
+    return fail(ctx, "gnk_set_segments: the slab must hold whole segments (row0 % seg_rows == nrows % seg_rows == 0)");
+  if (g.nrows / seg_rows > SEG_MAX) return fail(ctx, "gnk_set_segments: more than 64 segments per slab");
+  if (g.nrows > 65535) return fail(ctx, "gnk_set_segments: more than 65535 rows per slab");
+  ctx->seg = seg_rows;
+  ctx->nseg = int(g.nrows / seg_rows);
   return 0;
 }
 
@@ -3517,8 +3713,9 @@ int gnk_bratu_residual(gnk_ctx* ctx, const double* x, const double* y, double* r
   residual_rows(ctx, lr0, nlr);
   // one workgroup per row chunk (a persistent grid of the resident workgroups measured 17 % slower:
   // 0.37 vs 0.32 ms at 8192^2, profiles/round3/rocprof_window_breakdown.json)
-  RowLaunch L = rows(ctx, lr0, nlr, vec_of(ctx));
+  RowLaunch L = rows(ctx, lr0, nlr, vec_of(ctx), seg_row_cap(ctx));
   const int nblk = L.grid.x * L.grid.y;
+  if (seg_on(ctx) && int64_t(L.grid.y) != L.nlr) return fail(ctx, "bratu_residual: segments need one block row per grid row");
   // two rows per block where k_forward runs one row per block (its partials, bit for bit)
   if (int64_t(L.grid.y) == L.nlr && rows2(ctx, L))
     hipLaunchKernelGGL(k_forward2, L.grid, dim3(BLOCK), 0, ctx->stream, x, y, r, ctx->geo, ctx->coef, L.lr0, L.nlr,
@@ -3527,6 +3724,8 @@ int gnk_bratu_residual(gnk_ctx* ctx, const double* x, const double* y, double* r
     DISPATCH_VEC(ctx, k_forward, L, 0, x, y, r, ctx->geo, ctx->coef, L.lr0, L.nlr, ctx->scratch);
   int rc = check_launch(ctx, "bratu_residual");
   if (rc) return rc;
+  if (norm2_out && seg_on(ctx))     // owned row m's partials at (G - lr0 + m) * grid.x
+    return sreduce_rows(ctx, ctx->scratch + (G - L.lr0) * L.grid.x, int(ctx->seg * L.grid.x), 1, 1, nullptr, norm2_out);
   if (norm2_out) return reduce(ctx, ctx->scratch, nblk, 1, 1, nullptr, norm2_out);
   return 0;
 }
@@ -3566,7 +3765,8 @@ int gnk_vjp_gemv_t(gnk_ctx* ctx, const double* u, const double* r, const double*
   const int kct = k <= 24 ? std::max(4, (k + 3) / 4 * 4) : 16;
   const int nchunk = std::max(1, (k + kct - 1) / kct);
   const int cap = tuning(ctx, GNK_TUNE_VJPG_BLOCKS);
-  RowLaunch L = rows(ctx, G, ctx->geo.nrows, vec_of(ctx), cap > 0 ? cap : std::max(64, 2048 / nchunk));
+  RowLaunch L = rows(ctx, G, ctx->geo.nrows, vec_of(ctx),
+                     seg_on(ctx) ? (1 << 30) : (cap > 0 ? cap : std::max(64, 2048 / nchunk)));
   L.grid.z = nchunk;
   const int nblk = L.grid.x * L.grid.y;
   if (size_t(nblk) * nchunk * kct > SCRATCH_DOUBLES) return fail(ctx, "vjp_gemv_t: scratch too small");
@@ -3591,6 +3791,8 @@ int gnk_vjp_gemv_t(gnk_ctx* ctx, const double* u, const double* r, const double*
 #undef VJPG_LAUNCH
   int rc = check_launch(ctx, "vjp_gemv_t");
   if (rc || k == 0 || !h_out) return rc;
+  if (seg_on(ctx))                  // one block row per owned row: segment s = blocks s * seg * grid.x ..
+    return sreduce(ctx, ctx->scratch, int(ctx->seg * L.grid.x), k, kct, kct, int64_t(nblk) * kct, nullptr, h_out);
   return wreduce(ctx, ctx->scratch, nblk, k, kct, kct, int64_t(nblk) * kct, nullptr, h_out);
 }
 
@@ -3622,23 +3824,30 @@ static int gemv_vjpg_launch(gnk_ctx* ctx, const char* what, const double* V, int
   const void* fn = vec_of(ctx) == 2 ? (pend ? vjpg_pick<2, true>(kct) : vjpg_pick<2, false>(kct))
                                     : (pend ? vjpg_pick<1, true>(kct) : vjpg_pick<1, false>(kct));
   RowLaunch L = rows(ctx, 0, ctx->geo.nrows + 2 * G, vec_of(ctx), resident_blocks(ctx, fn));
+  // segments: the resident grid once per segment (grid.z = nseg + 1: the segments, then the ghost rows);
+  // a segment's partials then depend on the resident count only, not on the slab
+  const int ns = seg_on(ctx) ? ctx->nseg + 1 : 1;                  // partial sets
+  L.grid.z = unsigned(ns);
+  if (seg_on(ctx)) L.grid.y = unsigned(std::min<int64_t>(resident_blocks(ctx, fn) / L.grid.x, ctx->seg));
   const int nblk = L.grid.x * L.grid.y;
-  const size_t soff = (size_t(nblk) * kct + 1) & ~size_t(1);     // stats partials after the h partials
-  if (soff + 2 * size_t(nblk) > SCRATCH_DOUBLES / 2) return fail(ctx, std::string(what) + ": scratch too small");
+  const size_t soff = (size_t(nblk) * ns * kct + 1) & ~size_t(1);  // stats partials after the h partials
+  if (soff + 2 * size_t(nblk) * ns > SCRATCH_DOUBLES / 2) return fail(ctx, std::string(what) + ": scratch too small");
   double* spart = ctx->scratch + soff;
   Geo geo = ctx->geo;
   Coef coef = ctx->coef;
   double* part = ctx->scratch;
-  void* args[] = {&V, &ldv, &k, &c, &hh, &wcol, &r, &x, &g, &geo, &coef, &L.lr0, &L.nlr, &part, &spart};
+  int64_t seg = ctx->seg;
+  int nseg = ctx->nseg;
+  void* args[] = {&V, &ldv, &k, &c, &hh, &wcol, &r, &x, &g, &geo, &coef, &L.lr0, &L.nlr, &part, &spart, &seg, &nseg};
   // algorithmic bytes (owned rows): the k settled columns, r in, x and g out; pending: w read + written
   TimedLaunch tl(ctx, GNK_TIMER_TRIAL, 8.0 * double(ctx->geo.nrows) * double(ctx->geo.N) * double(k + 3 + (pend ? 2 : 0)));
   (void)hipLaunchKernel(fn, L.grid, dim3(BLOCK), args, 0, ctx->stream);
   tl.done();
   int rc = check_launch(ctx, what);
   if (rc) return rc;
-  rc = wreduce(ctx, ctx->scratch, nblk, kk, kct, kct, int64_t(nblk) * kct, nullptr, h_out);
+  rc = sreduce(ctx, ctx->scratch, nblk, kk, kct, kct, int64_t(nblk) * kct, nullptr, h_out);
   if (rc || !pend) return rc;
-  return reduce(ctx, spart, nblk, 2, 2, sum_max_flags(), stats_out);
+  return sreduce_rows(ctx, spart, nblk, 2, 2, sum_max_flags(), stats_out);
 }
 
 int gnk_basis_gemv_vjp_gemv_t(gnk_ctx* ctx, const double* V, int64_t ldv, int k, const double* c, const double* r,
@@ -3665,11 +3874,16 @@ int gnk_basis_gemv_pending(gnk_ctx* ctx, const double* V, int64_t ldv, int k, co
   if (x == w) return fail(ctx, "basis_gemv_pending: x aliases the pending column");
   const void* fnp = vec_of(ctx) == 2 ? (const void*)&k_gemv_p<2> : (const void*)&k_gemv_p<1>;
   RowLaunch L = rows(ctx, 0, ctx->geo.nrows + 2 * G, vec_of(ctx), resident_blocks(ctx, fnp));
+  if (seg_on(ctx)) {                                      // as gemv_vjpg_launch
+    L.grid.z = unsigned(ctx->nseg + 1);
+    L.grid.y = unsigned(std::min<int64_t>(resident_blocks(ctx, fnp) / L.grid.x, ctx->seg));
+  }
   const int nblk = L.grid.x * L.grid.y;
-  DISPATCH_VEC(ctx, k_gemv_p, L, 0, V, ldv, k, c, hh, w, x, ctx->geo, L.lr0, L.nlr, ctx->scratch);
+  DISPATCH_VEC(ctx, k_gemv_p, L, 0, V, ldv, k, c, hh, w, x, ctx->geo, L.lr0, L.nlr, ctx->scratch, ctx->seg,
+               ctx->nseg);
   int rc = check_launch(ctx, "basis_gemv_pending");
   if (rc) return rc;
-  return reduce(ctx, ctx->scratch, nblk, 2, 2, sum_max_flags(), stats_out);
+  return sreduce_rows(ctx, ctx->scratch, nblk, 2, 2, sum_max_flags(), stats_out);
 }
 
 int gnk_cgs_update(gnk_ctx* ctx, const double* V, int64_t ldv, int k, const double* h, double* g,
@@ -3677,22 +3891,23 @@ int gnk_cgs_update(gnk_ctx* ctx, const double* V, int64_t ldv, int k, const doub
   if (!ready(ctx)) return -1;
   if (k < 1) return fail(ctx, "cgs_update: k < 1");
   if (vec_of(ctx) == 2 && (ldv % 2 != 0)) return fail(ctx, "cgs_update: ldv must be even");
-  RowLaunch L = rows(ctx, G, ctx->geo.nrows, vec_of(ctx));
+  RowLaunch L = rows(ctx, G, ctx->geo.nrows, vec_of(ctx), seg_row_cap(ctx));
   const int nblk = L.grid.x * L.grid.y;
   DISPATCH_VEC(ctx, k_cgs, L, 0, V, ldv, k, h, g, ctx->geo, L.lr0, L.nlr, ctx->scratch);
   int rc = check_launch(ctx, "cgs_update");
   if (rc) return rc;
+  if (seg_on(ctx)) return sreduce_rows(ctx, ctx->scratch, int(ctx->seg * L.grid.x), 2, 2, sum_max_flags(), stats_out);
   return reduce(ctx, ctx->scratch, nblk, 2, 2, sum_max_flags(), stats_out);
 }
 
 int gnk_vec_stats(gnk_ctx* ctx, const double* x, double* stats_out) {
   if (!ready(ctx)) return -1;
-  RowLaunch L = rows(ctx, G, ctx->geo.nrows, vec_of(ctx));
+  RowLaunch L = rows(ctx, G, ctx->geo.nrows, vec_of(ctx), seg_row_cap(ctx));
   const int nblk = L.grid.x * L.grid.y;
   DISPATCH_VEC(ctx, k_stats, L, 0, x, ctx->geo, L.lr0, L.nlr, ctx->scratch);
   int rc = check_launch(ctx, "vec_stats");
   if (rc) return rc;
-  return reduce_stats(ctx, ctx->scratch, nblk, stats_out);
+  return reduce_stats(ctx, ctx->scratch, seg_on(ctx) ? int(ctx->seg * L.grid.x) : nblk, stats_out);
 }
 
 int gnk_vec_div(gnk_ctx* ctx, const double* src, double denom, double* dst, int full_slab) {
@@ -3708,11 +3923,13 @@ int gnk_normalize_jnorm(gnk_ctx* ctx, const double* u, const double* g, double d
   if (!ready(ctx)) return -1;
   if (!u || !g || !v) return fail(ctx, "normalize_jnorm: NULL vector");
   if (g == v) return fail(ctx, "normalize_jnorm: v must not alias g (stencil reads of g)");
-  RowLaunch L = rows(ctx, 0, ctx->geo.nrows + 2 * G, vec_of(ctx));
+  RowLaunch L = rows(ctx, 0, ctx->geo.nrows + 2 * G, vec_of(ctx), seg_row_cap(ctx));
   const int nblk = L.grid.x * L.grid.y;
   DISPATCH_VEC(ctx, k_div_jnorm, L, 0, u, g, denom, v, ctx->geo, ctx->coef, L.lr0, L.nlr, ctx->scratch);
   int rc = check_launch(ctx, "normalize_jnorm");
   if (rc || !jnorm2_out) return rc;
+  if (seg_on(ctx))                  // owned rows from grid row G
+    return sreduce_rows(ctx, ctx->scratch + G * L.grid.x, int(ctx->seg * L.grid.x), 1, 1, nullptr, jnorm2_out);
   return reduce(ctx, ctx->scratch, nblk, 1, 1, nullptr, jnorm2_out);   // sum (J g)^2
 }
 
@@ -3748,7 +3965,12 @@ int gnk_gram(gnk_ctx* ctx, const double* u, const double* V, int64_t ldv, int k,
     // about 8 waves per CU, whole row ranges per strip
     int64_t nranges = std::max<int64_t>(1, std::min<int64_t>(nrows, int64_t(ctx->num_cus) * 8 / nstrips));
     const int rpr_t = tuning(ctx, GNK_TUNE_GRAM_RPR);
-    const int64_t rpr = rpr_t > 0 ? int64_t(rpr_t) : (nrows + nranges - 1) / nranges;
+    // segments: the decomposition of a one-segment slab, in every segment (0: this grid cannot, per rank)
+    const int64_t rpr_s = seg_on(ctx) ? seg_rpr(ctx->seg, std::max<int64_t>(1, std::min<int64_t>(
+                                                    ctx->seg, int64_t(ctx->num_cus) * 8 / nstrips)), nstrips,
+                                                BLOCK / 64)
+                                      : 0;
+    const int64_t rpr = rpr_s > 0 ? rpr_s : rpr_t > 0 ? int64_t(rpr_t) : (nrows + nranges - 1) / nranges;
     nranges = (nrows + rpr - 1) / rpr;
     const int64_t nwaves = nstrips * nranges;
     const int64_t nblk = (nwaves + BLOCK / 64 - 1) / (BLOCK / 64);
@@ -3785,7 +4007,14 @@ int gnk_gram(gnk_ctx* ctx, const double* u, const double* V, int64_t ldv, int k,
     if (rcv) return rcv;
     (void)hipMemsetAsync(G_out, 0, size_t(KP) * KP * sizeof(double), ctx->stream);
     double* red = ctx->scratch + (SCRATCH_DOUBLES - size_t(NT));
-    rcv = wreduce(ctx, ctx->scratch, int(nblk), NT, int64_t(NT), NT, 0, nullptr, red);
+    if (rpr_s > 0) {
+      if (size_t(nblk) * NT > SEG_WS) return fail(ctx, "gram: scratch too small (valu, segments)");
+      // a block is BLOCK / 64 consecutive waves = tiles (range-major): a segment's blocks are contiguous
+      rcv = sreduce(ctx, ctx->scratch, int((ctx->seg / rpr) * nstrips / (BLOCK / 64)), NT, int64_t(NT), NT, 0,
+                    nullptr, red);
+    } else {
+      rcv = wreduce(ctx, ctx->scratch, int(nblk), NT, int64_t(NT), NT, 0, nullptr, red);
+    }
     if (rcv) return rcv;
     hipLaunchKernelGGL(k_gram_scatter_v, dim3(1), dim3(64), 0, ctx->stream, red, k + 1, KP, G_out);
     return check_launch(ctx, "gram scatter (valu)");
@@ -3825,8 +4054,12 @@ int gnk_gram(gnk_ctx* ctx, const double* u, const double* V, int64_t ldv, int k,
       const int64_t nrows = ctx->geo.nrows;
       int64_t nranges = std::max<int64_t>(1, std::min<int64_t>(nrows, int64_t(ctx->num_cus) * wgpc / nstrips));
       const int rpr_t = tuning(ctx, GNK_TUNE_GRAM_RPR);
-      const int64_t rpr = rpr_t > 0 ? int64_t(rpr_t) : (nrows + nranges - 1) / nranges;
+      const int64_t rpr_s = seg_on(ctx) ? seg_rpr(ctx->seg, std::max<int64_t>(1, std::min<int64_t>(
+                                                      ctx->seg, int64_t(ctx->num_cus) * wgpc / nstrips)), nstrips, 1)
+                                        : 0;
+      const int64_t rpr = rpr_s > 0 ? rpr_s : rpr_t > 0 ? int64_t(rpr_t) : (nrows + nranges - 1) / nranges;
       nranges = (nrows + rpr - 1) / rpr;
+      const int plog = rpr_s > 0 ? 1 : 0;             // partials at the logical (range, strip) tile
       const int64_t nwg = nstrips * nranges;
       if (nwg > (1 << 20) || size_t(nwg) * PL > SCRATCH_DOUBLES - size_t(PL))
         return fail(ctx, "gram: scratch too small (staged)");
@@ -3834,7 +4067,7 @@ int gnk_gram(gnk_ctx* ctx, const double* u, const double* V, int64_t ldv, int k,
       TimedLaunch tls(ctx, GNK_TIMER_GRAM, 8.0 * double(nown) * double(k + 1 + (r ? 1 : 0)));
 #define GRAMS_RW(NBV, LV, KV, TV, RV, WV)                                                                     \
   hipLaunchKernelGGL((k_gram_s<NBV, LV, KV, TV, RV, WV>), dim3(unsigned(nwg)), dim3(64 * GS_NW), lds, ctx->stream, u, \
-                     V, ldv, k, rv, KP, r, ctx->geo, ctx->coef, rpr, ctx->scratch)
+                     V, ldv, k, rv, KP, r, ctx->geo, ctx->coef, rpr, ctx->scratch, plog)
 #define GRAMS(NBV, LV, KV)                                                 \
   do {                                                                     \
     if (ring == 4 && two_wg) GRAMS_RW(NBV, LV, KV, 0, 4, 4);               \
@@ -3872,7 +4105,12 @@ int gnk_gram(gnk_ctx* ctx, const double* u, const double* V, int64_t ldv, int k,
       if (rcs) return rcs;
       (void)hipMemsetAsync(G_out, 0, size_t(KP) * KP * sizeof(double), ctx->stream);
       double* red = ctx->scratch + (SCRATCH_DOUBLES - size_t(PL));
-      rcs = wreduce(ctx, ctx->scratch, int(nwg), PL, int64_t(PL), PL, 0, nullptr, red);
+      if (plog) {
+        if (size_t(nwg) * PL > SEG_WS) return fail(ctx, "gram: scratch too small (staged, segments)");
+        rcs = sreduce(ctx, ctx->scratch, int((ctx->seg / rpr) * nstrips), PL, int64_t(PL), PL, 0, nullptr, red);
+      } else {
+        rcs = wreduce(ctx, ctx->scratch, int(nwg), PL, int64_t(PL), PL, 0, nullptr, red);
+      }
       if (rcs) return rcs;
       hipLaunchKernelGGL(k_gram_scatter_s, dim3(4), dim3(BLOCK), 0, ctx->stream, red, nbs, nacc, k, r ? 1 : 0, KP,
                          G_out);

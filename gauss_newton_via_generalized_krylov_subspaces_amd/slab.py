@@ -7,8 +7,12 @@ residuals, CG vectors -- is split identically and stored as a slab vector with
 GHOST rows on each side (include/gnk.h).
 
 Determinism: every cross-rank reduction all-gathers the per-rank partials and
-sums them in rank order on every rank, so the control decisions (Armijo,
-breakdown, convergence, restart) are bit-identical on all ranks.
+sums them in one fixed pairwise order (``tree_sum``) on every rank, so the control
+decisions (Armijo, breakdown, convergence, restart) are bit-identical on all ranks.
+With reduction segments (``Comm(segments=...)``, gnk_set_segments) the library reduces
+fixed global row segments of N / 8 rows with a decomposition of their own and folds a
+rank's segments in the same pairwise order, so a run on 1, 2, 4 or 8 ranks gives the
+same bits: the rank values are exactly the subtrees of the one-rank fold.
 
 Collectives: only two kinds exist on the data path --
   * halo: P2P send/recv of GHOST boundary rows to the two neighbours, once per
@@ -27,6 +31,32 @@ import torch.distributed as dist
 from ._native import GHOST
 
 
+SEGMENTS_PER_GRID = 8      # reduction segments of N / 8 rows: rank-count invariance for world | 8
+
+
+def tree_sum(parts):
+    """Sum of the rows of ``parts`` (P x n) in the fixed pairwise order v[i] += v[i + w] for
+    w = 1, 2, 4, .. (i a multiple of 2w, i + w < P): the balanced binary tree for a power-of-two P,
+    and the order of gnk_rank_sum and of gnk_set_segments' segment fold."""
+    v = [np.array(parts[p], dtype=np.float64, copy=True) for p in range(parts.shape[0])]
+    w = 1
+    while w < len(v):
+        for i in range(0, len(v) - w, 2 * w):
+            v[i] = v[i] + v[i + w]
+        w *= 2
+    return v[0]
+
+
+def reduction_segments(N: int, world: int, want) -> int:
+    """Rows per reduction segment for a grid of N rows on ``world`` ranks (0 = none): N / 8 when
+    segments are wanted (``want`` True, or None and world > 1) and every rank holds whole segments
+    (N % 8 == 0 and world divides 8)."""
+    on = (world > 1) if want is None else bool(want)
+    if not on or N % SEGMENTS_PER_GRID != 0 or SEGMENTS_PER_GRID % world != 0:
+        return 0
+    return N // SEGMENTS_PER_GRID
+
+
 def row_partition(N: int, world: int, rank: int):
     """Contiguous, balanced split of N rows over `world` ranks -> (row0, nrows)."""
     base, rem = divmod(N, world)
@@ -40,7 +70,10 @@ class Comm:
     GPUs, gloo on CPU).  ``group=None`` with no initialised process group means a
     single rank."""
 
-    def __init__(self, group=None, single: bool = False):
+    def __init__(self, group=None, single: bool = False, segments=None):
+        # reduction segments (rank-count-independent reductions, gnk_set_segments): None = on when
+        # there is more than one rank, True / False = always / never
+        self.segments = segments
         if not single and dist.is_available() and dist.is_initialized():
             self.group = group
             self.rank = dist.get_rank(group)
@@ -52,21 +85,32 @@ class Comm:
             self.group = None
             self.rank, self.world = 0, 1
             self.stage = False
-        # device-side rank-ordered sum of all-gathered partials (one kernel, set by the device
+        # device-side sum (tree_sum's order) of all-gathered partials (one kernel, set by the device
         # backend: HipBackend.rank_sum); None: elementwise torch adds in the same order
         self.device_rank_sum = None
+        # traffic counters (what one outer step costs in collectives and host waits):
+        # all-gathers and their per-rank payload, P2P exchanges and their bytes sent, host waits on
+        # device results (a blocking read: the host cannot run ahead of the GPU there)
+        self.counters = {"all_gather": 0, "all_gather_bytes": 0, "p2p": 0, "p2p_bytes": 0, "host_wait": 0}
 
     def _sum_parts_device(self, gath: torch.Tensor, n: int) -> torch.Tensor:
         if self.device_rank_sum is not None:
             out = torch.empty(n, dtype=gath.dtype, device=gath.device)
             return self.device_rank_sum(gath, self.world, out)
         parts = gath.view(self.world, -1)
-        s = parts[0].clone()
-        for p in range(1, self.world):
-            s.add_(parts[p])
-        return s
+        v = [parts[p].clone() for p in range(self.world)]
+        w = 1
+        while w < len(v):                                   # tree_sum's order
+            for i in range(0, len(v) - w, 2 * w):
+                v[i].add_(v[i + w])
+            w *= 2
+        return v[0]
 
     # -- transport: the two collectives of the data path (RCCL on GPUs, gloo on CPU) ---------
+    def _count_gather(self, t: torch.Tensor):
+        self.counters["all_gather"] += 1
+        self.counters["all_gather_bytes"] += t.numel() * t.element_size()
+
     def _all_gather_into(self, buf: torch.Tensor, t: torch.Tensor):
         dist.all_gather_into_tensor(buf, t, group=self.group)
 
@@ -78,12 +122,15 @@ class Comm:
 
     # -- reductions -------------------------------------------------------------
     def _gather(self, t: torch.Tensor) -> np.ndarray:
+        if t.device.type != "cpu":
+            self.counters["host_wait"] += 1
         if self.world == 1:
             return t.detach().to("cpu", torch.float64).numpy()[None]
         t = t.contiguous().reshape(-1)
         if self.stage:
             t = t.to("cpu")
         buf = torch.empty(self.world * t.numel(), dtype=t.dtype, device=t.device)
+        self._count_gather(t)
         self._all_gather_into(buf, t)
         return buf.to("cpu").numpy().reshape(self.world, -1)
 
@@ -110,12 +157,8 @@ class Comm:
         return self.merge_pairs(self._gather(t[:2 * nq]))
 
     def sum(self, t: torch.Tensor) -> np.ndarray:
-        """Sum of a small per-rank tensor over ranks, in rank order (host result)."""
-        parts = self._gather(t)
-        s = parts[0].copy()
-        for p in range(1, parts.shape[0]):
-            s = s + parts[p]
-        return s
+        """Sum of a small per-rank tensor over ranks, in tree_sum's order (host result)."""
+        return tree_sum(self._gather(t))
 
     def sum_max(self, t: torch.Tensor) -> tuple[float, float]:
         """t = [sum, max] per rank -> (sum over ranks, NaN-propagating max over ranks)."""
@@ -123,13 +166,12 @@ class Comm:
         return float(sums[0]), m
 
     def sum_and_max(self, t: torch.Tensor, nsum: int) -> tuple[np.ndarray, float]:
-        """t = [s_0 .. s_{nsum-1}, m] per rank -> (rank-ordered sums, NaN-propagating max): several
+        """t = [s_0 .. s_{nsum-1}, m] per rank -> (sums over ranks, NaN-propagating max): several
         control scalars of one step in one collective and one host read."""
         parts = self._gather(t)
-        s = parts[0][:nsum].copy()
+        s = tree_sum(parts[:, :nsum])
         m = float(parts[0][nsum])
         for p in range(1, parts.shape[0]):
-            s = s + parts[p][:nsum]
             v = float(parts[p][nsum])
             if v > m or math.isnan(v):
                 m = v
@@ -147,10 +189,9 @@ class Comm:
                 return both[:n].copy(), both[n:].copy()
             return self.sum_except_max(t, imax), shared.to("cpu", torch.float64).numpy().copy()
         parts = self._gather(t)
-        s = parts[0].copy()
+        s = tree_sum(parts)
         m = float(parts[0][imax])
         for p in range(1, parts.shape[0]):
-            s = s + parts[p]
             v = float(parts[p][imax])
             if v > m or math.isnan(v):
                 m = v
@@ -161,7 +202,7 @@ class Comm:
     def read_async(self, t: torch.Tensor, shared: torch.Tensor = None, pinned: torch.Tensor = None):
         """Enqueue the cross-rank gather of a small per-rank device tensor ``t`` (and a copy of
         ``shared``, identical on every rank) into host memory; returns a handle for ``complete``
-        (the host does not wait here).  ``device_sum(handle)``: the rank-ordered sum on the device,
+        (the host does not wait here).  ``device_sum(handle)``: the sum over ranks on the device,
         for device-side consumers that must not wait for the host."""
         n = t.numel()
         m = shared.numel() if shared is not None else 0
@@ -174,6 +215,7 @@ class Comm:
             gath = t.reshape(-1)
         else:
             gath = torch.empty(self.world * n, dtype=t.dtype, device=t.device)
+            self._count_gather(t)
             self._all_gather_into(gath, t.contiguous().reshape(-1))
         wn = self.world * n
         host = pinned[:wn + m]
@@ -185,7 +227,7 @@ class Comm:
         return _ReadHandle(host, ev, n, None, None, gath)
 
     def device_sum(self, h) -> torch.Tensor:
-        """Rank-ordered sum (on the device) of the tensor behind a read handle."""
+        """Sum over ranks (on the device) of the tensor behind a read handle."""
         if self.world == 1:
             return h.gath
         if h.gath.numel() == h.n:                 # staged / CPU path: sum on the host, copy back
@@ -194,15 +236,13 @@ class Comm:
 
     @staticmethod
     def _rank_sum(parts):
-        s = parts[0].copy()
-        for p in range(1, parts.shape[0]):
-            s = s + parts[p]
-        return s
+        return tree_sum(parts)
 
     def complete(self, h, imax: int):
-        """Wait for a read handle -> (rank-ordered sums except entry ``imax``: NaN-propagating max
+        """Wait for a read handle -> (sums over ranks except entry ``imax``: NaN-propagating max
         over ranks, shared host copy or None)."""
         if h.ev is not None:
+            self.counters["host_wait"] += 1
             h.ev.synchronize()
             wn = self.world * h.n
             a = h.host.numpy()
@@ -219,7 +259,7 @@ class Comm:
         return s, h.shared
 
     def sum_device(self, t: torch.Tensor) -> torch.Tensor:
-        """Rank-ordered sum of a small per-rank device tensor, left on the device (no host round
+        """Sum over ranks of a small per-rank device tensor, left on the device (no host round
         trip on RCCL): the same IEEE additions in the same order as ``sum``."""
         if self.world == 1:
             return t
@@ -227,6 +267,7 @@ class Comm:
             return torch.from_numpy(self.sum(t)).to(t.device)
         t = t.contiguous().reshape(-1)
         buf = torch.empty(self.world * t.numel(), dtype=t.dtype, device=t.device)
+        self._count_gather(t)
         self._all_gather_into(buf, t)
         return self._sum_parts_device(buf, t.numel())
 
@@ -250,6 +291,8 @@ class Comm:
         if self.rank < self.world - 1:
             ops.append((dist.isend, host[own_end - g:own_end], self.rank + 1))
             ops.append((dist.irecv, host[own_end:own_end + g], self.rank + 1))
+        self.counters["p2p"] += 1
+        self.counters["p2p_bytes"] += sum(t.numel() * t.element_size() for op, t, _ in ops if op is dist.isend)
         self._p2p(ops)
         if staged:
             if self.rank > 0:

@@ -33,7 +33,7 @@ extern "C" {
 #endif
 
 #define GNK_GHOST_ROWS 2
-#define GNK_ABI_VERSION 4
+#define GNK_ABI_VERSION 5
 
 typedef struct gnk_ctx gnk_ctx;
 
@@ -49,6 +49,18 @@ int gnk_set_stream(gnk_ctx* ctx, void* hip_stream);
  * out[2j+1] = c_j (gnk_vec_stats: {s, c, max|x|}), so a multi-rank caller can merge every rank's
  * pair with TwoSum in rank order before rounding (slab.Comm.sum_pairs).  Default 0. */
 int gnk_set_reduce_pairs(gnk_ctx* ctx, int on);
+/* Rank-count-independent reductions.  seg_rows > 0 splits the grid into fixed global row segments
+ * of seg_rows rows (call after gnk_set_bratu; the slab must hold whole segments: row0 % seg_rows ==
+ * nrows % seg_rows == 0; at most 64 per slab; gnk_set_bratu resets it to 0).  Every reduction of the
+ * GNK path -- the Gram passes of gnk_gram at k <= 20 (N % 128 == 0), the first-trial / pending-column
+ * sums (gnk_basis_gemv_vjp_gemv_t*, gnk_basis_gemv_pending), gnk_bratu_residual, gnk_vec_stats,
+ * gnk_cgs_update, gnk_vjp_gemv_t, gnk_normalize_jnorm -- is then computed per segment with a block
+ * decomposition that depends on N and seg_rows only, and the segment values are folded pairwise in
+ * a fixed tree: v[i] += v[i + w] for w = 1, 2, 4, ... (i a multiple of 2w, i + w < n).  With
+ * seg_rows = N / P and P / w segments per rank, combining the w ranks' values in the same tree
+ * order (slab.Comm) gives the same bits for every w dividing P.  Compensated pairs
+ * (gnk_set_reduce_pairs) stay per rank.  0 = off (the default: one decomposition per slab). */
+int gnk_set_segments(gnk_ctx* ctx, int64_t seg_rows);
 /* Kernel-choice overrides for tests and A/B tooling (value 0 = the library's own choice, the
  * default; the solver never sets them):
  *   GNK_TUNE_GRAM_PATH   1 = the staged MFMA Gram kernel for every pass it covers (k <= 20),
@@ -140,8 +152,9 @@ int gnk_basis_gemv_vjp_gemv_t_pending(gnk_ctx* ctx, const double* V, int64_t ldv
  * d = -R^-1 z, jdd = ||R d||^2, e_try = e + sdd * d (elementwise).  P: k x k upper triangular.
  * out = [status (0 ok, 1 not SPD), jdd, s, d (k), R (k*k), Ry (k*k), R^-1 (k*k)].
  * 1 <= k <= gnk_lls_max_k().           ref:gauss_newton_krylow.py:16-36, armijo_goldstein.py:50 */
-/* out[j] = sum over p in rank order of parts[p * n + j] (left to right, as the host sums all-gathered
- * partials; slab.Comm): the rank-ordered reduction of a small per-rank vector after all_gather. */
+/* out[j] = sum over p of parts[p * n + j] in the fixed pairwise order of gnk_set_segments' fold
+ * (v[i] += v[i + w] for w = 1, 2, 4, ..; the order slab.Comm sums all-gathered partials on the host):
+ * the cross-rank reduction of a small per-rank vector after all_gather. */
 int gnk_rank_sum(gnk_ctx* ctx, const double* parts, int world, int64_t n, double* out);
 int gnk_lls_max_k(void);
 int gnk_lls_solve(gnk_ctx* ctx, const double* G, int kp, int k, const double* P, int rescale, const double* sdd,

@@ -17,7 +17,7 @@ process's anonymous memory stays ~ 25 GB -- at k = 17 an all-anonymous run reach
   exact_k1  the one-column steps (k = 1) with exactly rounded sums (math.fsum) -- the cancellation-
             limited step the device's compensated k = 1 path computes (tests/golden/make_sensitivity.py).
   cholqr    the device's least-squares arithmetic (lls.CholQR2Solver._passes) instead of Householder:
-            the exact k = 1 step, then for k >= 2 preconditioned CholeskyQR -- P = blockdiag(R_prev, 1),
+            the k = 1 step on exactly rounded sums in k_lls's operation order, then for k >= 2 preconditioned CholeskyQR -- P = blockdiag(R_prev, 1),
             Y = (J V) P^-1 (fp64 BLAS), the Gram of [Y | r] in extended precision (x87 80-bit products
             and sums over 64 Ki-row chunks, the chunk sums kept as double-double pairs and added exactly
             by math.fsum: ~1e-19 relative, orders below an fp64 Gram), the new column rescaled by
@@ -153,12 +153,16 @@ class CholQRLS:
             a = JV[:, 0] if k == 1 else None
             if k != 1:
                 raise RuntimeError("no preconditioner at k > 1: not the bench trajectory")
-            # the exact k = 1 step (the device's compensated one-column pass): G = [||Jv||^2, Jv.r]
+            # the k = 1 step on exactly rounded sums G = [||Jv||^2, Jv.r], in k_lls's arithmetic: the pass's
+            # rescale divides the Gram's row and column by s = sqrt(g00) (g00 / s / s, not exactly 1), then
+            # Cholesky ry = sqrt(.), z = (g01 / s) / ry, R = ry s, d = -(z / R)
             g00 = math.fsum(a * a)
             g01 = math.fsum(a * r)
             s = math.sqrt(g00)
-            R = np.array([[s]])
-            d = np.array([-(g01 / s) / s])
+            ry = math.sqrt((g00 / s) / s)
+            z = (g01 / s) / ry
+            R = np.array([[ry * s]])
+            d = np.array([-(z / R[0, 0])])
             self.R_prev = R
             self.passes.append((k, 1, [1.0]))
             return d, R

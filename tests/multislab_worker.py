@@ -10,10 +10,13 @@ Driven by tests/test_gpu_multislab.py.  Every rank runs every case; rank 0 colle
 results, repeats each solve single-rank and writes the comparison to --out:
   * all ranks took identical decisions (bookkeeping, stdout, per-iteration nfev) and hold the same
     iterate norms bit for bit;
-  * multi-rank vs single-rank: bookkeeping identical, per-iteration ||x_k|| within the case's bound:
-    GN + CGLS at north_star's 1e-10 (the CG scalars are compensated pairs merged across ranks,
-    slab.Comm.sum_pairs), GNK at the spread of the reference's own arithmetic reordered as 2 .. 8 slabs
-    order it (tests/test_oracle_sensitivity.py);
+  * multi-rank vs single-rank: bookkeeping identical; where the world divides 8 and N % 8 == 0 the
+    reductions are segmented (slab.reduction_segments, gnk_set_segments: on by default for several
+    ranks, asked for on the single rank) and every per-iteration ||x_k|| and the final x must agree BIT
+    FOR BIT, GNK and GN alike; otherwise (world 3) within the case's bound: GN + CGLS at north_star's
+    1e-10 (the CG scalars are compensated pairs merged across ranks, slab.Comm.sum_pairs), GNK at the
+    spread of the reference's own arithmetic reordered as 2 .. 8 slabs order it
+    (tests/test_oracle_sensitivity.py);
   * multi-rank vs the ORACLE (oracle/gnk_oracle.py, on rank 0's host): GNK bookkeeping and stdout
     identical, ||x_k|| within the same sensitivity bound; GN against the oracle with exactly rounded
     CG dot products (math.fsum -- what the device's compensated sums compute): bookkeeping and every
@@ -38,7 +41,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import gauss_newton_via_generalized_krylov_subspaces_amd as gnk  # noqa: E402
 from gauss_newton_via_generalized_krylov_subspaces_amd._device import BratuDevice  # noqa: E402
 from gauss_newton_via_generalized_krylov_subspaces_amd.inputs import slab_inputs  # noqa: E402
-from gauss_newton_via_generalized_krylov_subspaces_amd.slab import Comm  # noqa: E402
+from gauss_newton_via_generalized_krylov_subspaces_amd.slab import Comm, reduction_segments  # noqa: E402
 
 # ||x_k|| bound, multi-rank vs single-rank (every reduction summed in a different order): GNK at
 # max(1e-10, the spread of the reference's own arithmetic reordered as 2 .. 8 slabs order it, permuted
@@ -251,17 +254,19 @@ def main():
         return 0
     report, ok = [], True
     keys = ("nit", "nrev", "njev", "success", "nfev", "cg_iter", "stdout")
+    segmented = reduction_segments(N, world, None) > 0 and BACKEND is None   # the NumPy double has none
     for i, ((kind, kw), d) in enumerate(zip(cases, mine)):
         print(f"[rank 0] single-rank and oracle runs of case {i}: {kind} {kw}", file=sys.stderr, flush=True)
         ranks_equal = all(e["cases"][i] == d for e in every)
-        s = run(kind, prob, y, u0, Comm(single=True), **kw)
+        s = run(kind, prob, y, u0, Comm(single=True, segments=segmented), **kw)
         same = all(d[f] == s[f] for f in keys)
         rel = rel_diff(d["norms"], s["norms"])
         tol = bound(kind, kw, N)
-        case_ok = same and ranks_equal and rel <= tol
-        entry = {"case": kind, **kw, "world": world, "grid": N, "transport": a.transport,
-                 "ranks_identical": ranks_equal, "bookkeeping_equal": same, "max_rel_norm_diff": rel, "tol": tol,
-                 "nit": s["nit"], "nrev": s["nrev"]}
+        bits = d["norms"] == s["norms"] and d["xnorm"] == s["xnorm"]
+        case_ok = same and ranks_equal and (bits if segmented else rel <= tol)
+        entry = {"case": kind, **kw, "world": world, "grid": N, "transport": a.transport, "segmented": segmented,
+                 "ranks_identical": ranks_equal, "bookkeeping_equal": same, "bit_identical": bits,
+                 "max_rel_norm_diff": rel, "tol": 0.0 if segmented else tol, "nit": s["nit"], "nrev": s["nrev"]}
         if a.oracle:
             o = oracle_result(kind, N, kw)
             o_keys = keys if kind == "gn" else ("nit", "nrev", "njev", "success", "nfev", "stdout")

@@ -545,18 +545,16 @@ def test_lls_next_device(k, pending):
         np.testing.assert_allclose(d_.cpu().numpy(), h_.numpy(), rtol=1e-15, atol=0)
 
 
-@pytest.mark.parametrize("world,n", [(1, 5), (2, 1), (3, 441), (8, 3000)])
+@pytest.mark.parametrize("world,n", [(1, 5), (2, 1), (3, 441), (8, 3000), (6, 70), (13, 33)])
 def test_rank_sum_matches_host_order(world, n):
-    """gnk_rank_sum == the host's left-to-right sum over ranks (slab.Comm), bit for bit."""
+    """gnk_rank_sum == the host's sum over ranks (slab.tree_sum, slab.Comm), bit for bit."""
+    from gauss_newton_via_generalized_krylov_subspaces_amd.slab import tree_sum
     prob, dev, ref = make(24)
     be = dev.backend
     parts = np.random.default_rng(world * n).standard_normal((world, n)) * 10.0 ** np.arange(world)[:, None]
     out = be.zeros(n)
     be.rank_sum(be.to_device(parts.reshape(-1)), world, out)
-    s = parts[0].copy()
-    for p in range(1, world):
-        s = s + parts[p]
-    np.testing.assert_array_equal(out.cpu().numpy(), s)
+    np.testing.assert_array_equal(out.cpu().numpy(), tree_sum(parts))
 
 
 def test_timer_classes_and_stream_probe():

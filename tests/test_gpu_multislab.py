@@ -5,8 +5,9 @@ Each case starts fresh child processes (torch.distributed.run, gloo with host-st
 RCCL refuses two ranks on one device) that run the HIP kernels on real slabs -- row0 > 0,
 halo-filled ghost rows, rank-ordered reductions -- for GNK (all four versions, restart 20) and GN
 (with Jacobi; without it too at grid 256, where its sensitivity case is recorded), then compare with the single-rank solve (tests/multislab_worker.py):
-bookkeeping and printed messages identical, every rank identical, per-iteration ||x_k|| within the
-bounds the oracle sensitivity tests back; per-rank staged inputs (inputs.py) reproduce the full-grid
+bookkeeping and printed messages identical, every rank identical, per-iteration ||x_k|| bit for bit at
+world 2 and 8 (segmented reductions, gnk_set_segments) and at world 3 within the bounds the oracle
+sensitivity tests back; per-rank staged inputs (inputs.py) reproduce the full-grid
 inputs' run bit for bit.  World 8 is the C4 rank count (8 x 32 rows of a 256^2 grid).
 """
 import json
@@ -35,5 +36,7 @@ def test_multislab_hip_matches_single_rank_and_oracle(world, grid, transport, tm
     for c in rep["cases"]:
         assert c["ranks_identical"] and c["bookkeeping_equal"], c
         assert c["max_rel_norm_diff"] <= c["tol"], c
+        # world 2 and 8 (dividing 8, N % 8 == 0): segmented reductions, the single rank's bits exactly
+        assert c["segmented"] == (world in (2, 8)) and (c["bit_identical"] or not c["segmented"]), c
         assert c["oracle_bookkeeping_equal"] and c["oracle_max_rel_norm_diff"] <= c["oracle_tol"], c
     assert rep["ok"]

@@ -1,0 +1,147 @@
+"""Rank-count-independent reductions (gnk_set_segments, slab.reduction_segments) on the GPU.
+
+The slabs of a 1-, 2-, 4- and 8-rank row partition of the same grid run on cuda:0, each on a context
+of its own with reduction segments of N / 8 rows; every reduction of the GNK path is evaluated on
+every slab and the ranks' values are combined in slab.tree_sum's order (max for the max entries), as
+slab.Comm combines them.  All four partitions must give the same bits: the residual's sum of squares,
+the Gram passes of every Gram kernel of the GNK path (k_gram_v k <= 7, k_gram_v1 k = 8, 9, k_gram_s
+one and two column blocks), the first trial's V^T g and pending-column stats (persistent k_gemv_vjpg),
+the restart GEMV's stats (k_gemv_p), gnk_vec_stats, gnk_cgs_update, gnk_vjp_gemv_t and
+gnk_normalize_jnorm.  The one-rank values are also checked against fp64 NumPy (the oracle's
+arithmetic) to 1e-12, so the invariance is of correct sums.  N = 1024 (two-row residual kernel) and
+384 (one-row fallback, N % 512 != 0).
+"""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+import gauss_newton_via_generalized_krylov_subspaces_amd as gnk  # noqa: E402
+from gauss_newton_via_generalized_krylov_subspaces_amd._device import BratuDevice  # noqa: E402
+from gauss_newton_via_generalized_krylov_subspaces_amd.slab import Comm, tree_sum  # noqa: E402
+from oracle import gnk_oracle as O  # noqa: E402
+
+GRAM_KS = (3, 8, 9, 12, 16, 18, 20)
+
+
+def _fake_comm(world, rank):
+    """A Comm that reports (world, rank) without a process group: the slab geometry of that rank."""
+    c = Comm(single=True, segments=True)
+    c.world, c.rank = world, rank
+    return c
+
+
+def _inputs(N, kmax, seed):
+    rng = np.random.default_rng(seed)
+    n = N * N
+    V = np.linalg.qr(rng.standard_normal((n, kmax + 1)))[0].T.copy()
+    V[kmax] = rng.standard_normal(n)                          # a raw (pending) last column
+    return {"V": V, "u": 0.3 * rng.standard_normal(n), "x": 0.2 * rng.standard_normal(n),
+            "y": rng.standard_normal(n), "r": rng.standard_normal(n) * 1e2,
+            "c": rng.standard_normal(kmax + 1), "hh": 0.1 * rng.standard_normal(kmax)}
+
+
+def _rank_values(N, world, rank, inp, kmax):
+    """Every GNK-path reduction on this rank's slab (segments of N / 8 rows) -> dict of host arrays."""
+    prob = gnk.BratuPdeProblem(N + 1, 5, 10)
+    dev = BratuDevice(prob, _fake_comm(world, rank))
+    assert dev.seg_rows == N // 8
+    be = dev.backend
+    out = {}
+    u, x, y, r = (dev.load(inp[k]) for k in ("u", "x", "y", "r"))
+    V = be.zeros(kmax + 1, dev.slab.length)
+    for j in range(kmax + 1):
+        V[j].copy_(dev.load(inp["V"][j]))
+    s1 = be.zeros(4)
+    rb = dev.vec()
+    be.residual(x, y, rb, s1)
+    out["resid"] = s1[:1].cpu().numpy()
+    st = be.zeros(4)
+    be.vec_stats(x, st)
+    out["stats"] = st[:2].cpu().numpy()
+    for k in GRAM_KS:
+        kp = be.gram_dim(k, True)
+        T = np.zeros((kp, kp))
+        T[:k, :k] = np.triu(np.full((k, k), 0.05)) + np.eye(k)
+        T[k, k] = 1.0
+        G = be.zeros(kp * kp)
+        be.gram(u, V[:k], k, be.to_device(T.reshape(-1)), r, G)
+        out[f"gram{k}"] = G.cpu().numpy()
+    c = be.to_device(inp["c"])
+    hh = be.to_device(inp["hh"])
+    xo, g, h, st2 = dev.vec(), dev.vec(), be.zeros(kmax + 1), be.zeros(4)
+    Vp = V.clone()
+    be.gemv_vjp_gemv_t_pending(Vp, kmax, c, hh, r, xo, g, h, st2)     # column kmax pending
+    out["trial_h"], out["trial_stats"] = h.cpu().numpy(), st2[:2].cpu().numpy()
+    own = dev.slab.own
+    out["trial_x"], out["trial_g"] = xo[own].cpu().numpy(), g[own].cpu().numpy()
+    h2 = be.zeros(kmax)
+    be.gemv_vjp_gemv_t(V, kmax, c, r, xo, g, h2)
+    out["trial0_h"] = h2.cpu().numpy()
+    Vq = V.clone()
+    st3 = be.zeros(4)
+    be.gemv_pending(Vq, kmax, c, hh, xo, st3)
+    out["gemvp_stats"] = st3[:2].cpu().numpy()
+    gg = dev.load(inp["y"])
+    st4 = be.zeros(4)
+    be.cgs_update(V, kmax, be.to_device(0.1 * inp["hh"]), gg, st4)
+    out["cgs_stats"] = st4[:2].cpu().numpy()
+    h3 = be.zeros(kmax)
+    be.vjp_gemv_t(u, r, V, kmax, g, h3)
+    out["vjpg_h"] = h3.cpu().numpy()
+    jn = be.zeros(2)
+    be.normalize_jnorm(u, dev.load(inp["x"]), 3.0, dev.vec(), jn)
+    out["jnorm"] = jn[:1].cpu().numpy()
+    torch.cuda.synchronize()
+    del V, Vp, Vq, dev, be
+    return out
+
+
+MAX_KEYS = {"stats": 1, "trial_stats": 1, "gemvp_stats": 1, "cgs_stats": 1}   # entry that is a max
+
+
+def _combine(parts):
+    """The ranks' values combined as slab.Comm does: tree_sum, NaN-propagating max for the max entries;
+    pointwise vectors (trial_x, trial_g) concatenated in rank order."""
+    out = {}
+    for key in parts[0]:
+        if key in ("trial_x", "trial_g"):
+            out[key] = np.concatenate([p[key] for p in parts])
+            continue
+        arr = np.stack([p[key] for p in parts])
+        s = tree_sum(arr)
+        if key in MAX_KEYS:
+            s[MAX_KEYS[key]] = np.max(arr[:, MAX_KEYS[key]])
+        out[key] = s
+    return out
+
+
+@pytest.mark.parametrize("N", [1024, 384])
+def test_segment_reductions_rank_count_invariant(N):
+    kmax = max(GRAM_KS)
+    inp = _inputs(N, kmax, 7 + N)
+    res = {}
+    for world in (1, 2, 4, 8):
+        res[world] = _combine([_rank_values(N, world, p, inp, kmax) for p in range(world)])
+        torch.cuda.empty_cache()
+    diffs = {}
+    for world in (2, 4, 8):
+        for key, v in res[world].items():
+            if not np.array_equal(v.view(np.int64), res[1][key].view(np.int64)):
+                diffs[(world, key)] = float(np.max(np.abs(v - res[1][key]) / (np.abs(res[1][key]) + 1e-300)))
+    print(f"N = {N}: {len(res[1])} reductions, 4 partitions; differing: {diffs}")
+    assert not diffs
+    # the invariant values are correct sums: fp64 NumPy of the same quantities (one rank)
+    one = res[1]
+    resid = O.BratuPdeProblem(N + 1, 5, 10).make_res(inp["y"])(inp["x"])
+    np.testing.assert_allclose(one["resid"][0], np.sum(resid ** 2), rtol=1e-12)
+    np.testing.assert_allclose(one["stats"][0], np.sum(inp["x"] ** 2), rtol=1e-12)
+    assert one["stats"][1] == np.max(np.abs(inp["x"]))
+    w = inp["V"][kmax] - inp["V"][:kmax].T @ inp["hh"]
+    np.testing.assert_allclose(one["trial_stats"][0], np.sum(w * w), rtol=1e-12)
+    xt = inp["V"][:kmax].T @ inp["c"][:kmax] + w * inp["c"][kmax]
+    np.testing.assert_allclose(one["trial_x"], xt, rtol=1e-12, atol=1e-12 * np.max(np.abs(xt)))
+    Vw = np.vstack([inp["V"][:kmax], w])
+    hn = Vw @ one["trial_g"]
+    np.testing.assert_allclose(one["trial_h"], hn, rtol=1e-10, atol=1e-12 * np.max(np.abs(hn)))

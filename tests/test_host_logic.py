@@ -210,3 +210,39 @@ def test_generic_wide_gram_arena_guard():
     ops.m = 500                                       # arena 80 000 / 500 -> kp 160: k <= 159
     assert ops.max_arena_k(True) == 159
     assert ops.be.gram_dim(159, True) * ops.m <= ops.be.scratch_doubles() < ops.be.gram_dim(160, True) * ops.m
+
+
+def test_tree_sum_is_the_subtree_fold_of_every_power_of_two_partition():
+    """slab.tree_sum (= gnk_rank_sum's and gnk_set_segments' fold order): folding 8 segments on one rank
+    equals folding each rank's 8 / w segments and then the w rank values, bit for bit, for w | 8 -- the
+    property that makes segment reductions rank-count independent.  Also the device's binary-counter form
+    of the same order (k_rank_sum) for every count up to 40."""
+    from gauss_newton_via_generalized_krylov_subspaces_amd.slab import reduction_segments, tree_sum
+    rng = np.random.default_rng(5)
+    for _ in range(200):
+        seg = rng.standard_normal((8, 7)) * 10.0 ** rng.integers(-8, 8, size=(8, 7))
+        one = tree_sum(seg)
+        for w in (2, 4, 8):
+            ranks = np.stack([tree_sum(seg[p * (8 // w):(p + 1) * (8 // w)]) for p in range(w)])
+            assert np.array_equal(tree_sum(ranks), one)
+
+    def counter_fold(vals):                      # k_rank_sum's stack form
+        sv, sz = [], []
+        for v in vals:
+            z = 1
+            while sz and sz[-1] == z:
+                v = sv.pop() + v
+                sz.pop()
+                z *= 2
+            sv.append(v)
+            sz.append(z)
+        s = sv.pop()
+        while sv:
+            s = sv.pop() + s
+        return s
+    for n in range(1, 41):
+        vals = rng.standard_normal(n) * 10.0 ** rng.integers(-10, 10, size=n)
+        assert counter_fold(list(vals)) == tree_sum(vals[:, None])[0]
+    assert reduction_segments(8192, 8, None) == 1024 and reduction_segments(8192, 1, None) == 0
+    assert reduction_segments(8192, 1, True) == 1024 and reduction_segments(8192, 4, False) == 0
+    assert reduction_segments(384, 3, None) == 0 and reduction_segments(100, 2, None) == 0
