@@ -509,7 +509,7 @@ def main():
                    "armijo_trials": int(sum(s["trials"] for s in tr)),
                    "parallelism": f"slab{world}",
                    "transport": (dist.get_backend() if world > 1 else "none"),
-                   "reduction_segments": int(getattr(solver.dev, "seg_rows", 0))},
+                   "reduction_segments": int(stage.seg_rows)},
         "roofline": {"kernel": "Gram pass of the CholeskyQR solve, J V T on the fly (k_gram_v: VALU, k <= 9; "
                                "k_gram_s: staged fp64 MFMA, k > 9)", "bound": "hbm",
                      "achieved": g_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": g_gbs / HBM_PEAK_GBS,

@@ -168,8 +168,9 @@ def test_headline_8192_full_restart_cycle_vs_oracle():
     are re-rounded (1e-7 at iterations 3-4: ||x_1|| cancels ||x_0|| to 1e-8, u ||x_0|| / ||x_1|| ~ 1e-8).
     Asserted, per iteration, for ||x_k|| and ||r_k||: the device is within max(1e-10, E_i) of exact_k1
     (measured ~10x inside: the device's k = 1 step is closer to the exactly rounded one than the
-    reference's) and of cholqr; hence within 2 E_i of base by the triangle inequality (round 3's bound,
-    now derived instead of assumed).  |cholqr - exact_k1| (the factorisation's own move) is printed."""
+    reference's), hence within 2 E_i of base by the triangle inequality (round 3's bound, now derived
+    instead of assumed); within max(1e-10, E_i / 3) of cholqr, and at iteration 1 (k = 1) equal to it to
+    1e-14.  |cholqr - exact_k1| (the factorisation's own move) is printed."""
     from gauss_newton_via_generalized_krylov_subspaces_amd._device import BratuDevice
     from gauss_newton_via_generalized_krylov_subspaces_amd.inputs import slab_inputs
     from gauss_newton_via_generalized_krylov_subspaces_amd.slab import Comm
@@ -219,4 +220,10 @@ def test_headline_8192_full_restart_cycle_vs_oracle():
     print(f"  device least-squares passes per solve {s.lls.passes / max(1, len(s.lls.history)):.3f}; "
           f"oracle cholqr passes {[p[1] for p in ch['ls_passes']]}")
     assert np.all(dxe <= E_x) and np.all(dre <= E_r), (np.nonzero(dxe > E_x), np.nonzero(dre > E_r))
-    assert np.all(dxc <= E_x) and np.all(drc <= E_r), (np.nonzero(dxc > E_x), np.nonzero(drc > E_r))
+    # the cholqr variant runs the device's least-squares arithmetic: the kernels add less than a third of
+    # what one re-rounding of the reference's k = 1 sums moves its own trajectory (measured 40x less for
+    # ||x_k||, 4x for ||r_k||), and the k = 1 step itself is the same step (measured 1.3e-16: the device's
+    # k = 1 Gram sums round like exactly rounded ones)
+    bx, br = np.maximum(TOL, E_x / 3), np.maximum(TOL, E_r / 3)
+    assert np.all(dxc <= bx) and np.all(drc <= br), (np.nonzero(dxc > bx), np.nonzero(drc > br))
+    assert dxc[0] <= 1e-14 and dxc[n - 1] <= 1e-9, (dxc[0], dxc[n - 1])
