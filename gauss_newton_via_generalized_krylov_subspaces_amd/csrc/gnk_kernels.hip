@@ -44,6 +44,12 @@ constexpr size_t SCRATCH_DOUBLES = size_t(16) << 20;   // 128 MiB arena
 constexpr int ident_offset(int nb) { return nb == 1 ? 0 : ident_offset(nb - 1) + 256 * (nb - 1) * (nb - 1); }
 
 typedef double d2 __attribute__((ext_vector_type(2)));
+// Streaming store of a result vector no kernel of the same launch reads again (the trial point, the new
+// basis column, the pending column, the residual): non-temporal, so the written lines do not displace
+// what the launch still reads from L2 (the neighbour rows of r, the basis rows of adjacent blocks).
+// k_gemv_vjpg at 8192^2: 10-17 % less time than plain stores (profiles/round4/trial_nt_ab.jsonl).
+__device__ __forceinline__ void st_nt(double* p, d2 v) { __builtin_nontemporal_store(v, reinterpret_cast<d2*>(p)); }
+__device__ __forceinline__ void st_nt(double* p, double v) { __builtin_nontemporal_store(v, p); }
 typedef double d4 __attribute__((ext_vector_type(4)));
 
 struct Geo {
@@ -560,10 +566,10 @@ __global__ __launch_bounds__(BLOCK) void k_gemv_p(const double* __restrict__ V, 
     d2 ww = *reinterpret_cast<const d2*>(w + li);
     ww.x = ww.x - s.x;
     ww.y = ww.y - s.y;
-    *reinterpret_cast<d2*>(w + li) = ww;
+    st_nt(w + li, ww);
     acc.x = acc.x + ww.x * ck;
     acc.y = acc.y + ww.y * ck;
-    *reinterpret_cast<d2*>(x + li) = acc;
+    st_nt(x + li, acc);
     if (owned) {
       ss += ww.x * ww.x;
       ss += ww.y * ww.y;
@@ -579,8 +585,8 @@ __global__ __launch_bounds__(BLOCK) void k_gemv_p(const double* __restrict__ V, 
         s = s + vv * hh[j];
       }
       const double wi = w[li + q] - s;
-      w[li + q] = wi;
-      x[li + q] = acc + wi * ck;
+      st_nt(w + li + q, wi);
+      st_nt(x + li + q, acc + wi * ck);
       if (owned) {
         ss += wi * wi;
         mx = nan_max(mx, fabs(wi));
@@ -690,7 +696,7 @@ __global__ __launch_bounds__(BLOCK) void k_gemv_vjpg(const double* __restrict__ 
 #pragma unroll
     for (int j = 0; j < KCT; ++j) {
       const char* rowj = reinterpret_cast<const char*>(V + (int64_t(min(j, jmax)) * ldv + lr * N));
-      vv[j] = *reinterpret_cast<const d2*>(rowj + boff);
+      vv[j] = __builtin_nontemporal_load(reinterpret_cast<const d2*>(rowj + boff));   // streamed once
     }
     int z = 0;
     asm volatile("" : "+s"(z));                     // opaque 0: the LDS reads stay in the row loop
@@ -706,7 +712,7 @@ __global__ __launch_bounds__(BLOCK) void k_gemv_vjpg(const double* __restrict__ 
       d2 ww = *reinterpret_cast<const d2*>(wcol + li);
       ww.x = ww.x - s.x;
       ww.y = ww.y - s.y;
-      *reinterpret_cast<d2*>(wcol + li) = ww;
+      st_nt(wcol + li, ww);
 #pragma unroll
       for (int j = 0; j < KCT; ++j)
         if (j == k) vv[j] = ww;
@@ -725,7 +731,7 @@ __global__ __launch_bounds__(BLOCK) void k_gemv_vjpg(const double* __restrict__ 
       xs.x = xs.x + vv[j].x * cj;
       xs.y = xs.y + vv[j].y * cj;
     }
-    *reinterpret_cast<d2*>(x + li) = xs;
+    st_nt(x + li, xs);
     if (owned) {
       const d2 rc = *reinterpret_cast<const d2*>(r + li);
       const d2 rn = *reinterpret_cast<const d2*>(r + li - N);
@@ -737,7 +743,7 @@ __global__ __launch_bounds__(BLOCK) void k_gemv_vjpg(const double* __restrict__ 
       if (lane == 63 || iy + 2 >= N) re = he ? r[li + 2] : 0.0;
       const double g0 = -vjp_pt(c, jdiag(c, xs.x), rn.x, rw, hw, rc.x, rc.y, true, rs.x);
       const double g1 = -vjp_pt(c, jdiag(c, xs.y), rn.y, rc.x, true, rc.y, re, he, rs.y);
-      *reinterpret_cast<d2*>(g + li) = d2{g0, g1};
+      st_nt(g + li, d2{g0, g1});
 #pragma unroll
       for (int j = 0; j < KCT; ++j) {
         acc[j] = acc[j] + vv[j].x * g0;
@@ -757,7 +763,7 @@ __global__ __launch_bounds__(BLOCK) void k_gemv_vjpg(const double* __restrict__ 
 #pragma unroll
         for (int j = 0; j < KCT; ++j) s = s + vv[j] * cl[KCT + j];
         const double wi = wcol[i] - s;
-        wcol[i] = wi;
+        st_nt(wcol + i, wi);
 #pragma unroll
         for (int j = 0; j < KCT; ++j)
           if (j == k) vv[j] = wi;
@@ -769,12 +775,12 @@ __global__ __launch_bounds__(BLOCK) void k_gemv_vjpg(const double* __restrict__ 
       double xs = 0.0;
 #pragma unroll
       for (int j = 0; j < KCT; ++j) xs = xs + vv[j] * cl[j];
-      x[i] = xs;
+      st_nt(x + i, xs);
       if (owned) {
         const bool hw = yy > 0, he = yy < N - 1;
         const double rw = hw ? r[i - 1] : 0.0, re = he ? r[i + 1] : 0.0;
         const double gi = -vjp_pt(c, jdiag(c, xs), r[i - N], rw, hw, r[i], re, he, r[i + N]);
-        g[i] = gi;
+        st_nt(g + i, gi);
 #pragma unroll
         for (int j = 0; j < KCT; ++j) acc[j] = acc[j] + vv[j] * gi;
       }

@@ -1,8 +1,8 @@
 """Ablation / experiment builds of libgnk.so (tooling only: the product source is never edited).
 
-python tools/build_variants.py NAME [NAME ...]      -> tools/_diag/libgnk_NAME.so
+python tools/build_variants.py NAME [NAME ...]      -> tools/_var/libgnk_NAME.so
 Each variant is the product source with the text substitutions listed in VARIANTS applied (every
-substitution must match, else the build stops).  Load one with GNK_LIB=tools/_diag/libgnk_NAME.so.
+substitution must match, else the build stops).  Load one with GNK_LIB=tools/_var/libgnk_NAME.so.
 """
 import os
 import subprocess
@@ -11,7 +11,7 @@ from concurrent.futures import ThreadPoolExecutor
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SRC = os.path.join(ROOT, "gauss_newton_via_generalized_krylov_subspaces_amd", "csrc", "gnk_kernels.hip")
-OUT = os.path.join(ROOT, "tools", "_diag")
+OUT = os.path.join(ROOT, "tools", "_var")   # gitignored, travels to the GPU box
 
 _STEP_BARRIER = ("__builtin_amdgcn_s_waitcnt(waitcnt_vm_lgkm0(L * INF));     // row x+3 landed\n"
                  "        __builtin_amdgcn_s_barrier();")
@@ -55,9 +55,28 @@ VARIANTS = {
     "jvpntres": [('      o.y = jvp_pt(c, d1, vn.y, vc.x, true, vc.y, ve, he, vs.y);\n    }\n    *reinterpret_cast<d2*>(out + li) = o;', '      o.y = jvp_pt(c, d1, vn.y, vc.x, true, vc.y, ve, he, vs.y);\n    }\n    __builtin_nontemporal_store(o, reinterpret_cast<d2*>(out + li));'), ('  RowLaunch L = rows(ctx, G, ctx->geo.nrows, vec_of(ctx), 1 << 30);\n  TimedLaunch tl(ctx, GNK_TIMER_JVP, 24.0 * double(ctx->geo.nrows) * double(ctx->geo.N));\n  DISPATCH_VEC(ctx, k_jvp, L, 0, u, v, out, ctx->geo, ctx->coef, L.lr0, L.nlr, 0);', '  RowLaunch L = rows(ctx, G, ctx->geo.nrows, vec_of(ctx), resident_blocks(ctx, (const void*)&k_jvp<2>));\n  TimedLaunch tl(ctx, GNK_TIMER_JVP, 24.0 * double(ctx->geo.nrows) * double(ctx->geo.N));\n  DISPATCH_VEC(ctx, k_jvp, L, 0, u, v, out, ctx->geo, ctx->coef, L.lr0, L.nlr, 0);')],
     # k_jvp2: two grid rows per lane pass (4 v row loads per 2 output rows instead of 6)
     "jvp2r": [('template <int VEC>\n__global__ __launch_bounds__(BLOCK) void k_forward(', '// J(u) v for two grid rows per lane pass (rows lr, lr + 1; N % 128 == 0): the centre and south v rows\n// serve both outputs, so 4 v row loads per 2 output rows instead of 6; same per-point arithmetic as k_jvp\n__global__ __launch_bounds__(BLOCK) void k_jvp2(const double* __restrict__ u, const double* __restrict__ v,\n                                                double* __restrict__ out, Geo geo, Coef c, int64_t lr0, int64_t nlr) {\n  const int lane = threadIdx.x & 63;\n  const int64_t N = geo.N;\n  const int64_t iy = (int64_t(blockIdx.x) * BLOCK + threadIdx.x) * 2;\n  const bool hw = iy > 0, he = iy + 2 < N;\n  for (int64_t p = blockIdx.y; 2 * p < nlr; p += gridDim.y) {\n    const int64_t lr = lr0 + 2 * p;\n    const bool two = 2 * p + 1 < nlr;\n    const int64_t li = lr * N + iy;\n    const d2 vn = *reinterpret_cast<const d2*>(v + li - N);\n    const d2 vc = *reinterpret_cast<const d2*>(v + li);\n    const d2 vs = *reinterpret_cast<const d2*>(v + li + N);\n    const d2 vss = *reinterpret_cast<const d2*>(v + li + 2 * N);     // row lr + 2 <= the last ghost row\n    const d2 u0 = *reinterpret_cast<const d2*>(u + li);\n    const d2 u1 = *reinterpret_cast<const d2*>(u + li + N);\n    double vw0 = __shfl_up(vc.y, 1), ve0 = __shfl_down(vc.x, 1);\n    double vw1 = __shfl_up(vs.y, 1), ve1 = __shfl_down(vs.x, 1);\n    if (lane == 0) {\n      vw0 = hw ? v[li - 1] : 0.0;\n      vw1 = hw ? v[li + N - 1] : 0.0;\n    }\n    if (lane == 63) {\n      ve0 = he ? v[li + 2] : 0.0;\n      ve1 = he ? v[li + N + 2] : 0.0;\n    }\n    d2 o0, o1;\n    o0.x = jvp_pt(c, jdiag(c, u0.x), vn.x, vw0, hw, vc.x, vc.y, true, vs.x);\n    o0.y = jvp_pt(c, jdiag(c, u0.y), vn.y, vc.x, true, vc.y, ve0, he, vs.y);\n    *reinterpret_cast<d2*>(out + li) = o0;\n    if (two) {\n      o1.x = jvp_pt(c, jdiag(c, u1.x), vc.x, vw1, hw, vs.x, vs.y, true, vss.x);\n      o1.y = jvp_pt(c, jdiag(c, u1.y), vc.y, vs.x, true, vs.y, ve1, he, vss.y);\n      *reinterpret_cast<d2*>(out + li + N) = o1;\n    }\n  }\n}\n\ntemplate <int VEC>\n__global__ __launch_bounds__(BLOCK) void k_forward('), ('  RowLaunch L = rows(ctx, G, ctx->geo.nrows, vec_of(ctx), 1 << 30);\n  TimedLaunch tl(ctx, GNK_TIMER_JVP, 24.0 * double(ctx->geo.nrows) * double(ctx->geo.N));\n  DISPATCH_VEC(ctx, k_jvp, L, 0, u, v, out, ctx->geo, ctx->coef, L.lr0, L.nlr, 0);', '  RowLaunch L = rows(ctx, G, ctx->geo.nrows, vec_of(ctx), 1 << 30);\n  TimedLaunch tl(ctx, GNK_TIMER_JVP, 24.0 * double(ctx->geo.nrows) * double(ctx->geo.N));\n  if (ctx->geo.N % 128 == 0) {\n    L.grid.y = unsigned(std::min<int64_t>((L.nlr + 1) / 2, 65535));\n    hipLaunchKernelGGL(k_jvp2, L.grid, dim3(BLOCK), 0, ctx->stream, u, v, out, ctx->geo, ctx->coef, L.lr0, L.nlr);\n  } else\n  DISPATCH_VEC(ctx, k_jvp, L, 0, u, v, out, ctx->geo, ctx->coef, L.lr0, L.nlr, 0);')],
+    # k_gemv_vjpg: one point per lane (8-B loads; half the V registers -> more waves per SIMD)
+    "tv1": [("""  const void* fn = vec_of(ctx) == 2 ? (pend ? vjpg_pick<2, true>(kct) : vjpg_pick<2, false>(kct))
+                                    : (pend ? vjpg_pick<1, true>(kct) : vjpg_pick<1, false>(kct));
+  RowLaunch L = rows(ctx, 0, ctx->geo.nrows + 2 * G, vec_of(ctx), resident_blocks(ctx, fn));""",
+             """  const void* fn = (pend ? vjpg_pick<1, true>(kct) : vjpg_pick<1, false>(kct));
+  RowLaunch L = rows(ctx, 0, ctx->geo.nrows + 2 * G, 1, resident_blocks(ctx, fn));""")],
+    # k_gemv_vjpg: non-temporal loads of the basis rows
+    "tntl": [("      vv[j] = *reinterpret_cast<const d2*>(rowj + boff);",
+              "      vv[j] = __builtin_nontemporal_load(reinterpret_cast<const d2*>(rowj + boff));")],
+    # k_gemv_vjpg: non-temporal stores of w, x, g
+    "tnts": [("      *reinterpret_cast<d2*>(wcol + li) = ww;", "      __builtin_nontemporal_store(ww, reinterpret_cast<d2*>(wcol + li));"),
+             ("    *reinterpret_cast<d2*>(x + li) = xs;\n    if (owned) {\n      const d2 rc", "    __builtin_nontemporal_store(xs, reinterpret_cast<d2*>(x + li));\n    if (owned) {\n      const d2 rc"),
+             ("      *reinterpret_cast<d2*>(g + li) = d2{g0, g1};", "      __builtin_nontemporal_store(d2{g0, g1}, reinterpret_cast<d2*>(g + li));")],
+    # k_gemv_vjpg: non-temporal V loads and w / x / g stores
+    "tnt2": None,
+    # k_forward2: non-temporal stores of r
+    "fnt": [("    *reinterpret_cast<d2*>(out + li) = f;", "    __builtin_nontemporal_store(f, reinterpret_cast<d2*>(out + li));"),
+            ("      *reinterpret_cast<d2*>(out + li + N) = f;", "      __builtin_nontemporal_store(f, reinterpret_cast<d2*>(out + li + N));")],
     # k_gemv_vjpg: one workgroup per row segment (as k_jvp2) instead of the resident persistent grid
     "vjpgrow": [('  RowLaunch L = rows(ctx, 0, ctx->geo.nrows + 2 * G, vec_of(ctx), resident_blocks(ctx, fn));', '  RowLaunch L = rows(ctx, 0, ctx->geo.nrows + 2 * G, vec_of(ctx), 1 << 30);')],
 }
+VARIANTS["tnt2"] = VARIANTS["tntl"] + VARIANTS["tnts"]
 
 
 def build(name):
