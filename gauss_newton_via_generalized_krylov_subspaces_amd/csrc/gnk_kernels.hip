@@ -47,7 +47,8 @@ typedef double d2 __attribute__((ext_vector_type(2)));
 // Streaming store of a result vector no kernel of the same launch reads again (the trial point, the new
 // basis column, the pending column, the residual): non-temporal, so the written lines do not displace
 // what the launch still reads from L2 (the neighbour rows of r, the basis rows of adjacent blocks).
-// k_gemv_vjpg at 8192^2: 10-17 % less time than plain stores (profiles/round4/trial_nt_ab.jsonl).
+// k_gemv_vjpg at 8192^2: 10-17 % less time than plain stores (profiles/round4/trial_nt_ab.jsonl); k_gemv and
+// k_vjp_gemv_t 1-3 % (profiles/round4/nt3_ab.jsonl; k_cgs unchanged, kept plain).
 __device__ __forceinline__ void st_nt(double* p, d2 v) { __builtin_nontemporal_store(v, reinterpret_cast<d2*>(p)); }
 __device__ __forceinline__ void st_nt(double* p, double v) { __builtin_nontemporal_store(v, p); }
 typedef double d4 __attribute__((ext_vector_type(4)));
@@ -510,7 +511,7 @@ __global__ __launch_bounds__(BLOCK) void k_gemv(const double* __restrict__ V, in
       acc.x = acc.x + vv.x * cj;
       acc.y = acc.y + vv.y * cj;
     }
-    *reinterpret_cast<d2*>(x + li) = acc;
+    st_nt(x + li, acc);
   } else {
     for (int q = 0; q < VEC && iy + q < N; ++q) {
       double acc = 0.0;
@@ -626,7 +627,7 @@ __global__ __launch_bounds__(BLOCK) void k_vjp_gemv_t(const double* __restrict__
     if (lane == 63 || iy + 2 >= N) re = he ? r[li + 2] : 0.0;
     const double g0 = -vjp_pt(c, jdiag(c, uc.x), rn.x, rw, hw, rc.x, rc.y, true, rs.x);
     const double g1 = -vjp_pt(c, jdiag(c, uc.y), rn.y, rc.x, true, rc.y, re, he, rs.y);
-    if (blockIdx.z == 0) *reinterpret_cast<d2*>(g + li) = d2{g0, g1};
+    if (blockIdx.z == 0) st_nt(g + li, d2{g0, g1});
     if (k > 0) {
 #pragma unroll
       for (int j = 0; j < KCT; ++j) {

@@ -73,6 +73,10 @@ VARIANTS = {
     # k_forward2: non-temporal stores of r
     "fnt": [("    *reinterpret_cast<d2*>(out + li) = f;", "    __builtin_nontemporal_store(f, reinterpret_cast<d2*>(out + li));"),
             ("      *reinterpret_cast<d2*>(out + li + N) = f;", "      __builtin_nontemporal_store(f, reinterpret_cast<d2*>(out + li + N));")],
+    # NT stores of the other GNK versions' streaming writes: k_vjp_gemv_t (g), k_cgs (g), k_gemv (x)
+    "nt3": [("    if (blockIdx.z == 0) *reinterpret_cast<d2*>(g + li) = d2{g0, g1};", "    if (blockIdx.z == 0) st_nt(g + li, d2{g0, g1});"),
+            ("    gg.y = gg.y - s.y;\n    *reinterpret_cast<d2*>(g + li) = gg;", "    gg.y = gg.y - s.y;\n    st_nt(g + li, gg);"),
+            ("      acc.y = acc.y + vv.y * cj;\n    }\n    *reinterpret_cast<d2*>(x + li) = acc;", "      acc.y = acc.y + vv.y * cj;\n    }\n    st_nt(x + li, acc);")],
     # k_gemv_vjpg: one workgroup per row segment (as k_jvp2) instead of the resident persistent grid
     "vjpgrow": [('  RowLaunch L = rows(ctx, 0, ctx->geo.nrows + 2 * G, vec_of(ctx), resident_blocks(ctx, fn));', '  RowLaunch L = rows(ctx, 0, ctx->geo.nrows + 2 * G, vec_of(ctx), 1 << 30);')],
 }
