@@ -1187,6 +1187,22 @@ __global__ __launch_bounds__(BLOCK) void k_cg_p(double beta, int first, const do
 // One launch instead of world - 1 elementwise adds.
 __global__ __launch_bounds__(BLOCK) void k_rank_sum(const double* __restrict__ parts, int world, int64_t n,
                                                     double* __restrict__ out) {
+  if (world <= 8) {
+    // one node: slab.tree_sum's bottom-up pairwise order (v[i] += v[i + w], w = 1, 2, 4), which the binary
+    // counter below reproduces, with the values in registers (the counter's stack lives in scratch memory)
+    for (int64_t j = int64_t(blockIdx.x) * BLOCK + threadIdx.x; j < n; j += int64_t(gridDim.x) * BLOCK) {
+      double v[8];
+#pragma unroll
+      for (int p = 0; p < 8; ++p) v[p] = p < world ? parts[int64_t(p) * n + j] : 0.0;
+#pragma unroll
+      for (int w = 1; w < 8; w *= 2)
+#pragma unroll
+        for (int i = 0; i + w < 8; i += 2 * w)
+          if (i + w < world) v[i] = v[i] + v[i + w];
+      out[j] = v[0];
+    }
+    return;
+  }
   for (int64_t j = int64_t(blockIdx.x) * BLOCK + threadIdx.x; j < n; j += int64_t(gridDim.x) * BLOCK) {
     double sv[32];
     int sz[32];
@@ -1285,9 +1301,24 @@ __global__ __launch_bounds__(64) void k_seg_fold(const double* __restrict__ in, 
                                                  const int* __restrict__ is_max, double* __restrict__ out) {
   const int j = blockIdx.x * 64 + threadIdx.x;
   if (j >= len) return;
+  const bool mx = is_max ? is_max[j] != 0 : false;
+  if (nseg <= 8) {
+    // the usual case (8 segments per grid): seg_tree_fold's order with the values in registers (the
+    // runtime-indexed array of the general form lives in scratch memory)
+    double v[8];
+#pragma unroll
+    for (int sgi = 0; sgi < 8; ++sgi) v[sgi] = sgi < nseg ? in[int64_t(j) * nseg + sgi] : 0.0;
+#pragma unroll
+    for (int w = 1; w < 8; w *= 2)
+#pragma unroll
+      for (int i = 0; i + w < 8; i += 2 * w)
+        if (i + w < nseg) v[i] = mx ? nan_max(v[i], v[i + w]) : v[i] + v[i + w];
+    out[j] = v[0];
+    return;
+  }
   double v[SEG_MAX];
   for (int sgi = 0; sgi < nseg; ++sgi) v[sgi] = in[int64_t(j) * nseg + sgi];
-  out[j] = seg_tree_fold(v, nseg, is_max ? is_max[j] != 0 : false);
+  out[j] = seg_tree_fold(v, nseg, mx);
 }
 
 // out[j] = sum over b of partial[b * stride + j] (mode is_max[j]: NaN-propagating max).
@@ -3165,15 +3196,22 @@ __global__ __launch_bounds__(64) void k_lls(const double* __restrict__ Gm, int k
       out[3 + k + i * k + l] = rr[i][l];
       out[3 + k + k * k + i * k + l] = ry[i][l];
     }
-    // column l of R^-1 (back substitution on e_l); rows below l are zero
+    // column l of R^-1 (back substitution on e_l); rows below l are zero.  Loops unrolled to LS_KMAX so
+    // every index into xc is a compile-time constant: xc lives in registers (a runtime-indexed xc went to
+    // scratch memory, 272 B per lane, and the solve took 27 us on average at the bench's k)
     double* rinv = out + 3 + k + 2 * k * k;
     double xc[LS_KMAX];
-    for (int i = k - 1; i >= 0; --i) {
+#pragma unroll
+    for (int i = LS_KMAX - 1; i >= 0; --i) {
       double a = (i == l) ? 1.0 : 0.0;
-      for (int m = i + 1; m <= l; ++m) a = a - rr[i][m] * xc[m];
-      xc[i] = (i <= l) ? a / rr[i][i] : 0.0;
+#pragma unroll
+      for (int m = i + 1; m < LS_KMAX; ++m)
+        if (m <= l) a = a - rr[i][m] * xc[m];           // m <= l < k: the same subtractions in the same order
+      xc[i] = (i < k && i <= l) ? a / rr[i][i] : 0.0;
     }
-    for (int i = 0; i < k; ++i) rinv[i * k + l] = xc[i];
+#pragma unroll
+    for (int i = 0; i < LS_KMAX; ++i)
+      if (i < k) rinv[i * k + l] = xc[i];
   }
 }
 
