@@ -1243,14 +1243,11 @@ __device__ __forceinline__ void seg_split_range(int split, int span, int nblk, i
   }
 }
 
-__global__ __launch_bounds__(64) void k_wave_reduce(const double* __restrict__ partial, int nblk, int span, int64_t sb,
-                                                    int cw, int64_t cs, const int* __restrict__ is_max,
-                                                    double* __restrict__ out, int segblk = 0) {
-  const int j = blockIdx.x, split = blockIdx.y, nsplit = gridDim.y, lane = threadIdx.x;
-  const bool mx = is_max ? is_max[j] != 0 : false;
-  const double* src = partial + int64_t(j / cw) * cs + (j % cw);
-  int b0, b1;
-  seg_split_range(split, span, nblk, segblk, b0, b1);
+// one wave's deterministic sum (or NaN-propagating max of |x| >= 0) of blocks [b0, b1) of one output: lane-strided
+// partial sums (8 loads in flight), then the xor-shuffle tree; shared by every reduction kernel below so that
+// a fused form gives the same bits as the separate launches
+__device__ __forceinline__ double wave_reduce_range(const double* __restrict__ src, int b0, int b1, int64_t sb, bool mx) {
+  const int lane = threadIdx.x & 63;
   double s = mx ? -1.0 : 0.0;    // identity (max is taken over |x| >= 0)
   for (int b = b0 + lane; b < b1; b += 64 * 8) {
     double v[8];
@@ -1265,7 +1262,71 @@ __global__ __launch_bounds__(64) void k_wave_reduce(const double* __restrict__ p
     const double t = __shfl_xor(s, o);
     s = mx ? nan_max(s, t) : s + t;
   }
-  if (lane == 0) out[int64_t(j) * nsplit + split] = (mx && s < 0.0) ? 0.0 : s;
+  return (mx && s < 0.0) ? 0.0 : s;
+}
+
+__global__ __launch_bounds__(64) void k_wave_reduce(const double* __restrict__ partial, int nblk, int span, int64_t sb,
+                                                    int cw, int64_t cs, const int* __restrict__ is_max,
+                                                    double* __restrict__ out, int segblk = 0) {
+  const int j = blockIdx.x, split = blockIdx.y, nsplit = gridDim.y, lane = threadIdx.x;
+  const bool mx = is_max ? is_max[j] != 0 : false;
+  const double* src = partial + int64_t(j / cw) * cs + (j % cw);
+  int b0, b1;
+  seg_split_range(split, span, nblk, segblk, b0, b1);
+  const double s = wave_reduce_range(src, b0, b1, sb, mx);
+  if (lane == 0) out[int64_t(j) * nsplit + split] = s;
+}
+
+// One reduction of the launch-fused forms below: output j < len reads partial[(j / cw) * cs + (j % cw) + b * sb]
+// over nblk blocks (per segment: segblk blocks).
+struct RedDesc {
+  const double* partial;
+  int nblk;
+  int64_t sb;
+  int cw;
+  int64_t cs;
+  const int* is_max;
+  double* out;
+  int len;
+};
+
+// wreduce of up to two reductions in one launch (each at most 4096 blocks: one split): output j of the
+// concatenated range [d0 outputs | d1 outputs]; the arithmetic of k_wave_reduce
+__global__ __launch_bounds__(64) void k_wave_reduce_n(RedDesc d0, RedDesc d1) {
+  const int jj = blockIdx.x;
+  const RedDesc& d = jj < d0.len ? d0 : d1;
+  const int j = jj < d0.len ? jj : jj - d0.len;
+  const bool mx = d.is_max ? d.is_max[j] != 0 : false;
+  const double s = wave_reduce_range(d.partial + int64_t(j / d.cw) * d.cs + (j % d.cw), 0, d.nblk, d.sb, mx);
+  if (threadIdx.x == 0) d.out[j] = s;
+}
+
+// sreduce in one launch (one split per segment, at most 8 segments), for up to two reductions: wave w sums
+// segment w's blocks exactly as k_wave_reduce's split w does, lane 0 of the block then folds the segment
+// values in k_seg_fold's order (nblk = segblk here)
+__global__ __launch_bounds__(512) void k_seg_reduce_n(RedDesc d0, RedDesc d1, int nseg) {
+  __shared__ double sv[8];
+  const int jj = blockIdx.x, w = threadIdx.x >> 6;
+  const RedDesc& d = jj < d0.len ? d0 : d1;
+  const int j = jj < d0.len ? jj : jj - d0.len;
+  const bool mx = d.is_max ? d.is_max[j] != 0 : false;
+  if (w < nseg) {
+    const double s = wave_reduce_range(d.partial + int64_t(j / d.cw) * d.cs + (j % d.cw), w * d.nblk,
+                                       (w + 1) * d.nblk, d.sb, mx);
+    if ((threadIdx.x & 63) == 0) sv[w] = s;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double v[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) v[q] = q < nseg ? sv[q] : 0.0;
+#pragma unroll
+    for (int wd = 1; wd < 8; wd *= 2)
+#pragma unroll
+      for (int i = 0; i + wd < 8; i += 2 * wd)
+        if (i + wd < nseg) v[i] = mx ? nan_max(v[i], v[i + wd]) : v[i] + v[i + wd];
+    d.out[j] = v[0];
+  }
 }
 
 // Compensated variant: output j folds the (s, c) pairs partial[j * cs + b * sb + {0, 1}] for b in
@@ -2832,6 +2893,9 @@ __global__ __launch_bounds__(BLOCK) void k_gram_v1(const double* __restrict__ u,
 // packed upper triangle (K1 columns) -> symmetric G[KP][KP]
 __global__ __launch_bounds__(64) void k_gram_scatter_v(const double* __restrict__ red, int K1, int KP,
                                                        double* __restrict__ Gout) {
+  // entries outside [0, K1)^2 are zero (written here instead of a memset launch before the scatter)
+  for (int idx = threadIdx.x; idx < KP * KP; idx += 64)
+    if (idx / KP >= K1 || idx % KP >= K1) Gout[idx] = 0.0;
   for (int i = 0, q = 0; i < K1; ++i)
     for (int j = i; j < K1; ++j, ++q)
       if (q % 64 == int(threadIdx.x)) {
@@ -2858,6 +2922,11 @@ __global__ __launch_bounds__(BLOCK) void k_gram_scatter_s(const double* __restri
   // column c of the Gram -> (block, column in block) of the VALU sums
   auto blk = [&](int c) { return c0 ? (c < c0 ? 0 : 1) : (c >> 4); };
   auto cin = [&](int c) { return c0 ? (c < c0 ? c : c - c0) : (c & 15); };
+  // entries outside [0, K1)^2 are zero (written here instead of a memset launch before the scatter); the
+  // writes below cover [0, K1)^2
+  const int K1 = k + has_r;
+  for (int idx = blockIdx.x * BLOCK + threadIdx.x; idx < KP * KP; idx += gridDim.x * BLOCK)
+    if (idx / KP >= K1 || idx % KP >= K1) Gout[idx] = 0.0;
   for (int idx = blockIdx.x * BLOCK + threadIdx.x; idx < 256 + 24 * 33 + 33; idx += gridDim.x * BLOCK) {
     if (idx < 256) {
       const int lane = idx >> 2, i = idx & 3;
@@ -3486,11 +3555,37 @@ constexpr size_t SEG_WS2 = SCRATCH_DOUBLES - (size_t(1) << 20);
 constexpr size_t SEG_WS_END = SCRATCH_DOUBLES - (size_t(1) << 19);
 bool seg_on(const gnk_ctx* ctx) { return ctx->seg > 0; }
 
+// Up to two reductions (b.len == 0: one) in one launch when their shapes allow it -- at most 4096 blocks
+// (per segment) and at most 8 segments -- else as separate sreduce calls; the same bits either way
+// (k_wave_reduce_n / k_seg_reduce_n share k_wave_reduce's per-wave arithmetic and k_seg_fold's order).
+// desc.nblk: blocks per segment with segments, else all blocks.
+int sreduce(gnk_ctx* ctx, const double* partial, int segblk, int len, int64_t sb, int cw, int64_t cs,
+            const int* is_max, double* out);
+int sreduce_n(gnk_ctx* ctx, const RedDesc& a, const RedDesc& b) {
+  constexpr int SPAN = 4096;
+  const bool fits = a.nblk >= 1 && a.nblk <= SPAN && (b.len == 0 || (b.nblk >= 1 && b.nblk <= SPAN));
+  if (fits && a.len + b.len > 0 && !seg_on(ctx)) {
+    hipLaunchKernelGGL(k_wave_reduce_n, dim3(a.len + b.len), dim3(64), 0, ctx->stream, a, b);
+    return check_launch(ctx, "reduce (fused)");
+  }
+  if (fits && a.len + b.len > 0 && ctx->nseg <= 8) {
+    hipLaunchKernelGGL(k_seg_reduce_n, dim3(a.len + b.len), dim3(512), 0, ctx->stream, a, b, ctx->nseg);
+    return check_launch(ctx, "segment reduce (fused)");
+  }
+  int rc = sreduce(ctx, a.partial, a.nblk, a.len, a.sb, a.cw, a.cs, a.is_max, a.out);
+  if (rc || b.len == 0) return rc;
+  return sreduce(ctx, b.partial, b.nblk, b.len, b.sb, b.cw, b.cs, b.is_max, b.out);
+}
+
 int sreduce(gnk_ctx* ctx, const double* partial, int segblk, int len, int64_t sb, int cw, int64_t cs,
             const int* is_max, double* out) {
   if (!seg_on(ctx)) return wreduce(ctx, partial, segblk, len, sb, cw, cs, is_max, out);
   constexpr int SPAN = 4096;
   const int nseg = ctx->nseg;
+  if (len > 0 && nseg <= 8 && segblk >= 1 && segblk <= SPAN) {   // one launch: the per-segment sums and their fold
+    const RedDesc a{partial, segblk, sb, cw, cs, is_max, out, len}, none{partial, 1, 1, 1, 0, nullptr, out, 0};
+    return sreduce_n(ctx, a, none);
+  }
   const int span = std::min(SPAN, std::max(1, segblk));
   const int nsps = (std::max(1, segblk) + span - 1) / span;
   double* t1 = ctx->scratch + SEG_WS;
@@ -3890,9 +3985,10 @@ static int gemv_vjpg_launch(gnk_ctx* ctx, const char* what, const double* V, int
   tl.done();
   int rc = check_launch(ctx, what);
   if (rc) return rc;
-  rc = sreduce(ctx, ctx->scratch, nblk, kk, kct, kct, int64_t(nblk) * kct, nullptr, h_out);
-  if (rc || !pend) return rc;
-  return sreduce_rows(ctx, spart, nblk, 2, 2, sum_max_flags(), stats_out);
+  // the h partials and (pending) the {sum w^2, max |w|} partials: one launch
+  const RedDesc dh{ctx->scratch, nblk, kct, kct, int64_t(nblk) * kct, nullptr, h_out, kk};
+  const RedDesc ds{spart, nblk, 2, 2, 0, sum_max_flags(), stats_out, pend ? 2 : 0};
+  return sreduce_n(ctx, dh, ds);
 }
 
 int gnk_basis_gemv_vjp_gemv_t(gnk_ctx* ctx, const double* V, int64_t ldv, int k, const double* c, const double* r,
@@ -4050,7 +4146,6 @@ int gnk_gram(gnk_ctx* ctx, const double* u, const double* V, int64_t ldv, int k,
     tlv.done();
     int rcv = check_launch(ctx, "gram_v");
     if (rcv) return rcv;
-    (void)hipMemsetAsync(G_out, 0, size_t(KP) * KP * sizeof(double), ctx->stream);
     double* red = ctx->scratch + (SCRATCH_DOUBLES - size_t(NT));
     if (rpr_s > 0) {
       if (size_t(nblk) * NT > SEG_WS) return fail(ctx, "gram: scratch too small (valu, segments)");
@@ -4148,7 +4243,6 @@ int gnk_gram(gnk_ctx* ctx, const double* u, const double* V, int64_t ldv, int k,
       tls.done();
       int rcs = check_launch(ctx, "gram_s");
       if (rcs) return rcs;
-      (void)hipMemsetAsync(G_out, 0, size_t(KP) * KP * sizeof(double), ctx->stream);
       double* red = ctx->scratch + (SCRATCH_DOUBLES - size_t(PL));
       if (plog) {
         if (size_t(nwg) * PL > SEG_WS) return fail(ctx, "gram: scratch too small (staged, segments)");

@@ -1,9 +1,10 @@
 """Per-cycle kernel-time breakdown of the bench's timed window from a rocprofv3 kernel trace.
 
-  python tools/rocprof_breakdown.py <run_kernel_trace.csv> <bench window json (GNK_BENCH_WINDOW_OUT)> [cycles]
+  python tools/rocprof_breakdown.py <run_kernel_trace.csv> <bench window json (GNK_BENCH_WINDOW_OUT)> [cycles] [min_ns]
 
 The window runs from the first timed Gram launch to the launch after the last one (tools/rocprof_window.py's
-selection of the bench-grid Gram launches); every kernel that starts inside it is summed per name, and
+selection of the bench-grid Gram launches: longer than min_ns, default 10 us, which drops the 256^2
+pre-warm's); every kernel that starts inside it is summed per name, and
 the totals are divided by the number of restart cycles timed (``cycles``, default: the bench's repeats).
 Also reports the GPU-busy fraction (union of kernel intervals over the window span) and launches per cycle.
 """
@@ -21,14 +22,14 @@ def short(name):
     return n.split("(")[0].split("<")[0]
 
 
-def main(trace, window, cycles=None):
+def main(trace, window, cycles=None, min_ns=10_000):
     win = json.load(open(window))
     rows = []
     for r in csv.DictReader(open(trace)):
         rows.append((int(r.get("Dispatch_Id") or r["Correlation_Id"]), int(r["Start_Timestamp"]),
                      int(r["End_Timestamp"]), r["Kernel_Name"]))
     rows.sort()
-    grams = [r for r in rows if GRAM.search(r[3]) and r[2] - r[1] > 50_000]
+    grams = [r for r in rows if GRAM.search(r[3]) and r[2] - r[1] > int(min_ns)]
     lo, cnt = win["gram_launch_offset"], win["gram_launches"]
     t0 = grams[lo][1]
     t1 = grams[lo + cnt][1] if lo + cnt < len(grams) else max(r[2] for r in rows)
