@@ -123,6 +123,11 @@ class BratuOps:
 class GNKSolver:
     """One rank of the device GNK loop; ``step()`` runs exactly one outer iteration."""
 
+    # an adopted speculative solve hands its device-formed hh' / sc' to the first trial and to the next
+    # speculation instead of uploading the host's copies (two host->device copies per step fewer; the
+    # same values: tests/test_gpu_spec_reuse.py runs both ways bit for bit)
+    reuse_spec_device = True
+
     def __init__(self, problem, y, krylow_restart=None, tol=1e-8, max_iter=100, version="res_old",
                  comm: Optional[Comm] = None, device=None, backend=None, callback: Callable = None,
                  callback_format: str = "numpy", ops=None):
@@ -192,7 +197,9 @@ class GNKSolver:
         the next pass runs at u = x_t with r = r_t."""
         par = self._par ^ 1
         self.basis.halo_slot(slot)
-        sc_dev = self.basis.sc_device(par, ls.k)
+        # k_lls_next reads sc[:k-1] of a pending solve: an adopted speculative solve already holds them
+        reuse = self.reuse_spec_device and getattr(ls, "sc_dev", None) is not None and ls.pending
+        sc_dev = ls.sc_dev if reuse else self.basis.sc_device(par, ls.k)
         return self.lls.launch_next(x_t, self.basis, r_t, ls, self.comm.device_sum(rd), sc_dev, par)
 
     def _drop_spec(self):
@@ -271,7 +278,8 @@ class GNKSolver:
             prod = fuse and kk <= basis.FUSE_KMAX
             e_ext = np.append(self.e, np.zeros(kk - len(self.e)))
             sdd = basis.step_scale()
-            if spec is not None and pend and spec.k == kk:
+            adopted = spec is not None and pend and spec.k == kk
+            if adopted:
                 ls = spec
                 lls.adopt(ls, basis)
             else:
@@ -282,7 +290,8 @@ class GNKSolver:
                 rr, h, slot = self._trial_plain(e_ext + 1.0 * ds, x_t, r_t, r_old, prod)
                 return ls.d, ls.jdd, ds, rr, h, slot
             if ls.device:
-                pack, slot = basis.trial_first(None, x_t, r_old if prod else None, coef_dev=ls.e_try)
+                pack, slot = basis.trial_first(None, x_t, r_old if prod else None, coef_dev=ls.e_try,
+                                               hh_dev=ls.hh_dev if (adopted and self.reuse_spec_device) else None)
                 rd = self.ops.residual_read(x_t, r_t, pack[:3 + kk], ls.out, self._pinned())
                 if prod and self._can_speculate(it, kk):
                     self._spec = self._launch_spec(ls, rd, x_t, r_t, slot)

@@ -168,9 +168,10 @@ class DeviceKrylovBasis:
         self.be.upload(self._sc_dev[par], self.sc[:k])
         return self._sc_dev[par]
 
-    def trial_first(self, e_ext, out, r_products=None, coef_dev=None, pack=None):
+    def trial_first(self, e_ext, out, r_products=None, coef_dev=None, pack=None, hh_dev=None):
         """``enqueue_trial`` on the host's current basis (settled k, pending column if any; its hh
-        uploaded), coefficients e_ext (host, stored units) or ``coef_dev``.  Returns (pack, slot)."""
+        uploaded, or ``hh_dev``: the same coefficients already on the device -- an adopted speculative
+        solve's), coefficients e_ext (host, stored units) or ``coef_dev``.  Returns (pack, slot)."""
         pack = self.pack if pack is None else pack
         kk = self.gram_k()
         if coef_dev is None:
@@ -184,8 +185,10 @@ class DeviceKrylovBasis:
         if pend:
             if self.pend["slot"] != self.k:
                 raise RuntimeError("pending column is not stored in V")
-            self.be.upload(self._hh, self.pend["hh"])
-        slot = self.enqueue_trial(self.k, pend, out, coef_dev, self._hh, pack, r_products)
+            if hh_dev is None or hh_dev.numel() != len(self.pend["hh"]):
+                self.be.upload(self._hh, self.pend["hh"])
+                hh_dev = self._hh
+        slot = self.enqueue_trial(self.k, pend, out, coef_dev, hh_dev, pack, r_products)
         return pack, slot
 
     def resolve(self, sumsq: float, maxabs: float) -> bool:

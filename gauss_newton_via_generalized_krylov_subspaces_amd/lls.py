@@ -71,9 +71,14 @@ class DeviceSolve:
 
     device = True
 
-    def __init__(self, k, kp, M, M_cont, P, rescale, pending, G, out, e_try):
+    def __init__(self, k, kp, M, M_cont, P, rescale, pending, G, out, e_try, hh_dev=None, sc_dev=None):
         self.k, self.kp, self.M, self.M_cont, self.P, self.rescale = k, kp, M, M_cont, P, rescale
         self.pending, self.G, self.out, self.e_try = pending, G, out, e_try
+        # speculative solves (launch_next): the pending column's projection coefficients hh' and the
+        # column scales sc'[:k-1] that k_lls_next formed on the device -- the values the host computes
+        # for the same step once it has read the previous one (same IEEE operations on the same
+        # inputs), so the step that adopts this solve uses them instead of uploading its own
+        self.hh_dev, self.sc_dev = hh_dev, sc_dev
 
 
 class _LSBuffers:
@@ -225,7 +230,8 @@ class CholQR2Solver:
         self.be.lls_next(ls.k, ls.pending, ls.out, ls.e_try, pack_sum, sc_dev, kp, B.T, B.P, B.sdd, B.e, B.hh, B.sc)
         G = self._gram_device(u, basis, k, None, r, T_dev=B.T, G_dev=B.G)
         self.be.lls_solve(G, kp, k, B.P, True, B.sdd, B.e, B.out, B.etry)
-        return DeviceSolve(k, kp, None, None, None, True, True, G, B.out[:3 + k + 3 * k * k], B.etry[:k])
+        return DeviceSolve(k, kp, None, None, None, True, True, G, B.out[:3 + k + 3 * k * k], B.etry[:k],
+                           hh_dev=B.hh[:ls.k], sc_dev=B.sc)        # sc': entries [:k - 1] valid
 
     def adopt(self, ls: "DeviceSolve", basis):
         """A speculative solve became the current step: fill its host-side fields from the (now
