@@ -3284,6 +3284,180 @@ __global__ __launch_bounds__(64) void k_lls(const double* __restrict__ Gm, int k
   }
 }
 
+// lane `src`'s value of v on every lane (src wave-uniform): two v_readlane_b32, no LDS
+__device__ __forceinline__ double rdl(double v, int src) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_readlane(int(b & 0xffffffffll), src);
+  const int hi = __builtin_amdgcn_readlane(int(b >> 32), src);
+  return __longlong_as_double((static_cast<long long>(hi) << 32) | static_cast<unsigned int>(lo));
+}
+
+// k_lls in registers: the same solve, the same IEEE operations in the same order (tools/lls_bitcheck.py
+// compares it with k_lls bit for bit), but lane l keeps column l of G / Ry, P, R and R^-1 in registers
+// and takes another lane's entry by v_readlane (every cross-lane index is a compile-time constant of the
+// loops, unrolled to KU >= k).  k_lls's column-per-lane loops read LDS inside their dependent chains (the
+// left-looking Cholesky dot products, R = Ry P, the back substitutions): 5 us at k = 1 growing to 52 us at
+// k = 20, on the stream between the Gram pass and the first trial of every step.  Here the Cholesky is
+// right-looking (row j's update g'[i][l] -= ry[j][i] ry[j][l] applied for j = 0, 1, .. as the left-looking
+// sums subtract them) and LDS holds only two one-shot transposes (the r column and the rows of R).
+template <int KU>
+__global__ __launch_bounds__(64) void k_lls_r(const double* __restrict__ Gm, int kp, int k, const double* __restrict__ P,
+                                              int rescale, const double* __restrict__ sdd,
+                                              const double* __restrict__ e, double* __restrict__ out,
+                                              double* __restrict__ etry) {
+  __shared__ double zcol[KU + 1];
+  __shared__ double rr_s[KU][KU + 1];
+  const int l = threadIdx.x;
+  const int k1 = k + 1;
+  double gc[KU + 1], pc[KU];                        // column l of G (rows 0..k), of P (rows 0..k-1)
+#pragma unroll
+  for (int i = 0; i <= KU; ++i) gc[i] = (i < k1 && l < k1) ? Gm[i * kp + l] : 0.0;
+#pragma unroll
+  for (int m = 0; m < KU; ++m) pc[m] = (m < k && l < k) ? P[m * k + l] : 0.0;
+  double s = 1.0;
+  if (rescale) {
+    double s2 = 0.0;
+#pragma unroll
+    for (int i = 0; i < KU; ++i)
+      if (i == k - 1) s2 = gc[i];
+    s2 = rdl(s2, k - 1);                            // G[k-1][k-1]
+    if (isfinite(s2) && s2 > 0.0) {
+      s = sqrt(s2);
+#pragma unroll
+      for (int i = 0; i < KU; ++i)                  // row k-1 of every column
+        if (i == k - 1 && l < k1) gc[i] = gc[i] / s;
+      if (l == k - 1) {                             // then column k-1, every row
+#pragma unroll
+        for (int i = 0; i <= KU; ++i)
+          if (i < k1) gc[i] = gc[i] / s;
+#pragma unroll
+        for (int i = 0; i < KU; ++i)
+          if (i == k - 1) pc[i] = s;
+      }
+    }
+  }
+  // the r column G[:k, k] (lane k's column) to every lane's row, before the factorisation overwrites it
+  if (l == k) {
+#pragma unroll
+    for (int i = 0; i < KU; ++i)
+      if (i < k) zcol[i] = gc[i];
+  }
+  // Cholesky, upper: after step j, gc[j] of lane l is ry[j][l] (0 below the diagonal)
+  int bad = 0;
+#pragma unroll
+  for (int j = 0; j < KU; ++j) {
+    if (j < k) {
+      const double t = gc[j];                       // g'[j][l]: g[j][l] - sum_{i<j} ry[i][j] ry[i][l]
+      const double tj = rdl(t, j);
+      if (!(tj > 0.0)) bad = 1;
+      const double rjj = sqrt(tj);
+      const double ryjl = (l > j && l < k) ? t / rjj : (l == j ? rjj : 0.0);
+      gc[j] = ryjl;
+#pragma unroll
+      for (int i = j + 1; i < KU; ++i)
+        if (i < k) {
+          const double ryji = rdl(ryjl, i);        // ry[j][i]
+          if (l >= i && l < k) gc[i] = gc[i] - ryji * ryjl;
+        }
+    }
+  }
+  __syncthreads();
+  // z = Ry^-T G[:k, k] (forward substitution, subtractions in row order); zl = z_l on lane l
+  double b = (l < k) ? zcol[l] : 0.0;
+  double zl = 0.0;
+#pragma unroll
+  for (int j = 0; j < KU; ++j)
+    if (j < k) {
+      const double svj = rdl(b / gc[j], j);         // lane j: b / ry[j][j]
+      if (l == j) zl = svj;
+      if (l > j && l < k) b = b - gc[j] * svj;
+    }
+  // R = Ry P (column l: R[i][l] = sum_{m=i..l} ry[i][m] p[m][l], m ascending)
+  double rc[KU];
+#pragma unroll
+  for (int i = 0; i < KU; ++i) {
+    double a = 0.0;
+    if (i < k) {
+#pragma unroll
+      for (int m = i; m < KU; ++m)
+        if (m < k) {
+          const double rim = rdl(gc[i], m);         // ry[i][m]
+          if (m <= l) a = a + rim * pc[m];
+        }
+    }
+    rc[i] = (i < k && i <= l) ? a : 0.0;
+  }
+  // rows of R to their lanes (R[l][j] on lane l)
+  if (l < KU) {
+#pragma unroll
+    for (int i = 0; i < KU; ++i) rr_s[i][l] = rc[i];
+  }
+  __syncthreads();
+  double rrow[KU];
+#pragma unroll
+  for (int j = 0; j < KU; ++j) rrow[j] = (l < KU) ? rr_s[l][j] : 0.0;
+  // x = R^-1 z, column-oriented back substitution; d = -x
+  double xv = (l < k) ? zl : 0.0, xl = 0.0;
+  double xs[KU];
+#pragma unroll
+  for (int j = KU - 1; j >= 0; --j) {
+    xs[j] = 0.0;
+    if (j < k) {
+      const double xj = rdl(xv / rc[j], j);         // lane j: xv / rr[j][j]
+      xs[j] = xj;
+      if (l == j) xl = xj;
+      if (l < j) xv = xv - xj * rrow[j];
+    }
+  }
+  const double d = (l < k) ? -xl : 0.0;
+  // jdd = sum_i (R d)_i^2, summed in row order
+  double a = 0.0;
+#pragma unroll
+  for (int c = 0; c < KU; ++c)
+    if (c < k && c >= l) a = a + rrow[c] * (-xs[c]);
+  const double rd2 = a * a;
+  double jdd = 0.0;
+#pragma unroll
+  for (int i = 0; i < KU; ++i)
+    if (i < k) jdd = jdd + rdl(rd2, i);
+  if (l == 0) {
+    out[0] = bad ? 1.0 : 0.0;
+    out[1] = jdd;
+    out[2] = s;
+  }
+  if (l < k) {
+    out[3 + l] = d;
+    etry[l] = e[l] + sdd[l] * d;
+#pragma unroll
+    for (int i = 0; i < KU; ++i)
+      if (i < k) {
+        out[3 + k + i * k + l] = rc[i];
+        out[3 + k + k * k + i * k + l] = gc[i];
+      }
+  }
+  // column l of R^-1 (back substitution on e_l); rows below l are zero
+  double xc[KU];
+#pragma unroll
+  for (int i = KU - 1; i >= 0; --i) {
+    double t = (i == l) ? 1.0 : 0.0;
+    if (i < k) {
+#pragma unroll
+      for (int m = i + 1; m < KU; ++m)
+        if (m < k) {
+          const double rim = rdl(rc[i], m);         // R[i][m]
+          if (m <= l) t = t - rim * xc[m];
+        }
+    }
+    xc[i] = (i < k && i <= l) ? t / rdl(rc[i], i) : 0.0;
+  }
+  if (l < k) {
+    double* rinv = out + 3 + k + 2 * k * k;
+#pragma unroll
+    for (int i = 0; i < KU; ++i)
+      if (i < k) rinv[i * k + l] = xc[i];
+  }
+}
+
 // The next GNK step's least-squares inputs, on the device (speculative enqueue; lls.py / krylow.py
 // bookkeeping restated): this step solved over k columns (the last one pending if `pending`), its
 // first trial was accepted (t = 1) and the basis update appended a pending column with raw products
@@ -3292,7 +3466,7 @@ __global__ __launch_bounds__(64) void k_lls(const double* __restrict__ Gm, int k
 //   R_true = R with its last column / ||w|| (pending);  P' = blockdiag(R_true, 1);
 //   T' = [[diag(sc') D R^-1, -hh'], [0, 1]] (+ the r column), D = diag(1, .., ||w||)  (= M' P'^-1);
 //   sdd' = [sc', 1];  e' = [e_try, 0].
-__global__ __launch_bounds__(64) void k_lls_next(int k, int pending, const double* __restrict__ out,
+__global__ __launch_bounds__(256) void k_lls_next(int k, int pending, const double* __restrict__ out,
                                                  const double* __restrict__ etry, const double* __restrict__ pack,
                                                  const double* __restrict__ sc, int kpn, double* __restrict__ T,
                                                  double* __restrict__ Pn, double* __restrict__ sddn,
@@ -3303,7 +3477,7 @@ __global__ __launch_bounds__(64) void k_lls_next(int k, int pending, const doubl
   const double* R = out + 3 + k;
   const double* rinv = out + 3 + k + 2 * k * k;
   const double nrm = pending ? sqrt(pack[1]) : 1.0;
-  for (int j = l; j < k; j += 64) {
+  for (int j = l; j < k; j += 256) {
     const double scj = (pending && j == k - 1) ? 1.0 / nrm : sc[j];
     scn[j] = scj;
     sddn[j] = scj;
@@ -3315,7 +3489,7 @@ __global__ __launch_bounds__(64) void k_lls_next(int k, int pending, const doubl
     en[k] = 0.0;
   }
   __syncthreads();
-  for (int idx = l; idx < kpn * kpn; idx += 64) {
+  for (int idx = l; idx < kpn * kpn; idx += 256) {
     const int i = idx / kpn, j = idx % kpn;
     double t = 0.0;
     if (i < k && j < k) {
@@ -3328,7 +3502,7 @@ __global__ __launch_bounds__(64) void k_lls_next(int k, int pending, const doubl
     }
     T[idx] = t;
   }
-  for (int idx = l; idx < kn * kn; idx += 64) {
+  for (int idx = l; idx < kn * kn; idx += 256) {
     const int i = idx / kn, j = idx % kn;
     double pv = 0.0;
     if (i < k && j < k) pv = (pending && j == k - 1) ? R[i * k + j] / nrm : R[i * k + j];
@@ -4782,7 +4956,8 @@ int gnk_lls_next(gnk_ctx* ctx, int k, int pending, const double* out, const doub
   if (kp_next < k + 2) return fail(ctx, "lls_next: kp_next < k + 2");
   if (!out || !e_try || !pack || !sc || !T_next || !P_next || !sdd_next || !e_next || !hh_next || !sc_next)
     return fail(ctx, "lls_next: NULL argument");
-  hipLaunchKernelGGL(k_lls_next, dim3(1), dim3(64), 0, ctx->stream, k, pending, out, e_try, pack, sc, kp_next,
+  hipLaunchKernelGGL(k_lls_next, dim3(1), dim3(256),   // 4 waves: the T / P fills are latency bound
+                     0, ctx->stream, k, pending, out, e_try, pack, sc, kp_next,
                      T_next, P_next, sdd_next, e_next, hh_next, sc_next);
   return check_launch(ctx, "lls_next");
 }
@@ -4793,7 +4968,17 @@ int gnk_lls_solve(gnk_ctx* ctx, const double* Gm, int kp, int k, const double* P
   if (k < 1 || k > LS_KMAX) return fail(ctx, "lls_solve: k must be in [1, gnk_lls_max_k()]");
   if (kp < k + 1) return fail(ctx, "lls_solve: kp < k + 1 (G must hold the r column)");
   if (!Gm || !P || !sdd || !e || !out || !e_try) return fail(ctx, "lls_solve: NULL argument");
-  hipLaunchKernelGGL(k_lls, dim3(1), dim3(64), 0, ctx->stream, Gm, kp, k, P, rescale, sdd, e, out, e_try);
+  // the register form (k_lls_r) for the GNK path's basis sizes; tuning GNK_TUNE_LLS 1 keeps k_lls (tooling A/B)
+  if (k <= 24 && tuning(ctx, GNK_TUNE_LLS) != 1) {
+    if (k <= 8)
+      hipLaunchKernelGGL(k_lls_r<8>, dim3(1), dim3(64), 0, ctx->stream, Gm, kp, k, P, rescale, sdd, e, out, e_try);
+    else if (k <= 16)
+      hipLaunchKernelGGL(k_lls_r<16>, dim3(1), dim3(64), 0, ctx->stream, Gm, kp, k, P, rescale, sdd, e, out, e_try);
+    else
+      hipLaunchKernelGGL(k_lls_r<24>, dim3(1), dim3(64), 0, ctx->stream, Gm, kp, k, P, rescale, sdd, e, out, e_try);
+  } else {
+    hipLaunchKernelGGL(k_lls, dim3(1), dim3(64), 0, ctx->stream, Gm, kp, k, P, rescale, sdd, e, out, e_try);
+  }
   return check_launch(ctx, "lls_solve");
 }
 

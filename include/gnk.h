@@ -72,7 +72,9 @@ int gnk_set_segments(gnk_ctx* ctx, int64_t seg_rows);
  *   GNK_TUNE_GRAM_WIDE   1 = never the prefetching wide Gram kernel, 2 = also for 2..3 column blocks,
  *                        3 = the pair-split kernel instead of the VGPR-RinvAug one for 5..7 blocks
  *   GNK_TUNE_GRAM_RPR    > 0: grid rows per row range of the staged / VALU Gram kernels (a finer,
- *                        fixed decomposition; A/B of what rank-count-independent partials cost) */
+ *                        fixed decomposition; A/B of what rank-count-independent partials cost)
+ *   GNK_TUNE_LLS         1 = the LDS-resident device solve (k_lls) instead of the register one (k_lls_r,
+ *                        k <= 24; the same bits) */
 #define GNK_TUNE_GRAM_PATH 0
 #define GNK_TUNE_GRAM_RING 1
 #define GNK_TUNE_GRAM_V1MIN 2
@@ -80,7 +82,8 @@ int gnk_set_segments(gnk_ctx* ctx, int64_t seg_rows);
 #define GNK_TUNE_VJPG_BLOCKS 4
 #define GNK_TUNE_GRAM_WIDE 5
 #define GNK_TUNE_GRAM_RPR 6
-#define GNK_TUNE_COUNT 7
+#define GNK_TUNE_LLS 7
+#define GNK_TUNE_COUNT 8
 int gnk_set_tuning(gnk_ctx* ctx, int key, int value);
 /* doubles in the context's scratch arena (bounds the wide generic Gram: kp * m <= this) */
 int64_t gnk_scratch_doubles(void);

@@ -32,7 +32,23 @@ def main(trace, window, cycles=None, min_ns=10_000):
     grams = [r for r in rows if GRAM.search(r[3]) and r[2] - r[1] > int(min_ns)]
     lo, cnt = win["gram_launch_offset"], win["gram_launches"]
     t0 = grams[lo][1]
-    t1 = grams[lo + cnt][1] if lo + cnt < len(grams) else max(r[2] for r in rows)
+    if lo + cnt < len(grams) and "trial" not in win:
+        t1 = grams[lo + cnt][1]
+    else:
+        # the window's last step: its first trial, then the residual and the reductions that follow it
+        TRIAL = re.compile(r"k_gemv_vjpg<")
+        t = win.get("trial") or {}
+        trials = [r for r in rows if TRIAL.search(r[3]) and r[2] - r[1] > int(min_ns)]
+        last = trials[t["trial_launch_offset"] + t["trial_launches"] - 1] if t else grams[lo + cnt - 1]
+        after = [r for r in rows if r[0] > last[0]]
+        res = next((i for i, r in enumerate(after) if "k_forward" in r[3]), None)
+        t1 = last[2]
+        if res is not None:
+            t1 = after[res][2]
+            for r in after[res + 1:]:
+                if "reduce" not in r[3]:
+                    break
+                t1 = r[2]
     sel = [r for r in rows if t0 <= r[1] < t1]
     ncyc = float(cycles) if cycles else float(win.get("repeats", 1))
     per = defaultdict(float)
