@@ -77,6 +77,14 @@ VARIANTS = {
     "nt3": [("    if (blockIdx.z == 0) *reinterpret_cast<d2*>(g + li) = d2{g0, g1};", "    if (blockIdx.z == 0) st_nt(g + li, d2{g0, g1});"),
             ("    gg.y = gg.y - s.y;\n    *reinterpret_cast<d2*>(g + li) = gg;", "    gg.y = gg.y - s.y;\n    st_nt(g + li, gg);"),
             ("      acc.y = acc.y + vv.y * cj;\n    }\n    *reinterpret_cast<d2*>(x + li) = acc;", "      acc.y = acc.y + vv.y * cj;\n    }\n    st_nt(x + li, acc);")],
+    # k_gemv_vjpg: one point per lane with the NT basis loads of the product's two-point path
+    "tv1nt": [("""  const void* fn = vec_of(ctx) == 2 ? (pend ? vjpg_pick<2, true>(kct) : vjpg_pick<2, false>(kct))
+                                    : (pend ? vjpg_pick<1, true>(kct) : vjpg_pick<1, false>(kct));
+  RowLaunch L = rows(ctx, 0, ctx->geo.nrows + 2 * G, vec_of(ctx), resident_blocks(ctx, fn));""",
+             """  const void* fn = (pend ? vjpg_pick<1, true>(kct) : vjpg_pick<1, false>(kct));
+  RowLaunch L = rows(ctx, 0, ctx->geo.nrows + 2 * G, 1, resident_blocks(ctx, fn));"""),
+              ("      for (int j = 0; j < KCT; ++j) vv[j] = V[min(j, jmax) * ldv + i];",
+               "      for (int j = 0; j < KCT; ++j) vv[j] = __builtin_nontemporal_load(V + min(j, jmax) * ldv + i);")],
     # k_gemv_vjpg: one workgroup per row segment (as k_jvp2) instead of the resident persistent grid
     "vjpgrow": [('  RowLaunch L = rows(ctx, 0, ctx->geo.nrows + 2 * G, vec_of(ctx), resident_blocks(ctx, fn));', '  RowLaunch L = rows(ctx, 0, ctx->geo.nrows + 2 * G, vec_of(ctx), 1 << 30);')],
 }
