@@ -3284,177 +3284,112 @@ __global__ __launch_bounds__(64) void k_lls(const double* __restrict__ Gm, int k
   }
 }
 
-// lane `src`'s value of v on every lane (src wave-uniform): two v_readlane_b32, no LDS
-__device__ __forceinline__ double rdl(double v, int src) {
-  const long long b = __double_as_longlong(v);
-  const int lo = __builtin_amdgcn_readlane(int(b & 0xffffffffll), src);
-  const int hi = __builtin_amdgcn_readlane(int(b >> 32), src);
-  return __longlong_as_double((static_cast<long long>(hi) << 32) | static_cast<unsigned int>(lo));
-}
-
-// k_lls in registers: the same solve, the same IEEE operations in the same order (tools/lls_bitcheck.py
-// compares it with k_lls bit for bit), but lane l keeps column l of G / Ry, P, R and R^-1 in registers
-// and takes another lane's entry by v_readlane (every cross-lane index is a compile-time constant of the
-// loops, unrolled to KU >= k).  k_lls's column-per-lane loops read LDS inside their dependent chains (the
-// left-looking Cholesky dot products, R = Ry P, the back substitutions): 5 us at k = 1 growing to 52 us at
-// k = 20, on the stream between the Gram pass and the first trial of every step.  Here the Cholesky is
-// right-looking (row j's update g'[i][l] -= ry[j][i] ry[j][l] applied for j = 0, 1, .. as the left-looking
-// sums subtract them) and LDS holds only two one-shot transposes (the r column and the rows of R).
-template <int KU>
-__global__ __launch_bounds__(64) void k_lls_r(const double* __restrict__ Gm, int kp, int k, const double* __restrict__ P,
-                                              int rescale, const double* __restrict__ sdd,
-                                              const double* __restrict__ e, double* __restrict__ out,
-                                              double* __restrict__ etry) {
-  __shared__ double zcol[KU + 1];
-  __shared__ double rr_s[KU][KU + 1];
-  const int l = threadIdx.x;
+// k_lls on 32 x 32 threads (16 waves): thread (i, l) = (t / 32, t % 32) owns entry (i, l) of the
+// factorisation's upper triangles -- the same solve with the same IEEE operations in the same order as
+// k_lls (tests/test_gpu_lls_regs.py compares them bit for bit), but the O(k^3) parts run one entry per
+// thread: the Cholesky right-looking (entry (i, l) subtracts ry[j][i] ry[j][l] for j = 0, 1, .. exactly as
+// k_lls's left-looking dot product does, the pivot row per step), R = Ry P one dot product per entry, R^-1
+// one row per step.  Only the two triangular solves of the step itself stay sequential (k barriers each).
+// k_lls (one wave, column per lane) spends 5 us at k = 1 .. 52 us at k = 20 in dependent chains through LDS
+// (a register form of it, v_readlane instead of LDS, measured the same: ~7 k dependent instructions at
+// k = 20); this form: 4 us .. 28 us, ~6 barriers of 16 waves per column.
+__global__ __launch_bounds__(1024) void k_lls_2d(const double* __restrict__ Gm, int kp, int k,
+                                                 const double* __restrict__ P, int rescale,
+                                                 const double* __restrict__ sdd, const double* __restrict__ e,
+                                                 double* __restrict__ out, double* __restrict__ etry) {
+  __shared__ double g[LS_LD][LS_LD + 1];
+  __shared__ double pm[LS_KMAX][LS_LD];
+  __shared__ double ry[LS_KMAX][LS_LD];
+  __shared__ double rr[LS_KMAX][LS_LD];
+  __shared__ double xm[LS_KMAX][LS_LD];
+  __shared__ double sv[LS_KMAX], rd2[LS_KMAX];
+  __shared__ int bad;
+  const int t = threadIdx.x, i = t >> 5, l = t & 31;
   const int k1 = k + 1;
-  double gc[KU + 1], pc[KU];                        // column l of G (rows 0..k), of P (rows 0..k-1)
-#pragma unroll
-  for (int i = 0; i <= KU; ++i) gc[i] = (i < k1 && l < k1) ? Gm[i * kp + l] : 0.0;
-#pragma unroll
-  for (int m = 0; m < KU; ++m) pc[m] = (m < k && l < k) ? P[m * k + l] : 0.0;
+  for (int idx = t; idx < k1 * k1; idx += 1024) g[idx / k1][idx % k1] = Gm[(idx / k1) * kp + idx % k1];
+  for (int idx = t; idx < k * k; idx += 1024) pm[idx / k][idx % k] = P[idx];
+  if (t == 0) bad = 0;
+  __syncthreads();
   double s = 1.0;
   if (rescale) {
-    double s2 = 0.0;
-#pragma unroll
-    for (int i = 0; i < KU; ++i)
-      if (i == k - 1) s2 = gc[i];
-    s2 = rdl(s2, k - 1);                            // G[k-1][k-1]
+    const double s2 = g[k - 1][k - 1];
     if (isfinite(s2) && s2 > 0.0) {
       s = sqrt(s2);
-#pragma unroll
-      for (int i = 0; i < KU; ++i)                  // row k-1 of every column
-        if (i == k - 1 && l < k1) gc[i] = gc[i] / s;
-      if (l == k - 1) {                             // then column k-1, every row
-#pragma unroll
-        for (int i = 0; i <= KU; ++i)
-          if (i < k1) gc[i] = gc[i] / s;
-#pragma unroll
-        for (int i = 0; i < KU; ++i)
-          if (i == k - 1) pc[i] = s;
-      }
+      if (t < k1) g[k - 1][t] = g[k - 1][t] / s;          // lls.py: Gp[k-1, :] /= s
+      __syncthreads();
+      if (t < k1) g[t][k - 1] = g[t][k - 1] / s;          //         Gp[:, k-1] /= s
+      if (t == 0) pm[k - 1][k - 1] = s;
+      __syncthreads();
     }
   }
-  // the r column G[:k, k] (lane k's column) to every lane's row, before the factorisation overwrites it
-  if (l == k) {
-#pragma unroll
-    for (int i = 0; i < KU; ++i)
-      if (i < k) zcol[i] = gc[i];
-  }
-  // Cholesky, upper: after step j, gc[j] of lane l is ry[j][l] (0 below the diagonal)
-  int bad = 0;
-#pragma unroll
-  for (int j = 0; j < KU; ++j) {
-    if (j < k) {
-      const double t = gc[j];                       // g'[j][l]: g[j][l] - sum_{i<j} ry[i][j] ry[i][l]
-      const double tj = rdl(t, j);
-      if (!(tj > 0.0)) bad = 1;
-      const double rjj = sqrt(tj);
-      const double ryjl = (l > j && l < k) ? t / rjj : (l == j ? rjj : 0.0);
-      gc[j] = ryjl;
-#pragma unroll
-      for (int i = j + 1; i < KU; ++i)
-        if (i < k) {
-          const double ryji = rdl(ryjl, i);        // ry[j][i]
-          if (l >= i && l < k) gc[i] = gc[i] - ryji * ryjl;
-        }
+  // Cholesky, upper
+  double gv = (i <= l && l < k) ? g[i][l] : 0.0;
+  for (int j = 0; j < k; ++j) {
+    if (i == j && l == j) {
+      if (!(gv > 0.0)) bad = 1;
+      ry[j][j] = sqrt(gv);
     }
-  }
-  __syncthreads();
-  // z = Ry^-T G[:k, k] (forward substitution, subtractions in row order); zl = z_l on lane l
-  double b = (l < k) ? zcol[l] : 0.0;
-  double zl = 0.0;
-#pragma unroll
-  for (int j = 0; j < KU; ++j)
-    if (j < k) {
-      const double svj = rdl(b / gc[j], j);         // lane j: b / ry[j][j]
-      if (l == j) zl = svj;
-      if (l > j && l < k) b = b - gc[j] * svj;
+    __syncthreads();
+    if (i == j && l < k) {
+      if (l > j) ry[j][l] = gv / ry[j][j];
+      else if (l < j) ry[j][l] = 0.0;
     }
-  // R = Ry P (column l: R[i][l] = sum_{m=i..l} ry[i][m] p[m][l], m ascending)
-  double rc[KU];
-#pragma unroll
-  for (int i = 0; i < KU; ++i) {
+    __syncthreads();
+    if (i > j && i <= l && l < k) gv = gv - ry[j][i] * ry[j][l];
+  }
+  // z = Ry^-T G[:k, k] (forward substitution, subtractions in row order)
+  double b = (t < k) ? g[t][k] : 0.0;
+  for (int j = 0; j < k; ++j) {
+    if (t == j) sv[j] = b / ry[j][j];
+    __syncthreads();
+    if (t > j && t < k) b = b - ry[j][t] * sv[j];
+  }
+  // R = Ry P, one entry per thread (m ascending)
+  if (i < k && l < k) {
     double a = 0.0;
-    if (i < k) {
-#pragma unroll
-      for (int m = i; m < KU; ++m)
-        if (m < k) {
-          const double rim = rdl(gc[i], m);         // ry[i][m]
-          if (m <= l) a = a + rim * pc[m];
-        }
-    }
-    rc[i] = (i < k && i <= l) ? a : 0.0;
-  }
-  // rows of R to their lanes (R[l][j] on lane l)
-  if (l < KU) {
-#pragma unroll
-    for (int i = 0; i < KU; ++i) rr_s[i][l] = rc[i];
+    for (int m = i; m <= l; ++m) a = a + ry[i][m] * pm[m][l];
+    rr[i][l] = (i <= l) ? a : 0.0;
   }
   __syncthreads();
-  double rrow[KU];
-#pragma unroll
-  for (int j = 0; j < KU; ++j) rrow[j] = (l < KU) ? rr_s[l][j] : 0.0;
   // x = R^-1 z, column-oriented back substitution; d = -x
-  double xv = (l < k) ? zl : 0.0, xl = 0.0;
-  double xs[KU];
-#pragma unroll
-  for (int j = KU - 1; j >= 0; --j) {
-    xs[j] = 0.0;
-    if (j < k) {
-      const double xj = rdl(xv / rc[j], j);         // lane j: xv / rr[j][j]
-      xs[j] = xj;
-      if (l == j) xl = xj;
-      if (l < j) xv = xv - xj * rrow[j];
-    }
+  double xv = (t < k) ? sv[t] : 0.0;
+  __syncthreads();
+  for (int j = k - 1; j >= 0; --j) {
+    if (t == j) sv[j] = xv / rr[j][j];
+    __syncthreads();
+    if (t < j) xv = xv - sv[j] * rr[t][j];
   }
-  const double d = (l < k) ? -xl : 0.0;
-  // jdd = sum_i (R d)_i^2, summed in row order
-  double a = 0.0;
-#pragma unroll
-  for (int c = 0; c < KU; ++c)
-    if (c < k && c >= l) a = a + rrow[c] * (-xs[c]);
-  const double rd2 = a * a;
-  double jdd = 0.0;
-#pragma unroll
-  for (int i = 0; i < KU; ++i)
-    if (i < k) jdd = jdd + rdl(rd2, i);
-  if (l == 0) {
+  __syncthreads();
+  const double d = (t < k) ? -sv[t] : 0.0;
+  if (t < k) {
+    double a = 0.0;
+    for (int c = t; c < k; ++c) a = a + rr[t][c] * (-sv[c]);
+    rd2[t] = a * a;
+  }
+  // R^-1, one row per step (rows descending): X[r][l] = (delta_rl - sum_{m=r+1..l} R[r][m] X[m][l]) / R[r][r]
+  for (int r = k - 1; r >= 0; --r) {
+    if (i == r && l < k) {
+      double a = (r == l) ? 1.0 : 0.0;
+      for (int m = r + 1; m <= l; ++m) a = a - rr[r][m] * xm[m][l];
+      xm[r][l] = (r <= l) ? a / rr[r][r] : 0.0;
+    }
+    __syncthreads();
+  }
+  if (t == 0) {
+    double jdd = 0.0;
+    for (int q = 0; q < k; ++q) jdd = jdd + rd2[q];
     out[0] = bad ? 1.0 : 0.0;
     out[1] = jdd;
     out[2] = s;
   }
-  if (l < k) {
-    out[3 + l] = d;
-    etry[l] = e[l] + sdd[l] * d;
-#pragma unroll
-    for (int i = 0; i < KU; ++i)
-      if (i < k) {
-        out[3 + k + i * k + l] = rc[i];
-        out[3 + k + k * k + i * k + l] = gc[i];
-      }
+  if (t < k) {
+    out[3 + t] = d;
+    etry[t] = e[t] + sdd[t] * d;
   }
-  // column l of R^-1 (back substitution on e_l); rows below l are zero
-  double xc[KU];
-#pragma unroll
-  for (int i = KU - 1; i >= 0; --i) {
-    double t = (i == l) ? 1.0 : 0.0;
-    if (i < k) {
-#pragma unroll
-      for (int m = i + 1; m < KU; ++m)
-        if (m < k) {
-          const double rim = rdl(rc[i], m);         // R[i][m]
-          if (m <= l) t = t - rim * xc[m];
-        }
-    }
-    xc[i] = (i < k && i <= l) ? t / rdl(rc[i], i) : 0.0;
-  }
-  if (l < k) {
-    double* rinv = out + 3 + k + 2 * k * k;
-#pragma unroll
-    for (int i = 0; i < KU; ++i)
-      if (i < k) rinv[i * k + l] = xc[i];
+  if (i < k && l < k) {
+    out[3 + k + i * k + l] = rr[i][l];
+    out[3 + k + k * k + i * k + l] = ry[i][l];
+    out[3 + k + 2 * k * k + i * k + l] = xm[i][l];
   }
 }
 
@@ -4968,17 +4903,12 @@ int gnk_lls_solve(gnk_ctx* ctx, const double* Gm, int kp, int k, const double* P
   if (k < 1 || k > LS_KMAX) return fail(ctx, "lls_solve: k must be in [1, gnk_lls_max_k()]");
   if (kp < k + 1) return fail(ctx, "lls_solve: kp < k + 1 (G must hold the r column)");
   if (!Gm || !P || !sdd || !e || !out || !e_try) return fail(ctx, "lls_solve: NULL argument");
-  // the register form (k_lls_r) for the GNK path's basis sizes; tuning GNK_TUNE_LLS 1 keeps k_lls (tooling A/B)
-  if (k <= 24 && tuning(ctx, GNK_TUNE_LLS) != 1) {
-    if (k <= 8)
-      hipLaunchKernelGGL(k_lls_r<8>, dim3(1), dim3(64), 0, ctx->stream, Gm, kp, k, P, rescale, sdd, e, out, e_try);
-    else if (k <= 16)
-      hipLaunchKernelGGL(k_lls_r<16>, dim3(1), dim3(64), 0, ctx->stream, Gm, kp, k, P, rescale, sdd, e, out, e_try);
-    else
-      hipLaunchKernelGGL(k_lls_r<24>, dim3(1), dim3(64), 0, ctx->stream, Gm, kp, k, P, rescale, sdd, e, out, e_try);
-  } else {
+  // one entry per thread (k_lls_2d) by default; tuning GNK_TUNE_LLS 1 keeps the one-wave k_lls (tooling A/B,
+  // the same bits)
+  if (tuning(ctx, GNK_TUNE_LLS) != 1)
+    hipLaunchKernelGGL(k_lls_2d, dim3(1), dim3(1024), 0, ctx->stream, Gm, kp, k, P, rescale, sdd, e, out, e_try);
+  else
     hipLaunchKernelGGL(k_lls, dim3(1), dim3(64), 0, ctx->stream, Gm, kp, k, P, rescale, sdd, e, out, e_try);
-  }
   return check_launch(ctx, "lls_solve");
 }
 

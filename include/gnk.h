@@ -73,8 +73,8 @@ int gnk_set_segments(gnk_ctx* ctx, int64_t seg_rows);
  *                        3 = the pair-split kernel instead of the VGPR-RinvAug one for 5..7 blocks
  *   GNK_TUNE_GRAM_RPR    > 0: grid rows per row range of the staged / VALU Gram kernels (a finer,
  *                        fixed decomposition; A/B of what rank-count-independent partials cost)
- *   GNK_TUNE_LLS         1 = the LDS-resident device solve (k_lls) instead of the register one (k_lls_r,
- *                        k <= 24; the same bits) */
+ *   GNK_TUNE_LLS         1 = the device least-squares solve on one wave, a column per lane (k_lls), instead of
+ *                        one entry per thread on 32 x 32 threads (k_lls_2d); the same bits */
 #define GNK_TUNE_GRAM_PATH 0
 #define GNK_TUNE_GRAM_RING 1
 #define GNK_TUNE_GRAM_V1MIN 2

@@ -1,5 +1,5 @@
-"""The register-resident device solve (k_lls_r, k <= 24) against the LDS-resident k_lls it replaces on the GNK
-path (GNK_TUNE_LLS 1 keeps k_lls): the same preconditioned-CholeskyQR step (ref:gauss_newton_krylow.py:16-36
+"""The device least-squares solve in its two forms -- one entry per thread on 32 x 32 threads (k_lls_2d, the
+default) and one wave with a column per lane (k_lls, GNK_TUNE_LLS 1): the same preconditioned-CholeskyQR step (ref:gauss_newton_krylow.py:16-36
 restated in lls.py) with the same IEEE operations in the same order, so every output -- status, jdd, the
 rescale s, d, R, Ry, R^-1 and the first trial's coefficients -- must agree bit for bit, and for a Gram that is not
 numerically SPD the same values with NaN in the same places."""
@@ -34,7 +34,7 @@ def _solve(be, G, kp, k, P, rescale, sdd, e, lls_mode):
     return out.cpu().numpy(), et.cpu().numpy()
 
 
-@pytest.mark.parametrize("k", [1, 2, 3, 7, 8, 9, 12, 16, 17, 20, 24])
+@pytest.mark.parametrize("k", [1, 2, 3, 7, 8, 9, 12, 16, 17, 20, 24, 28, 32])
 def test_register_solve_bit_identical(k):
     from gauss_newton_via_generalized_krylov_subspaces_amd._native import HipBackend
     be = HipBackend(torch.device("cuda", 0))
@@ -43,14 +43,15 @@ def test_register_solve_bit_identical(k):
     for cond, spd, rescale in ((1e2, True, 1), (1e5, True, 0), (1e3, False, 1), (10.0, True, 1)):
         G, P, sdd, e = _case(rng, k, cond, spd)
         o1, t1 = _solve(be, G, kp, k, P, rescale, sdd, e, 1)
-        o0, t0 = _solve(be, G, kp, k, P, rescale, sdd, e, 0)
-        if spd:
-            assert o0[0] == 0.0
-            assert np.array_equal(o0.view(np.int64), o1.view(np.int64)), (k, cond, rescale)
-            assert np.array_equal(t0.view(np.int64), t1.view(np.int64)), (k, cond, rescale)
-        else:
-            # not SPD: status 1 in both (the host then finishes the solve); the NaNs the factorisation
-            # spreads sit in the same places, their sign / payload bits may differ (operand order of
-            # NaN propagation), every other value is the same double
-            assert o0[0] == o1[0] == 1.0
-            assert np.array_equal(o0, o1, equal_nan=True) and np.array_equal(t0, t1, equal_nan=True)
+        for mode in (0,):
+            o0, t0 = _solve(be, G, kp, k, P, rescale, sdd, e, mode)
+            if spd:
+                assert o0[0] == 0.0
+                assert np.array_equal(o0.view(np.int64), o1.view(np.int64)), (mode, k, cond, rescale)
+                assert np.array_equal(t0.view(np.int64), t1.view(np.int64)), (mode, k, cond, rescale)
+            else:
+                # not SPD: status 1 in all (the host then finishes the solve); the NaNs the factorisation
+                # spreads sit in the same places, their sign / payload bits may differ (operand order of
+                # NaN propagation), every other value is the same double
+                assert o0[0] == o1[0] == 1.0
+                assert np.array_equal(o0, o1, equal_nan=True) and np.array_equal(t0, t1, equal_nan=True)
