@@ -605,10 +605,11 @@ template <int VEC, int KCT>
 __global__ __launch_bounds__(BLOCK) void k_vjp_gemv_t(const double* __restrict__ u, const double* __restrict__ r,
                                                       const double* __restrict__ V, int64_t ldv, int k,
                                                       double* __restrict__ g, Geo geo, Coef c, int64_t lr0,
-                                                      int64_t nlr, double* __restrict__ partial) {
+                                                      int64_t nlr, double* __restrict__ partial, int z0) {
   __shared__ double sh[(BLOCK / 64) * KCT];
   const int lane = threadIdx.x & 63;
-  const int j0 = blockIdx.z * KCT;
+  const int zc = z0 + int(blockIdx.z);              // column chunk (launches may cover a range of chunks)
+  const int j0 = zc * KCT;
   const int kc = max(0, min(KCT, k - j0));
   const int jmax = max(k - 1, 0);
   double acc[KCT];
@@ -627,7 +628,7 @@ __global__ __launch_bounds__(BLOCK) void k_vjp_gemv_t(const double* __restrict__
     if (lane == 63 || iy + 2 >= N) re = he ? r[li + 2] : 0.0;
     const double g0 = -vjp_pt(c, jdiag(c, uc.x), rn.x, rw, hw, rc.x, rc.y, true, rs.x);
     const double g1 = -vjp_pt(c, jdiag(c, uc.y), rn.y, rc.x, true, rc.y, re, he, rs.y);
-    if (blockIdx.z == 0) st_nt(g + li, d2{g0, g1});
+    if (zc == 0) st_nt(g + li, d2{g0, g1});
     if (k > 0) {
 #pragma unroll
       for (int j = 0; j < KCT; ++j) {
@@ -645,7 +646,7 @@ __global__ __launch_bounds__(BLOCK) void k_vjp_gemv_t(const double* __restrict__
       const double d = jdiag(c, u[i]);
       const double rw = hw ? r[i - 1] : 0.0, re = he ? r[i + 1] : 0.0;
       const double gi = -vjp_pt(c, d, r[i - N], rw, hw, r[i], re, he, r[i + N]);
-      if (blockIdx.z == 0) g[i] = gi;
+      if (zc == 0) g[i] = gi;
       if (k > 0) {
 #pragma unroll
         for (int j = 0; j < KCT; ++j) acc[j] = acc[j] + V[min(j0 + j, jmax) * ldv + i] * gi;
@@ -4016,12 +4017,22 @@ int gnk_vjp_gemv_t(gnk_ctx* ctx, const double* u, const double* r, const double*
   const int cap = tuning(ctx, GNK_TUNE_VJPG_BLOCKS);
   RowLaunch L = rows(ctx, G, ctx->geo.nrows, vec_of(ctx),
                      seg_on(ctx) ? (1 << 30) : (cap > 0 ? cap : std::max(64, 2048 / nchunk)));
-  L.grid.z = nchunk;
   const int nblk = L.grid.x * L.grid.y;
-  if (size_t(nblk) * nchunk * kct > SCRATCH_DOUBLES) return fail(ctx, "vjp_gemv_t: scratch too small");
+  // column chunks per launch: with segments every owned row has its own block row (nblk = grid.x * rows), and
+  // a wide basis (C5: k up to 200) on a large slab would overflow the partials' workspace -- then the chunks
+  // go in several launches (each chunk's arithmetic and reduction unchanged; only the launch containing
+  // chunk 0 stores g)
+  const size_t room = SEG_WS;
+  if (size_t(nblk) * kct > room) return fail(ctx, "vjp_gemv_t: scratch too small");
+  const int zt = tuning(ctx, GNK_TUNE_VJPG_ZMAX);
+  const int zmax = int(std::min<size_t>(std::min<size_t>(size_t(nchunk), room / (size_t(nblk) * kct)),
+                                        zt > 0 ? size_t(zt) : size_t(nchunk)));
+  for (int z0 = 0; z0 < nchunk; z0 += zmax) {
+    const int nz = std::min(zmax, nchunk - z0);
+    L.grid.z = unsigned(nz);
 #define VJPG_LAUNCH(V_, K_)                                                                                 \
   hipLaunchKernelGGL((k_vjp_gemv_t<V_, K_>), L.grid, dim3(BLOCK), 0, ctx->stream, u, r, V, ldv, k, g, ctx->geo, \
-                     ctx->coef, L.lr0, L.nlr, ctx->scratch)
+                     ctx->coef, L.lr0, L.nlr, ctx->scratch, z0)
 #define VJPG_SWITCH(V_)                  \
   switch (kct) {                         \
     case 4: VJPG_LAUNCH(V_, 4); break;   \
@@ -4031,18 +4042,25 @@ int gnk_vjp_gemv_t(gnk_ctx* ctx, const double* u, const double* r, const double*
     case 20: VJPG_LAUNCH(V_, 20); break; \
     default: VJPG_LAUNCH(V_, 24); break; \
   }
-  if (vec_of(ctx) == 2) {
-    VJPG_SWITCH(2)
-  } else {
-    VJPG_SWITCH(1)
-  }
+    if (vec_of(ctx) == 2) {
+      VJPG_SWITCH(2)
+    } else {
+      VJPG_SWITCH(1)
+    }
 #undef VJPG_SWITCH
 #undef VJPG_LAUNCH
-  int rc = check_launch(ctx, "vjp_gemv_t");
-  if (rc || k == 0 || !h_out) return rc;
-  if (seg_on(ctx))                  // one block row per owned row: segment s = blocks s * seg * grid.x ..
-    return sreduce(ctx, ctx->scratch, int(ctx->seg * L.grid.x), k, kct, kct, int64_t(nblk) * kct, nullptr, h_out);
-  return wreduce(ctx, ctx->scratch, nblk, k, kct, kct, int64_t(nblk) * kct, nullptr, h_out);
+    int rc = check_launch(ctx, "vjp_gemv_t");
+    if (rc) return rc;
+    if (k == 0 || !h_out) continue;
+    const int len = std::min(k - z0 * kct, nz * kct);
+    if (seg_on(ctx))                // one block row per owned row: segment s = blocks s * seg * grid.x ..
+      rc = sreduce(ctx, ctx->scratch, int(ctx->seg * L.grid.x), len, kct, kct, int64_t(nblk) * kct, nullptr,
+                   h_out + int64_t(z0) * kct);
+    else
+      rc = wreduce(ctx, ctx->scratch, nblk, len, kct, kct, int64_t(nblk) * kct, nullptr, h_out + int64_t(z0) * kct);
+    if (rc) return rc;
+  }
+  return 0;
 }
 
 }  // extern "C"

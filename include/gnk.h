@@ -74,7 +74,9 @@ int gnk_set_segments(gnk_ctx* ctx, int64_t seg_rows);
  *   GNK_TUNE_GRAM_RPR    > 0: grid rows per row range of the staged / VALU Gram kernels (a finer,
  *                        fixed decomposition; A/B of what rank-count-independent partials cost)
  *   GNK_TUNE_LLS         1 = the device least-squares solve on one wave, a column per lane (k_lls), instead of
- *                        one entry per thread on 32 x 32 threads (k_lls_2d); the same bits */
+ *                        one entry per thread on 32 x 32 threads (k_lls_2d); the same bits
+ *   GNK_TUNE_VJPG_ZMAX   > 0: at most this many column chunks per gnk_vjp_gemv_t launch (tests: the split
+ *                        that wide bases with segments need; the same bits) */
 #define GNK_TUNE_GRAM_PATH 0
 #define GNK_TUNE_GRAM_RING 1
 #define GNK_TUNE_GRAM_V1MIN 2
@@ -83,7 +85,8 @@ int gnk_set_segments(gnk_ctx* ctx, int64_t seg_rows);
 #define GNK_TUNE_GRAM_WIDE 5
 #define GNK_TUNE_GRAM_RPR 6
 #define GNK_TUNE_LLS 7
-#define GNK_TUNE_COUNT 8
+#define GNK_TUNE_VJPG_ZMAX 8
+#define GNK_TUNE_COUNT 9
 int gnk_set_tuning(gnk_ctx* ctx, int key, int value);
 /* doubles in the context's scratch arena (bounds the wide generic Gram: kp * m <= this) */
 int64_t gnk_scratch_doubles(void);

@@ -145,3 +145,29 @@ def test_segment_reductions_rank_count_invariant(N):
     Vw = np.vstack([inp["V"][:kmax], w])
     hn = Vw @ one["trial_g"]
     np.testing.assert_allclose(one["trial_h"], hn, rtol=1e-10, atol=1e-12 * np.max(np.abs(hn)))
+
+
+def test_vjp_gemv_t_chunk_launches_bit_identical():
+    """Wide bases with segments: gnk_vjp_gemv_t gives every owned row its own block row, so at C5's k (up to 200)
+    on a large slab its partials would overflow the workspace; it then splits the column chunks over launches.
+    One chunk per launch (GNK_TUNE_VJPG_ZMAX 1) must give the one-launch g = -J^T r and h = V^T g bit for bit
+    (ref:krylow.py:62-64)."""
+    N, k = 512, 40                                    # three 16-column chunks
+    prob = gnk.BratuPdeProblem(N + 1, 5, 10)
+    dev = BratuDevice(prob, Comm(single=True, segments=True))
+    be = dev.backend
+    rng = np.random.default_rng(7)
+    u, r = dev.load(0.3 * rng.standard_normal(N * N)), dev.load(rng.standard_normal(N * N))
+    V = be.zeros(k, dev.slab.length)
+    for j in range(k):
+        V[j].copy_(dev.load(rng.standard_normal(N * N)))
+    outs = []
+    for zmax in (0, 1):
+        be.set_tuning("vjpg_zmax", zmax)
+        g, h = dev.vec(), be.zeros(k)
+        be.vjp_gemv_t(u, r, V, k, g, h)
+        torch.cuda.synchronize()
+        outs.append((g.cpu().numpy(), h.cpu().numpy()))
+    be.set_tuning("vjpg_zmax", 0)
+    assert np.array_equal(outs[0][0], outs[1][0]) and np.array_equal(outs[0][1], outs[1][1])
+    assert np.all(np.isfinite(outs[0][1])) and np.any(outs[0][1] != 0.0)
