@@ -290,8 +290,11 @@ class GNKSolver:
                 rr, h, slot = self._trial_plain(e_ext + 1.0 * ds, x_t, r_t, r_old, prod)
                 return ls.d, ls.jdd, ds, rr, h, slot
             if ls.device:
+                # the pack beside the solve's output (lls._LSBuffers.comb): one copy for the step's read
+                pk = lls.bufs[self._par].pack if getattr(lls, "bufs", None) else None
                 pack, slot = basis.trial_first(None, x_t, r_old if prod else None, coef_dev=ls.e_try,
-                                               hh_dev=ls.hh_dev if (adopted and self.reuse_spec_device) else None)
+                                               hh_dev=ls.hh_dev if (adopted and self.reuse_spec_device) else None,
+                                               pack=pk)
                 rd = self.ops.residual_read(x_t, r_t, pack[:3 + kk], ls.out, self._pinned())
                 if prod and self._can_speculate(it, kk):
                     self._spec = self._launch_spec(ls, rd, x_t, r_t, slot)

@@ -85,13 +85,17 @@ class _LSBuffers:
     """Device inputs / outputs of one device solve; two sets, so that a speculatively enqueued next
     step never overwrites what the host has not read yet."""
 
-    def __init__(self, be, L, kp):
+    def __init__(self, be, L, kp, pack_room=0):
         self.T = be.zeros(kp * kp)            # augmented transform of the first pass
         self.G = be.zeros(kp * kp)            # its Gram
         self.P = be.zeros(L * L)
         self.sdd = be.zeros(L)
         self.e = be.zeros(L)
-        self.out = be.zeros(3 + L + 3 * L * L)
+        # [the first trial's scalar pack | the solve's output] in one buffer: the step's host read (the
+        # pack with the solve, DESIGN.md §5b) is then one device-to-host copy on one rank
+        self.comb = be.zeros(pack_room + 3 + L + 3 * L * L)
+        self.pack = self.comb[:pack_room]
+        self.out = self.comb[pack_room:]
         self.etry = be.zeros(L)
         self.hh = be.zeros(L)                 # next step's projection coefficients (k_lls_next)
         self.sc = be.zeros(L)
@@ -129,7 +133,8 @@ class CholQR2Solver:
         # device solve (k_lls): k <= lsk
         self.lsk = (min(int(self.be.lls_max_k()), int(kmax))
                     if device_solve and hasattr(self.be, "lls_solve") else 0)
-        self.bufs = [_LSBuffers(self.be, self.lsk, kp) for _ in range(2)] if self.lsk else []
+        self.pack_room = 4 + int(kmax)          # the basis's first-trial pack (krylow.DeviceKrylovBasis.pack)
+        self.bufs = [_LSBuffers(self.be, self.lsk, kp, self.pack_room) for _ in range(2)] if self.lsk else []
 
     # -- basis events (the solver tells us how V changed since the last solve) -------
     def on_append(self, s_new=None):

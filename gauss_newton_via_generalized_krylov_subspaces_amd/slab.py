@@ -213,6 +213,18 @@ class Comm:
             return _ReadHandle(None, None, n, parts, sh, t)
         if self.world == 1:
             gath = t.reshape(-1)
+            if (shared is not None and shared.untyped_storage().data_ptr() == gath.untyped_storage().data_ptr()
+                    and shared.storage_offset() >= gath.storage_offset() + n and shared.is_contiguous()):
+                # the pack and the solve's output share one device buffer (lls._LSBuffers.comb): one copy of
+                # the span from the pack's start to the output's end instead of two
+                base = gath.storage_offset()
+                span = shared.storage_offset() + m - base
+                src = torch.as_strided(gath, (span,), (1,), base)
+                host = pinned[:span]
+                host.copy_(src, non_blocking=True)
+                ev = torch.cuda.Event()
+                ev.record(torch.cuda.current_stream(t.device))
+                return _ReadHandle(host, ev, n, None, None, gath, shared.storage_offset() - base)
         else:
             gath = torch.empty(self.world * n, dtype=t.dtype, device=t.device)
             self._count_gather(t)
@@ -224,7 +236,7 @@ class Comm:
             host[wn:].copy_(shared.reshape(-1), non_blocking=True)
         ev = torch.cuda.Event()
         ev.record(torch.cuda.current_stream(t.device))
-        return _ReadHandle(host, ev, n, None, None, gath)
+        return _ReadHandle(host, ev, n, None, None, gath, wn if shared is not None else None)
 
     def device_sum(self, h) -> torch.Tensor:
         """Sum over ranks (on the device) of the tensor behind a read handle."""
@@ -247,7 +259,7 @@ class Comm:
             wn = self.world * h.n
             a = h.host.numpy()
             h.parts = a[:wn].reshape(self.world, h.n).copy()
-            h.shared = a[wn:].copy() if a.size > wn else None
+            h.shared = a[h.soff:].copy() if h.soff is not None else None
         parts = h.parts
         s = self._rank_sum(parts)
         m = float(parts[0][imax])
@@ -329,10 +341,11 @@ class SlabVector:
 
 
 class _ReadHandle:
-    __slots__ = ("host", "ev", "n", "parts", "shared", "gath")
+    __slots__ = ("host", "ev", "n", "parts", "shared", "gath", "soff")
 
-    def __init__(self, host, ev, n, parts, shared, gath):
+    def __init__(self, host, ev, n, parts, shared, gath, soff=None):
         self.host, self.ev, self.n, self.parts, self.shared, self.gath = host, ev, n, parts, shared, gath
+        self.soff = soff                      # where the shared buffer's copy starts in ``host``
 
 
 class Slab:
