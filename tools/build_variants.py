@@ -85,6 +85,11 @@ VARIANTS = {
   RowLaunch L = rows(ctx, 0, ctx->geo.nrows + 2 * G, 1, resident_blocks(ctx, fn));"""),
               ("      for (int j = 0; j < KCT; ++j) vv[j] = V[min(j, jmax) * ldv + i];",
                "      for (int j = 0; j < KCT; ++j) vv[j] = __builtin_nontemporal_load(V + min(j, jmax) * ldv + i);")],
+    # k_gram_v / k_gram_v1: non-temporal loads of the marching south rows (each basis value leaves HBM once)
+    "gvnt": [("        vs[j] = *reinterpret_cast<const d2*>(cp + N);\n        eo[j] = (edge_w || edge_e) ? cp[eoff] : 0.0;     // only the strip's edge lanes load",
+              "        vs[j] = __builtin_nontemporal_load(reinterpret_cast<const d2*>(cp + N));\n        eo[j] = (edge_w || edge_e) ? cp[eoff] : 0.0;     // only the strip's edge lanes load"),
+             ("        vs[j] = cp[N];\n        eo[j] = (edge_w || edge_e) ? cp[eoff] : 0.0;     // only the strip's edge lanes load",
+              "        vs[j] = __builtin_nontemporal_load(cp + N);\n        eo[j] = (edge_w || edge_e) ? cp[eoff] : 0.0;     // only the strip's edge lanes load")],
     # k_gemv_vjpg: one workgroup per row segment (as k_jvp2) instead of the resident persistent grid
     "vjpgrow": [('  RowLaunch L = rows(ctx, 0, ctx->geo.nrows + 2 * G, vec_of(ctx), resident_blocks(ctx, fn));', '  RowLaunch L = rows(ctx, 0, ctx->geo.nrows + 2 * G, vec_of(ctx), 1 << 30);')],
 }
