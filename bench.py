@@ -8,8 +8,13 @@ N x N interior grid (default N = 8192, the metric's grid).  One *step* = one GNK
 outer iteration (LS solve + Armijo trials + basis update); the timed steps cover
 a full restart cycle so every basis size 1..21 is represented.
 
-Multi-GPU (torchrun, one process per GPU): the same grid is row-partitioned
-over the ranks (strong scaling); halos + rank-ordered all-gathers over RCCL.
+Multi-GPU, one process per GPU: the same grid is row-partitioned over the ranks
+(strong scaling); halos + rank-ordered all-gathers over RCCL.  Either launched by
+torch.distributed.run (WORLD_SIZE set: every rank checks WORLD_SIZE == --gpus), or
+``python bench.py --gpus N`` itself starts the N ranks as child processes with the
+same environment torch.distributed.run gives them (``launch_ranks``; the parent never
+touches the GPU), relays rank 0's line and fails if any rank fails.  Under RCCL a
+box with fewer than N GPUs is refused, never measured as one rank.
 value = outer iterations of the whole job per second (max elapsed over ranks).
 
 Also reported: the dominant kernel's roofline (fp64-MFMA Gram pass, HBM-bound,
@@ -319,22 +324,90 @@ def stream_floor(be, n, device, reps):
     return out
 
 
+def _free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n, cmd, env=None, poll_s=0.2, grace_s=15.0):
+    """Start ``cmd`` as ranks 0..n-1 of one single-node job (the variables torch.distributed.run sets:
+    RANK, LOCAL_RANK, WORLD_SIZE, LOCAL_WORLD_SIZE, GROUP_RANK, MASTER_ADDR = 127.0.0.1, a free
+    MASTER_PORT), each in a process group of its own, and wait.  The ranks inherit stdout / stderr (rank 0
+    prints the result line).  If any rank exits non-zero the others are terminated (then killed after
+    ``grace_s``) and that exit code is returned; 0 when all succeed.  Child processes, never exec: the
+    caller must not have initialised the GPU."""
+    import signal
+    import subprocess
+    base = dict(os.environ if env is None else env)
+    base.update(WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n), GROUP_RANK="0", MASTER_ADDR="127.0.0.1",
+                MASTER_PORT=str(_free_port()), HSA_ENABLE_IPC_MODE_LEGACY="0")
+    procs = []
+    for r in range(n):
+        e = dict(base, RANK=str(r), LOCAL_RANK=str(r))
+        procs.append(subprocess.Popen(cmd, env=e, start_new_session=True))
+    failed = 0
+    try:
+        while [p.poll() for p in procs].count(None):          # poll every rank (no short-circuit)
+            bad = [p.returncode for p in procs if p.returncode not in (None, 0)]
+            if bad:
+                failed = bad[0]
+                break
+            time.sleep(poll_s)
+        else:
+            bad = [p.returncode for p in procs if p.returncode != 0]
+            failed = bad[0] if bad else 0
+    finally:
+        live = [p for p in procs if p.poll() is None]
+        for sig in (signal.SIGTERM, signal.SIGKILL):
+            for p in live:
+                with contextlib.suppress(ProcessLookupError):
+                    os.killpg(p.pid, sig)
+            t_end = time.time() + grace_s
+            while live and time.time() < t_end:
+                live = [p for p in live if p.poll() is None]
+                time.sleep(poll_s)
+            if not live:
+                break
+        for p in procs:
+            with contextlib.suppress(Exception):
+                p.wait(timeout=grace_s)
+    return failed if failed >= 0 else 1            # a rank killed by a signal: 1
+
+
 def main():
     args = parse()
+    if args.gpus < 1:
+        raise SystemExit("bench.py: --gpus must be >= 1")
+    backend = os.environ.get("GNK_BENCH_BACKEND", "nccl")
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # `python bench.py --gpus N`: start the N ranks here (this process has not touched the GPU;
+        # device_count does not initialise it on this image)
+        if backend != "gloo" and torch.cuda.device_count() < args.gpus:
+            raise SystemExit(f"bench.py: --gpus {args.gpus} needs {args.gpus} GPUs under RCCL, "
+                             f"this node has {torch.cuda.device_count()}; refusing to measure fewer ranks")
+        sys.exit(launch_ranks(args.gpus, [sys.executable, os.path.abspath(__file__)] + sys.argv[1:]))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}: refusing a mislabelled run")
     if world > 1:
         os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
         # GNK_BENCH_BACKEND=gloo: rehearsal of the multi-rank bench on fewer GPUs than ranks (ranks
         # share cards, collectives staged through the host); the measured runs use RCCL, one GPU each
-        backend = os.environ.get("GNK_BENCH_BACKEND", "nccl")
         if backend == "gloo":
             torch.cuda.set_device(local % torch.cuda.device_count())
             dist.init_process_group("gloo")
         else:
+            if torch.cuda.device_count() < world:
+                raise SystemExit(f"bench.py: rank {rank}: {world} ranks under RCCL need {world} GPUs, "
+                                 f"this node has {torch.cuda.device_count()}")
             torch.cuda.set_device(local)
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if dist.get_world_size() != args.gpus:
+            raise SystemExit(f"bench.py: process group has {dist.get_world_size()} ranks, --gpus {args.gpus}")
     else:
         torch.cuda.set_device(0)
     device = torch.device("cuda", torch.cuda.current_device())

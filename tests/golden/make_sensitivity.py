@@ -48,6 +48,7 @@ OUT = os.path.dirname(os.path.abspath(__file__))
 PATH = os.environ.get("SENS_OUT", os.path.join(OUT, "sensitivity.json"))   # (merge tooling: SENS_OUT)
 _LLS = O.linear_least_squares
 _UPDATE = O.KrylovBasis.update
+_ARMIJO = O.armijo_goldstein
 THREADS = (1, 8)
 
 
@@ -133,22 +134,60 @@ def slab_variant(N, P):
     return lls, update
 
 
-def variants(N, slabs=False):
+def armijo_sums(total):
+    """ref:armijo_goldstein.py:46-70 with its three sums of squares (the previous loss, each trial's loss,
+    ||J d||^2) evaluated by ``total`` -- an algebraically equivalent summation (exactly rounded, or over
+    row blocks in order, the device's per-block partials)."""
+    def armijo(res, x, res_ev, jac_ev, args, d, max_iter=100, initial_step_length=1.0):
+        t = initial_step_length
+        prev = total(res_ev ** 2)
+        jdd = total((jac_ev @ d) ** 2)
+        for it in range(max_iter):
+            cur_res = res(x + t * d, *args)
+            if prev - total(cur_res ** 2) >= 0.5 * t * jdd:
+                return t, cur_res, it + 1
+            t /= 2
+        return _ARMIJO(res, x, res_ev, jac_ev, args, d, max_iter, initial_step_length)   # raises as the reference
+    return armijo
+
+
+def _blocked_sum(P):
+    def total(a):
+        edges = np.linspace(0, a.size, P + 1).astype(int)
+        s = 0.0
+        for lo, hi in zip(edges[:-1], edges[1:]):
+            s = s + float(np.sum(a[lo:hi]))
+        return s
+    return total
+
+
+def variants(N, slabs=False, armijo=False):
     v = {"base": (_LLS, _UPDATE), "exact_k1": (lls_variant(True, None), _UPDATE),
          "perm7": (lls_variant(False, 7), _UPDATE), "perm8+k1": (lls_variant(True, 8), _UPDATE),
          "cholqr2": (cholqr2_lls, _UPDATE)}
     v.update({f"cholqr2b{P}": (cholqr2_blocked(P), _UPDATE) for P in (4, 64, 256)})
     if slabs:
         v.update({f"slab{P}": slab_variant(N, P) for P in range(2, 9)})
+    if armijo:
+        # the Armijo-Goldstein sums themselves re-rounded (round 5): a converged step's trial count is
+        # decided by them, so they belong in the family that bounds it
+        fsum = armijo_sums(math.fsum)
+        v.update({"armijo_fsum": (_LLS, _UPDATE, fsum), "armijo_fsum+k1": (lls_variant(True, None), _UPDATE, fsum),
+                  "armijo_fsum+cholqr2": (cholqr2_lls, _UPDATE, fsum)})
+        v.update({f"armijo_b{P}": (_LLS, _UPDATE, armijo_sums(_blocked_sum(P))) for P in (8, 64, 512)})
+        v.update({f"perm{s}": (lls_variant(False, s), _UPDATE) for s in (9, 10, 11, 12)})
+        v.update({f"cholqr2b{P}+armijo_fsum": (cholqr2_blocked(P), _UPDATE, fsum) for P in (64, 256)})
     return v
 
 
-def trajectory(prob, y, u0, lls, update, threads, **kw):
+def trajectory(prob, y, u0, lls, update, threads, armijo=None, **kw):
     res = prob.make_res(y)
     xs, rs, nf = [], [], []
     O.linear_least_squares = lls
     if update is not _UPDATE:
         O.KrylovBasis.update = update
+    if armijo is not None:
+        O.armijo_goldstein = armijo
     try:
         with threadpool_limits(limits=threads, user_api="blas"), contextlib.redirect_stdout(io.StringIO()):
             O.gauss_newton_krylow(res, u0, prob.make_jac(), callback=lambda x, nfev, cg_iter: (
@@ -157,24 +196,41 @@ def trajectory(prob, y, u0, lls, update, threads, **kw):
         pass
     finally:
         O.linear_least_squares = _LLS
+        O.armijo_goldstein = _ARMIJO
         if update is not _UPDATE:
             O.KrylovBasis.update = _UPDATE
     return np.array(xs), np.array(rs), nf
 
 
+JOBS = int(os.environ.get("SENS_JOBS", "1"))      # variants run in this many forked processes
+
+
+def _run_one(job):
+    name, t = job
+    spec = _JOBSPEC["variants"][name]
+    return f"{name}@{t}", trajectory(*_JOBSPEC["inputs"], *spec[:2], t, *spec[2:], **_JOBSPEC["kw"])
+
+
+_JOBSPEC = {}
+
+
 ONLY = None            # --only v1,v2: recompute these variants (and base) and merge into the stored case
 
 
-def envelope(N, ref=None, slabs=False, threads=THREADS, **kw):
+def envelope(N, ref=None, slabs=False, threads=THREADS, armijo=False, **kw):
     """Per-variant and maximal per-iteration distances from ``ref`` = (xnorm, rnorm) (None: the
     1-thread base oracle)."""
     prob, y, u0 = O.bratu_workload(N)
-    runs = {}
-    for name, (lls, upd) in variants(N, slabs).items():
-        if ONLY is not None and name not in ONLY and not (name == "base" and ref is None):
-            continue
-        for t in threads:
-            runs[f"{name}@{t}"] = trajectory(prob, y, u0, lls, upd, t, **kw)
+    vs = variants(N, slabs, armijo)
+    jobs = [(name, t) for name in vs for t in threads
+            if ONLY is None or name in ONLY or (name == "base" and ref is None)]
+    _JOBSPEC.update(variants=vs, inputs=(prob, y, u0), kw=kw)
+    if JOBS > 1:
+        import multiprocessing as mp
+        with mp.get_context("fork").Pool(JOBS) as pool:
+            runs = dict(pool.map(_run_one, jobs, chunksize=1))
+    else:
+        runs = dict(map(_run_one, jobs))
     if ref is None:
         ref = runs[f"base@{threads[0]}"][:2]
     ref_x, ref_r = np.asarray(ref[0]), np.asarray(ref[1])
@@ -309,7 +365,8 @@ def _large(fixture, version):
 
 CASES = {
     # BASELINE sizes vs the reference's own fixtures (make_golden_large.py)
-    "c2_res_old": lambda: envelope(1024, _large("c2", "res_old"), krylow_restart=20, max_iter=100, version="res_old"),
+    "c2_res_old": lambda: envelope(1024, _large("c2", "res_old"), armijo=True, krylow_restart=20, max_iter=100,
+                                   version="res_old"),
     "c2_res_new": lambda: envelope(1024, _large("c2", "res_new"), krylow_restart=20, max_iter=100, version="res_new"),
     "head8192": lambda: envelope(8192, _large("head8192", "res_old"), threads=(4, 8), krylow_restart=20, max_iter=5,
                                  version="res_old"),
