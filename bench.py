@@ -300,6 +300,30 @@ def pmc_traffic(config_key, window, section=None):
     return None, None
 
 
+def pmc_sq(config_key, window):
+    """fp64 pipe use of the Gram passes from a committed SQ counter summary (tools/pmc_bench_sq.sh ->
+    tools/pmc_sq_summary.py) of this configuration and this timed window (same warmup / steps / repeats /
+    launch count / algorithmic bytes per launch): the window's mfma_busy (MFMA pipe cycles / SIMD cycles)
+    and per basis size k (mfma_busy, share of wave time waiting on operands, wave instructions).  The
+    last matching summary in path order wins; (None, None) when none matches."""
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "pmc_sq_summary*.json")), reverse=True):
+        try:
+            with open(path) as f:
+                d = json.load(f)
+        except (OSError, ValueError):
+            continue
+        w = d.get("window") or {}
+        if (d.get("config") == config_key and d.get("mfma_busy") is not None
+                and all(w.get(k) == window[k] for k in ("warmup", "steps", "repeats", "gram_launches"))
+                and abs(w.get("algorithmic_bytes_per_launch", 0.0) - window["algorithmic_bytes_per_launch"])
+                <= 1e-9 * window["algorithmic_bytes_per_launch"]):
+            per_k = {k: {"kernel": v["kernel"], "mfma_busy": v["mfma_busy"], "wait_inst_any_frac": v["wait_inst_any_frac"],
+                         "valu_per_launch": v["insts_valu"], "mfma_per_launch": v["insts_mfma"]}
+                     for k, v in d["per_k"].items()}
+            return {"mfma_busy": d["mfma_busy"], "by_k": per_k}, os.path.relpath(path, ROOT)
+    return None, None
+
+
 def stream_floor(be, n, device, reps):
     """Measured HBM streaming floor on this box (gnk_probe_stream, HIP events): triad a = b + s c
     (24 n bytes), read-only (8 n) and copy (16 n) over n doubles, the median of reps launches each --
@@ -563,6 +587,7 @@ def main():
     config_key = f"bratu{N}_gnk_restart{args.restart}_{args.version}_ranks{world}"
     traffic, traffic_src = pmc_traffic(config_key, window)
     t_traffic, t_traffic_src = pmc_traffic(config_key, twindow, section="trial")
+    sq, sq_src = pmc_sq(config_key, window)
     result = {
         "metric": "GN-Krylov outer iters/sec + JVP HBM GB/s, Bratu 8192² fp64, 1/2/4/8 GPUs",
         "value": steps_done / elapsed,
@@ -582,7 +607,10 @@ def main():
                    "armijo_trials": int(sum(s["trials"] for s in tr)),
                    "parallelism": f"slab{world}",
                    "transport": (dist.get_backend() if world > 1 else "none"),
-                   "reduction_segments": int(stage.seg_rows)},
+                   "reduction_segments": int(stage.seg_rows),
+                   # reductions that ran unsegmented while segments were on (wide Gram passes): 0 = the
+                   # timed steps' bits do not depend on the rank count (same GPU model)
+                   "segment_fallbacks": int(be.segment_fallbacks())},
         "roofline": {"kernel": "Gram pass of the CholeskyQR solve, J V T on the fly (k_gram_v: VALU, k <= 9; "
                                "k_gram_s: staged fp64 MFMA, k > 9)", "bound": "hbm",
                      "achieved": g_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": g_gbs / HBM_PEAK_GBS,
@@ -590,6 +618,10 @@ def main():
                      "traffic_over_algorithmic": (traffic / g_avg_bytes) if traffic else None, "window": window,
                      "avg_launch_ms": g_avg_ms, "algorithmic_bytes_per_launch": g_avg_bytes,
                      "launches": len(g_ms), "share_of_step_time": gram_share, "by_k": gram_by_k,
+                     "mfma_busy": sq["mfma_busy"] if sq else None, "mfma_busy_source": sq_src,
+                     "mfma_busy_by_k": sq["by_k"] if sq else None,
+                     "mfma_busy_note": "SQ_VALU_MFMA_BUSY_CYCLES / (128 GRBM_GUI_ACTIVE) over the window's Gram "
+                                       "launches (tools/pmc_bench_sq.sh; f64 MFMA = 64 busy cycles each)",
                      "trial": {"kernel": "k_gemv_vjpg (first Armijo trial x = V c, g = -J(x)^T r_old, h = V^T g; "
                                          "pending column w = g - V hh materialised), one launch per step",
                                "bound": "hbm", "achieved": t_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",

@@ -19,7 +19,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("GNK_LIB", os.path.join(_HERE, "libgnk.so"))
 GHOST = 2  # GNK_GHOST_ROWS
 TIMER_GRAM, TIMER_JVP, TIMER_CG_MATVEC, TIMER_TRIAL, TIMER_PROBE = 1, 2, 3, 4, 5  # GNK_TIMER_*
-ABI_VERSION = 5  # GNK_ABI_VERSION
+ABI_VERSION = 6  # GNK_ABI_VERSION
 # GNK_TUNE_* keys of gnk_set_tuning (tests / A/B tooling only; the solver never sets them)
 TUNE = {"gram_path": 0, "gram_ring": 1, "gram_v1min": 2, "cg_matvec": 3, "vjpg_blocks": 4, "gram_wide": 5, "gram_rpr": 6, "lls": 7, "vjpg_zmax": 8}
 
@@ -34,6 +34,7 @@ SIGNATURES = {
     "gnk_set_stream": (_c_int, [_c_vp, _c_vp]),
     "gnk_set_reduce_pairs": (_c_int, [_c_vp, _c_int]),
     "gnk_set_segments": (_c_int, [_c_vp, _c_i64]),
+    "gnk_segment_fallbacks": (_c_i64, [_c_vp]),
     "gnk_set_tuning": (_c_int, [_c_vp, _c_int, _c_int]),
     "gnk_scratch_doubles": (_c_i64, []),
     "gnk_set_bratu": (_c_int, [_c_vp, _c_i64, _c_i64, _c_i64, _c_dbl, _c_dbl, _c_dbl]),
@@ -197,6 +198,11 @@ class HipBackend:
         (gnk_set_segments; 0 = off).  Call after set_bratu, which resets it."""
         self._chk(self.lib.gnk_set_segments(self.ctx, int(seg_rows)), "set_segments")
         self.seg_rows = int(seg_rows)
+
+    def segment_fallbacks(self) -> int:
+        """Reductions that ran on the per-slab decomposition while segments were on (the wide Gram
+        passes, k > 20): rank-count dependent in rounding (gnk_segment_fallbacks)."""
+        return int(self.lib.gnk_segment_fallbacks(self.ctx))
 
     def slab_len(self):
         return int(self.lib.gnk_slab_len(self.ctx))

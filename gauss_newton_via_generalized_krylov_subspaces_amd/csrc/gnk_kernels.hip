@@ -3192,6 +3192,7 @@ __global__ __launch_bounds__(64) void k_lls(const double* __restrict__ Gm, int k
   double s = 1.0;
   if (rescale) {
     const double s2 = g[k - 1][k - 1];
+    __syncthreads();      // every thread holds s2 before any thread rescales row k-1 (LDS race)
     if (isfinite(s2) && s2 > 0.0) {
       s = sqrt(s2);
       if (l < k1) g[k - 1][l] = g[k - 1][l] / s;          // lls.py: Gp[k-1, :] /= s
@@ -3314,6 +3315,7 @@ __global__ __launch_bounds__(1024) void k_lls_2d(const double* __restrict__ Gm, 
   double s = 1.0;
   if (rescale) {
     const double s2 = g[k - 1][k - 1];
+    __syncthreads();      // every thread holds s2 before any thread rescales row k-1 (LDS race)
     if (isfinite(s2) && s2 > 0.0) {
       s = sqrt(s2);
       if (t < k1) g[k - 1][t] = g[k - 1][t] / s;          // lls.py: Gp[k-1, :] /= s
@@ -3513,6 +3515,8 @@ struct gnk_ctx {
   // gnk_set_segments: reduction segment rows (0: off) and this slab's segment count
   int64_t seg = 0;
   int nseg = 1;
+  // reductions that ran on the per-slab decomposition while segments were on (gnk_segment_fallbacks)
+  int64_t seg_fallbacks = 0;
   // gnk_set_tuning (tooling A/B of kernel choices; 0 = the product's choice)
   int tune[GNK_TUNE_COUNT] = {};
   // per-launch timer (tooling, see gnk_timer_start)
@@ -3806,6 +3810,8 @@ RowLaunch flat_rows(int64_t n, int vec, int cap = MAX_RED_BLOCKS) {
 extern "C" {
 
 int gnk_abi_version(void) { return GNK_ABI_VERSION; }
+
+int64_t gnk_segment_fallbacks(const gnk_ctx* ctx) { return ctx ? ctx->seg_fallbacks : -1; }
 
 int gnk_ctx_create(int device, gnk_ctx** out) {
   if (!out) return -1;
@@ -4193,6 +4199,10 @@ int gnk_normalize_jnorm(gnk_ctx* ctx, const double* u, const double* g, double d
   if (g == v) return fail(ctx, "normalize_jnorm: v must not alias g (stencil reads of g)");
   RowLaunch L = rows(ctx, 0, ctx->geo.nrows + 2 * G, vec_of(ctx), seg_row_cap(ctx));
   const int nblk = L.grid.x * L.grid.y;
+  // the segmented reduction below reads one block row per grid row (partials at G * grid.x, seg * grid.x);
+  // rows() caps grid.y at 65535 (nrows + 2 G past that would misplace the offsets silently)
+  if (seg_on(ctx) && jnorm2_out && int64_t(L.grid.y) != L.nlr)
+    return fail(ctx, "normalize_jnorm: segments need one block row per grid row");
   DISPATCH_VEC(ctx, k_div_jnorm, L, 0, u, g, denom, v, ctx->geo, ctx->coef, L.lr0, L.nlr, ctx->scratch);
   int rc = check_launch(ctx, "normalize_jnorm");
   if (rc || !jnorm2_out) return rc;
@@ -4239,6 +4249,7 @@ int gnk_gram(gnk_ctx* ctx, const double* u, const double* V, int64_t ldv, int k,
                                                 BLOCK / 64)
                                       : 0;
     const int64_t rpr = rpr_s > 0 ? rpr_s : rpr_t > 0 ? int64_t(rpr_t) : (nrows + nranges - 1) / nranges;
+    if (seg_on(ctx) && rpr_s <= 0) ++ctx->seg_fallbacks;
     nranges = (nrows + rpr - 1) / rpr;
     const int64_t nwaves = nstrips * nranges;
     const int64_t nblk = (nwaves + BLOCK / 64 - 1) / (BLOCK / 64);
@@ -4325,6 +4336,7 @@ int gnk_gram(gnk_ctx* ctx, const double* u, const double* V, int64_t ldv, int k,
                                                       ctx->seg, int64_t(ctx->num_cus) * wgpc / nstrips)), nstrips, 1)
                                         : 0;
       const int64_t rpr = rpr_s > 0 ? rpr_s : rpr_t > 0 ? int64_t(rpr_t) : (nrows + nranges - 1) / nranges;
+      if (seg_on(ctx) && rpr_s <= 0) ++ctx->seg_fallbacks;
       nranges = (nrows + rpr - 1) / rpr;
       const int plog = rpr_s > 0 ? 1 : 0;             // partials at the logical (range, strip) tile
       const int64_t nwg = nstrips * nranges;
@@ -4383,6 +4395,8 @@ int gnk_gram(gnk_ctx* ctx, const double* u, const double* V, int64_t ldv, int k,
       return check_launch(ctx, "gram scatter (staged)");
     }
   }
+  // the wide passes below reduce over their own slab decomposition (not segmented)
+  if (seg_on(ctx)) ++ctx->seg_fallbacks;
   // 5..7 column blocks on a grid of 32-point strips: k_gram_x (marching, RinvAug in VGPRs); tuning
   // GNK_TUNE_GRAM_WIDE 3 keeps the pair-split k_gram below (tooling A/B).  At 2..4 blocks (k = 21..63)
   // the barrier-free chunked / prefetching kernels stay 1.1-1.5x faster (profiles/round3/gram_wide_ab.jsonl)

@@ -33,7 +33,7 @@ extern "C" {
 #endif
 
 #define GNK_GHOST_ROWS 2
-#define GNK_ABI_VERSION 5
+#define GNK_ABI_VERSION 6
 
 typedef struct gnk_ctx gnk_ctx;
 
@@ -55,12 +55,18 @@ int gnk_set_reduce_pairs(gnk_ctx* ctx, int on);
  * GNK path -- the Gram passes of gnk_gram at k <= 20 (N % 128 == 0), the first-trial / pending-column
  * sums (gnk_basis_gemv_vjp_gemv_t*, gnk_basis_gemv_pending), gnk_bratu_residual, gnk_vec_stats,
  * gnk_cgs_update, gnk_vjp_gemv_t, gnk_normalize_jnorm -- is then computed per segment with a block
- * decomposition that depends on N and seg_rows only, and the segment values are folded pairwise in
+ * decomposition that depends on N, seg_rows and the device model (its CU count and resident workgroups
+ * size some grids: equal bits need the same GPU model on every rank), and the segment values are folded pairwise in
  * a fixed tree: v[i] += v[i + w] for w = 1, 2, 4, ... (i a multiple of 2w, i + w < n).  With
  * seg_rows = N / P and P / w segments per rank, combining the w ranks' values in the same tree
  * order (slab.Comm) gives the same bits for every w dividing P.  Compensated pairs
  * (gnk_set_reduce_pairs) stay per rank.  0 = off (the default: one decomposition per slab). */
 int gnk_set_segments(gnk_ctx* ctx, int64_t seg_rows);
+/* Reductions run on the per-slab decomposition although segments were on, since the context was created:
+ * the wide Gram passes (k > 20, or N % 128 != 0) and a Gram grid the segment rows cannot tile.  Those
+ * results are rank-count dependent (rounding only); 0 means every reduction so far was segmented.
+ * -1 for a NULL context.  Replaces nothing in the reference (multi-rank bookkeeping). */
+int64_t gnk_segment_fallbacks(const gnk_ctx* ctx);
 /* Kernel-choice overrides for tests and A/B tooling (value 0 = the library's own choice, the
  * default; the solver never sets them):
  *   GNK_TUNE_GRAM_PATH   1 = the staged MFMA Gram kernel for every pass it covers (k <= 20),

@@ -79,7 +79,8 @@ def solve(N, comm, iters, orth=False):
     out = {"nit": r.nit, "nrev": r.nrev, "njev": r.njev, "success": bool(r.success), **rec,
            "k": [t["k"] for t in s.trace], "trials": [t["trials"] for t in s.trace], "stdout": buf.getvalue(),
            "max_cond": max((h[2][-1] for h in s.lls.history if h[2]), default=None),
-           "multi_pass_solves": sum(1 for h in s.lls.history if h[1] > 1), "seconds": secs}
+           "multi_pass_solves": sum(1 for h in s.lls.history if h[1] > 1), "seconds": secs,
+           "segment_fallbacks": dev.backend.segment_fallbacks()}
     if orth:
         b, be = s.basis, dev.backend
         k = b.k

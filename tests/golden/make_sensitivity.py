@@ -175,7 +175,7 @@ def variants(N, slabs=False, armijo=False):
         v.update({"armijo_fsum": (_LLS, _UPDATE, fsum), "armijo_fsum+k1": (lls_variant(True, None), _UPDATE, fsum),
                   "armijo_fsum+cholqr2": (cholqr2_lls, _UPDATE, fsum)})
         v.update({f"armijo_b{P}": (_LLS, _UPDATE, armijo_sums(_blocked_sum(P))) for P in (8, 64, 512)})
-        v.update({f"perm{s}": (lls_variant(False, s), _UPDATE) for s in (9, 10, 11, 12)})
+        v.update({f"perm{s}": (lls_variant(False, s), _UPDATE) for s in range(9, 31)})
         v.update({f"cholqr2b{P}+armijo_fsum": (cholqr2_blocked(P), _UPDATE, fsum) for P in (64, 256)})
     return v
 

@@ -33,7 +33,7 @@ def test_binding_table_matches_header():
 
 def test_load_library_binds_and_reports_version():
     lib = _native.load_library()
-    assert lib.gnk_abi_version() == _native.ABI_VERSION == 5
+    assert lib.gnk_abi_version() == _native.ABI_VERSION == 6
     assert lib.gnk_scratch_doubles() == 16 << 20
     assert lib.gnk_gram_padded_dim(20, 1) == 32
     assert lib.gnk_gram_padded_dim(16, 0) == 16

@@ -66,6 +66,31 @@ def test_c4_32768_eight_ranks_on_one_gpu(tmp_path):
     assert rep["ok"]
 
 
+def test_c5_k200_eight_ranks_on_one_gpu(tmp_path):
+    """C5's basis growth to k = 200 on C5's 8 ranks (tests/c5_worker.py: 8192^2, no restart, V = 108 GB; C5's
+    own 16384^2 basis is 429 GB, the 8 GPUs' HBM): every wide Gram kernel in turn, including the pair-split
+    k_gram for k >= 112, with (k+1)^2 Grams all-gathered and rank-summed through slab.Comm's RCCL branches
+    (host-staged transport), then one rank over the whole grid.  Asserted: identical decisions on every rank
+    and vs one rank (ref:krylow.py:72-73 grows the basis every iteration, ref:gauss_newton_krylow.py:81-82
+    never restarts), per-iteration ||x_k|| / ||r_k|| bit for bit while the basis is on the segmented kernels
+    (iterations 1..21, k <= 20) and within 1e-12 after (the wide kernels reduce over their own slab
+    decomposition), the one-rank reference basis orthonormal (max |V^T V - I| <= ORTH_TOL) and every accepted
+    least-squares factor well conditioned (cond(R_Y) <= COND_ACCEPT, the threshold of a second CholeskyQR pass)."""
+    out = tmp_path / "c5.json"
+    rc, err = run_workers(8, "c5_worker.py", ["--out", out], "c5_8192_k200_8ranks", timeout=900)
+    assert rc == 0, err
+    rep = json.loads(out.read_text())
+    print(json.dumps({k: v for k, v in rep.items() if k not in ("multi", "single", "rel_xnorm_diff", "rel_rnorm_diff")}))
+    assert rep["world"] == 8 and rep["max_k"] == 200 and rep["single_basis_k"] == 201, rep["max_k"]
+    assert rep["ranks_identical"] and rep["bookkeeping_equal"]
+    ex, er = np.array(rep["rel_xnorm_diff"]), np.array(rep["rel_rnorm_diff"])
+    assert ex.size == er.size == 200
+    assert np.all(ex[:21] == 0.0) and np.all(er[:21] == 0.0), (ex[:21], er[:21])
+    assert ex.max() <= 1e-12 and er.max() <= 1e-12, (ex.max(), er.max())
+    assert rep["single_max_abs_VtV_minus_I"] <= ORTH_TOL
+    assert rep["max_cond_multi"] <= COND_ACCEPT and rep["max_cond_single"] <= COND_ACCEPT
+
+
 def _c5_run(N, max_iter):
     prob = gnk.BratuPdeProblem(N + 1, 5, 10)
     comm = Comm(single=True)
