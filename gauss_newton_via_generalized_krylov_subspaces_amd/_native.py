@@ -73,6 +73,9 @@ SIGNATURES = {
     "gnk_cg_update_xr": (_c_int, [_c_vp, _c_dbl, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp]),
     "gnk_cg_step_matvec": (_c_int, [_c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_dbl, _c_int, _c_vp, _c_dbl,
                                     _c_vp]),
+    "gnk_cg_step_matvec_dev": (_c_int, [_c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_int, _c_vp, _c_vp, _c_vp]),
+    "gnk_cg_update_xr_dev": (_c_int, [_c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp]),
+    "gnk_cg_scalars": (_c_int, [_c_vp, _c_vp, _c_int, _c_int, _c_vp]),
     "gnk_cg_update_p": (_c_int, [_c_vp, _c_dbl, _c_int, _c_vp, _c_vp]),
     "gnk_cg_sr_update": (_c_int, [_c_vp, _c_dbl, _c_dbl, _c_int, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp,
                                   _c_vp]),
@@ -383,6 +386,21 @@ class HipBackend:
 
     def cg_update_p(self, beta, first, z, p):
         self._call("gnk_cg_update_p", float(beta), int(bool(first)), _p(z), _p(p))
+
+    def cg_step_matvec_dev(self, d, z, p_in, p_out, q, first, x, state, pq):
+        """gnk_cg_step_matvec with beta / the lagged alpha from the device CG state (pairs out)."""
+        self._mode(True, pq, 1, 2, "cg_step_matvec_dev")
+        self._call("gnk_cg_step_matvec_dev", _p(d), _p(z), _p(p_in), _p(p_out), _p(q), int(bool(first)), _p(x),
+                   _p(state), _p(pq))
+
+    def cg_update_xr_dev(self, state, p, q, x, r, dinv, z, out):
+        """gnk_cg_update_xr with alpha from the device CG state (pairs out)."""
+        self._mode(True, out, 2, 4, "cg_update_xr_dev")
+        self._call("gnk_cg_update_xr_dev", _p(state), _p(p), _p(q), _p(x), _p(r), _p(dinv), _p(z), _p(out))
+
+    def cg_scalars(self, parts, world, stage, state):
+        """The fused CG iteration's scalar recurrence on the device (gnk_cg_scalars)."""
+        self._call("gnk_cg_scalars", _p(parts), int(world), int(stage), _p(state))
 
     def timer_start(self, kernel_id, capacity):
         self._chk(self.lib.gnk_timer_start(self.ctx, int(kernel_id), int(capacity)), "timer_start")

@@ -1010,8 +1010,13 @@ __global__ __launch_bounds__(BLOCK) void k_cg_matvec_m(const double* __restrict_
                                                        double* __restrict__ q, Geo geo, Coef c, int64_t rpr,
                                                        double* __restrict__ partial, const double* __restrict__ z,
                                                        double* __restrict__ p, double beta, int first,
-                                                       double* __restrict__ x, double xalpha) {
+                                                       double* __restrict__ x, double xalpha,
+                                                       const double* __restrict__ cst) {
   __shared__ double sh[BLOCK / 64 * 2];
+  if (cst) {                       // device CG state (gnk_cg_scalars): beta = cst[0], lagged alpha = cst[1]
+    beta = cst[0];
+    xalpha = cst[1];
+  }
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int64_t N = geo.N;
   const int nbc = int((N + 4 * CGM_SW - 1) / (4 * CGM_SW));
@@ -1120,8 +1125,9 @@ __global__ __launch_bounds__(BLOCK) void k_cg_xr(double alpha, const double* __r
                                                  const double* __restrict__ q, double* __restrict__ x,
                                                  double* __restrict__ r, const double* __restrict__ dinv,
                                                  double* __restrict__ z, Geo geo, int64_t lr0, int64_t nlr,
-                                                 double* __restrict__ partial) {
+                                                 double* __restrict__ partial, const double* __restrict__ cst) {
   __shared__ double sh[(BLOCK / 64) * 2 * 2];
+  if (cst) alpha = cst[2];         // device CG state (gnk_cg_scalars)
   double acc[2] = {0.0, 0.0}, accc[2] = {0.0, 0.0};
   ROW_LOOP_BEGIN(VEC)
   for (int qq = 0; qq < VEC && iy + qq < N; ++qq) {
@@ -1178,6 +1184,55 @@ __global__ __launch_bounds__(BLOCK) void k_cg_p(double beta, int first, const do
     p[i] = first ? z[i] : p[i] * beta + z[i];
   }
   ROW_LOOP_END
+}
+
+// Device-side scalar recurrence of the fused scipy-cg iteration (DeviceCG._cg_fused_dev): merges the ranks'
+// compensated (s, c) pairs exactly as slab.Comm.merge_pairs does on the host (TwoSum in rank order, the
+// errors and the c accumulated beside, one rounding at the end; one rank: s + c) and forms the step
+// coefficients of scipy iterative.py:305-422 where the host formed them: the same IEEE operations, so the
+// kernels that read them compute the same bits, and no host read sits between two kernels.
+// state: [0] beta = rho / rho_prev  [1] the lagged alpha of the x update  [2] alpha = rho / (p . q)
+//        [3] rho = r . z  [4] rho_prev  [5] r . r  [6] p . q
+// stage 0 (the alpha = 0 update that forms z = M r; parts: rank x [s, c](r.r), [s, c](r.z)): r.r, rho
+// stage 1 (after the normal matvec; parts: rank x [s, c](p.q)):  alpha = rho / p.q
+// stage 2 (after the r, z update; parts as stage 0): r.r; rho_prev = rho, rho = r.z, beta = rho / rho_prev,
+//         the lagged alpha = alpha
+__device__ double merge_pair(const double* __restrict__ parts, int world, int stride, int q) {
+  double S = parts[2 * q], C = parts[2 * q + 1];
+  for (int w = 1; w < world; ++w) {
+    const double sp = parts[w * stride + 2 * q], cp = parts[w * stride + 2 * q + 1];
+    const double x = S + sp;
+    const double z = x - S;
+    const double err = (S - (x - z)) + (sp - z);
+    S = x;
+    C = C + (err + cp);
+  }
+  return S + C;
+}
+
+__global__ __launch_bounds__(64) void k_cg_scalars(const double* __restrict__ parts, int world, int stage,
+                                                   double* __restrict__ st) {
+  if (threadIdx.x != 0) return;
+  if (stage == 1) {
+    const double pq = merge_pair(parts, world, 2, 0);
+    st[6] = pq;
+    st[2] = st[3] / pq;
+    return;
+  }
+  const double rr = merge_pair(parts, world, 4, 0), rz = merge_pair(parts, world, 4, 1);
+  st[5] = rr;
+  if (stage == 0) {
+    st[0] = 0.0;
+    st[1] = 0.0;
+    st[2] = 0.0;
+    st[3] = rz;
+    st[4] = 0.0;
+    return;
+  }
+  st[4] = st[3];
+  st[3] = rz;
+  st[0] = rz / st[4];
+  st[1] = st[2];
 }
 
 // ---------------------------------------------------------------- deterministic partial reduction
@@ -4716,7 +4771,7 @@ int gnk_flat_cg_update_xr(gnk_ctx* ctx, double alpha, const double* p, const dou
   const int vec = flat_vec(n);
   const Geo geo{n, 0, 1};
   RowLaunch L = flat_rows(n, vec);
-  FLAT_DISPATCH(vec, k_cg_xr, L, alpha, p, q, x, r, dinv, z, geo, L.lr0, L.nlr, ctx->scratch);
+  FLAT_DISPATCH(vec, k_cg_xr, L, alpha, p, q, x, r, dinv, z, geo, L.lr0, L.nlr, ctx->scratch, nullptr);
   int rc = check_launch(ctx, "flat_cg_update_xr");
   if (rc) return rc;
   return wreduce2(ctx, ctx->scratch, int(L.grid.x), 2, 4, out);
@@ -4795,7 +4850,7 @@ int gnk_cg_normal_matvec(gnk_ctx* ctx, const double* d, const double* p, double*
     nblk = int(nbc * nranges);
     TimedLaunch tl(ctx, GNK_TIMER_CG_MATVEC, 24.0 * double(nrows) * double(ctx->geo.N));
     hipLaunchKernelGGL(k_cg_matvec_m<false>, dim3(unsigned(nblk)), dim3(BLOCK), 0, ctx->stream, d, p, q, ctx->geo,
-                       ctx->coef, rpr, ctx->scratch, nullptr, nullptr, 0.0, 0, nullptr, 0.0);
+                       ctx->coef, rpr, ctx->scratch, nullptr, nullptr, 0.0, 0, nullptr, 0.0, nullptr);
     tl.done();
   } else {
     RowLaunch L = rows(ctx, G, ctx->geo.nrows, vec_of(ctx));
@@ -4807,8 +4862,9 @@ int gnk_cg_normal_matvec(gnk_ctx* ctx, const double* d, const double* p, double*
   return wreduce2(ctx, ctx->scratch, nblk, 1, 2, pq_out);
 }
 
-int gnk_cg_step_matvec(gnk_ctx* ctx, const double* d, const double* z, const double* p_in, double* p_out, double* q,
-                       double beta, int first, double* x, double xalpha, double* pq_out) {
+static int cg_step_matvec(gnk_ctx* ctx, const double* d, const double* z, const double* p_in, double* p_out,
+                          double* q, double beta, int first, double* x, double xalpha, const double* cst,
+                          double* pq_out) {
   if (!ready(ctx)) return -1;
   if (ctx->geo.N % 2) return fail(ctx, "cg_step_matvec: N must be even (use cg_update_p + cg_normal_matvec)");
   if (!d || !z || !p_in || !p_out || !q || p_in == p_out) return fail(ctx, "cg_step_matvec: bad buffers");
@@ -4821,22 +4877,51 @@ int gnk_cg_step_matvec(gnk_ctx* ctx, const double* d, const double* z, const dou
   const int nblk = int(nbc * nranges);
   TimedLaunch tl(ctx, GNK_TIMER_CG_MATVEC, (x ? 56.0 : 40.0) * double(nrows) * double(ctx->geo.N));
   hipLaunchKernelGGL(k_cg_matvec_m<true>, dim3(unsigned(nblk)), dim3(BLOCK), 0, ctx->stream, d, p_in, q, ctx->geo,
-                     ctx->coef, rpr, ctx->scratch, z, p_out, beta, first, x, xalpha);
+                     ctx->coef, rpr, ctx->scratch, z, p_out, beta, first, x, xalpha, cst);
   tl.done();
   int rc = check_launch(ctx, "cg_step_matvec");
   if (rc) return rc;
   return wreduce2(ctx, ctx->scratch, nblk, 1, 2, pq_out);
 }
 
-int gnk_cg_update_xr(gnk_ctx* ctx, double alpha, const double* p, const double* q, double* x, double* r,
-                     const double* dinv, double* z, double* out) {
+int gnk_cg_step_matvec(gnk_ctx* ctx, const double* d, const double* z, const double* p_in, double* p_out, double* q,
+                       double beta, int first, double* x, double xalpha, double* pq_out) {
+  return cg_step_matvec(ctx, d, z, p_in, p_out, q, beta, first, x, xalpha, nullptr, pq_out);
+}
+
+int gnk_cg_step_matvec_dev(gnk_ctx* ctx, const double* d, const double* z, const double* p_in, double* p_out,
+                           double* q, int first, double* x, const double* state, double* pq_out) {
+  if (!state) return fail(ctx, "cg_step_matvec_dev: NULL state");
+  return cg_step_matvec(ctx, d, z, p_in, p_out, q, 0.0, first, x, 0.0, state, pq_out);
+}
+
+static int cg_update_xr(gnk_ctx* ctx, double alpha, const double* cst, const double* p, const double* q, double* x,
+                        double* r, const double* dinv, double* z, double* out) {
   if (!ready(ctx)) return -1;
   RowLaunch L = rows(ctx, G, ctx->geo.nrows, vec_of(ctx));
   const int nblk = L.grid.x * L.grid.y;
-  DISPATCH_VEC(ctx, k_cg_xr, L, 0, alpha, p, q, x, r, dinv, z, ctx->geo, L.lr0, L.nlr, ctx->scratch);
+  DISPATCH_VEC(ctx, k_cg_xr, L, 0, alpha, p, q, x, r, dinv, z, ctx->geo, L.lr0, L.nlr, ctx->scratch, cst);
   int rc = check_launch(ctx, "cg_update_xr");
   if (rc) return rc;
   return wreduce2(ctx, ctx->scratch, nblk, 2, 4, out);
+}
+
+int gnk_cg_update_xr(gnk_ctx* ctx, double alpha, const double* p, const double* q, double* x, double* r,
+                     const double* dinv, double* z, double* out) {
+  return cg_update_xr(ctx, alpha, nullptr, p, q, x, r, dinv, z, out);
+}
+
+int gnk_cg_update_xr_dev(gnk_ctx* ctx, const double* state, const double* p, const double* q, double* x, double* r,
+                         const double* dinv, double* z, double* out) {
+  if (!state) return fail(ctx, "cg_update_xr_dev: NULL state");
+  return cg_update_xr(ctx, 0.0, state, p, q, x, r, dinv, z, out);
+}
+
+int gnk_cg_scalars(gnk_ctx* ctx, const double* parts, int world, int stage, double* state) {
+  if (!ready(ctx)) return -1;
+  if (!parts || !state || world < 1 || stage < 0 || stage > 2) return fail(ctx, "cg_scalars: bad arguments");
+  hipLaunchKernelGGL(k_cg_scalars, dim3(1), dim3(64), 0, ctx->stream, parts, world, stage, state);
+  return check_launch(ctx, "cg_scalars");
 }
 
 int gnk_cg_sr_update(gnk_ctx* ctx, double alpha, double beta, int first, const double* w, double* p, double* s,

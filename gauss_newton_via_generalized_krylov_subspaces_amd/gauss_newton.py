@@ -147,6 +147,54 @@ class BratuGNOps:
     def cg_axpy(self, x, alpha, p):
         self.be.vec_axpy(x, alpha, p, x, False)                     # x + alpha p (owned rows)
 
+    # device-side scalars (DeviceCG._cg_fused_dev): the fused iteration's kernels read alpha / beta from a
+    # device state that gnk_cg_scalars forms from the ranks' all-gathered pairs -- no host value between
+    # the kernels of an iteration, one (lagged) host read of the state per iteration for the stopping test
+    cg_device_scalars = True
+
+    def cgd_state(self):
+        return self.dev.scalar(8)
+
+    def _cgd_scalars(self, local, stage, st):
+        parts = self.comm.gather_device(local)
+        self.be.cg_scalars(parts, self.comm.world, stage, st)
+
+    def cgd_update_rz0(self, q, r, dinv, z, st):
+        """z = M r and {r.r, rho = r.z} into the state (the alpha = 0 update before the loop)."""
+        self.be.cg_update_xr(0.0, None, q, None, r, dinv, z, self._s2, pairs=True)
+        self._cgd_scalars(self._s2[:4], 0, st)
+
+    def cgd_iteration(self, z, p_in, p_out, q, first, x, r, dinv, zbuf, st):
+        """One fused iteration with the coefficients on the device: direction + lagged x update + normal
+        matvec (alpha = rho / p.q), then r -= alpha q, z = M r (r.r, rho, beta), then z's halo."""
+        self.be.cg_step_matvec_dev(self.dvec, z, p_in, p_out, q, first, x, st, self._s1)
+        self._cgd_scalars(self._s1[:2], 1, st)
+        self.be.cg_update_xr_dev(st, None, q, None, r, dinv, zbuf, self._s2)
+        self._cgd_scalars(self._s2[:4], 2, st)
+        self.cg_halo(z)
+
+    def cgd_read(self, st):
+        """Enqueue the state's copy to the host (pinned, event): a handle for ``cgd_wait``."""
+        if st.device.type != "cuda":
+            return st.detach().clone()
+        if getattr(self, "_cgd_pin", None) is None:
+            self._cgd_pin = [torch.empty(8, dtype=torch.float64, pin_memory=True) for _ in range(2)]
+            self._cgd_i = 0
+        self._cgd_i ^= 1
+        host = self._cgd_pin[self._cgd_i]
+        host.copy_(st, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(st.device))
+        return host, ev
+
+    def cgd_wait(self, h) -> np.ndarray:
+        self.comm.counters["host_wait"] += 1
+        if isinstance(h, torch.Tensor):
+            return h.numpy().copy()
+        host, ev = h
+        ev.synchronize()
+        return host.numpy().copy()
+
     # single-reduction iteration (cg_variant="single_reduction"): the three scalars of one
     # iteration are partial sums in one device buffer, read with one collective
     def cg_sr_update(self, alpha, beta, first, w, p, s, x, r, dinv, u, buf):
@@ -185,6 +233,10 @@ class DeviceCG:
         self.p2 = v() if getattr(ops, "cg_fused", False) else None   # double-buffered direction
         self.dinv = v()
         self.total_iters = 0
+        # device-side CG scalars (ops.cg_device_scalars) and, without a user callback, the lagged host read
+        self.device_scalars = True
+        self.lag_reads = True
+        self.has_callback = False
 
     def solve(self, u, y, cg_rtol=1e-4, preconditioner=True, callback=None, maxiter=None, variant="scipy"):
         """x = argmin ||y - A x||, A = -J(u); returns (x, cg_iter) like ref:gauss_newton.py:11-60.
@@ -195,6 +247,7 @@ class DeviceCG:
         if variant not in ("scipy", "single_reduction"):
             raise ValueError("cg_variant must be 'scipy' or 'single_reduction'")
         self._variant = variant
+        self.has_callback = callback is not None
         ops = self.ops
         ops.cg_rhs(u, y, self.b)                                    # b = A.T @ y
         ops.cg_prepare(u)
@@ -218,6 +271,8 @@ class DeviceCG:
         if getattr(self, "_variant", "scipy") == "single_reduction":
             return self._cg_single_reduction(rtol, dinv, cb, maxiter)
         if self.p2 is not None:
+            if getattr(self.ops, "cg_device_scalars", False) and self.device_scalars:
+                return self._cg_fused_dev(rtol, dinv, cb, maxiter)
             return self._cg_fused(rtol, dinv, cb, maxiter)
         ops = self.ops
         bnrm2 = math.sqrt(ops.sumsq(self.b))
@@ -289,6 +344,59 @@ class DeviceCG:
         if alpha_prev is not None:
             ops.cg_axpy(self.x, alpha_prev, p_in)                       # the last x += alpha p
         return done
+
+    def _cg_fused_dev(self, rtol, dinv, cb, maxiter):
+        """``_cg_fused`` with its scalar recurrence on the device (gnk_cg_scalars): the same
+        IEEE operations on the same values -- the ranks' pairs merged in rank order, alpha = rho / p.q,
+        beta = rho / rho_prev -- so the same bits, but no host value between the kernels of an iteration.
+        The host reads the state once per iteration for the stopping test (||r|| < atol); without a user
+        callback that read is lagged: iteration j + 1 is enqueued before the host waits for iteration j's
+        r.r, so the GPU never idles on the read.  If iteration j's r.r stops the loop, the speculative
+        iteration's first kernel has already applied x += alpha_j p_j -- exactly the trailing update
+        ``_cg_fused`` applies after its loop -- and its r / z updates are dropped with the solve."""
+        ops = self.ops
+        bnrm2 = math.sqrt(ops.sumsq(self.b))
+        atol = max(0.0, float(rtol) * float(bnrm2))
+        self.x.zero_()
+        if bnrm2 == 0:
+            self.x.copy_(self.b)
+            return 0
+        maxiter = ops.n_global * 10 if maxiter is None else min(int(maxiter), ops.n_global * 10)
+        if getattr(self, "_st", None) is None:
+            self._st = ops.cgd_state()
+        st = self._st
+        self.r.copy_(self.b)
+        self.p.zero_()
+        self.p2.zero_()
+        self.q.zero_()
+        ops.cgd_update_rz0(self.q, self.r, dinv, self.z, st)
+        z = self.z if dinv is not None else self.r
+        ops.cg_halo(z)
+        if math.sqrt(float(ops.cgd_wait(ops.cgd_read(st))[5])) < atol:
+            return 0
+        P = (self.p, self.p2)
+        lag = self.lag_reads and not self.has_callback
+
+        def enqueue(j):
+            ops.cgd_iteration(z, P[j % 2], P[(j + 1) % 2], self.q, j == 0, self.x if j > 0 else None,
+                              self.r, dinv, self.z, st)
+
+        j = 0
+        enqueue(0)
+        while True:
+            h = ops.cgd_read(st)                       # the state after iteration j
+            nxt = j + 1 < maxiter
+            if nxt and lag:
+                enqueue(j + 1)                         # speculative: runs while the host waits
+            sv = ops.cgd_wait(h)
+            cb()
+            if math.sqrt(float(sv[5])) < atol or not nxt:      # scipy's stop at the next iteration's top,
+                if not (nxt and lag):                           # or the iteration cap
+                    ops.cg_axpy(self.x, float(sv[2]), P[(j + 1) % 2])    # the last x += alpha p
+                return j + 1
+            if not lag:
+                enqueue(j + 1)
+            j += 1
 
     def _cg_single_reduction(self, rtol, dinv, cb, maxiter):
         """Chronopoulos-Gear PCG (non-parity option): with u = M r, w = A u,

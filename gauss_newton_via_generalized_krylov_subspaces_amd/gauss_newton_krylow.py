@@ -343,21 +343,26 @@ class GNKSolver:
         fuse = self.ops.fuse_trial and self.version == "res_old"
         d, jdd, ds, rr1, h1, slot1 = self._first_trial(x_t, r_t, r_old, fuse, it)   # :86-89, first trial
         last = {"rr": rr1}
+        losses = []                      # every trial's sum r_t^2 (trace: the Armijo comparisons)
 
         def trial(t):                                                     # res_krylow(c + t d)
             if t == 1.0 and "first" not in last:
                 last["first"] = True
+                losses.append(rr1)
                 return rr1
             basis.x(self.e + t * ds, x_t)
             last["rr"] = self._residual(x_t, r_t)
+            losses.append(last["rr"])
             return last["rr"]
 
+        prev_loss = self.rr
         t, ntrial = armijo_device(trial, self.rr, jdd, d)                 # :91-93
         self.nfev += ntrial                                               # :94
         s = np.sum(self.c ** 2)                                           # :96
         self.c += t * d                                                   # :98
         self.e = self.e + t * ds              # the coefficients of the accepted trial point, bit for bit
-        self.trace.append({"t": t, "k": basis.k, "trials": ntrial})
+        self.trace.append({"t": t, "k": basis.k, "trials": ntrial, "prev_loss": prev_loss, "jdd": float(jdd),
+                           "losses": losses})
         self._emit(x_t, last["rr"])                                       # :100
         self.iter = it
         self.x_last = xi

@@ -283,6 +283,19 @@ class Comm:
         self._all_gather_into(buf, t)
         return self._sum_parts_device(buf, t.numel())
 
+    def gather_device(self, t: torch.Tensor) -> torch.Tensor:
+        """The ranks' copies of a small per-rank tensor, rank-major in one tensor on ``t``'s device
+        ([world * n]): a device all-gather on RCCL (no host wait); staged through the host on gloo."""
+        t = t.contiguous().reshape(-1)
+        if self.world == 1:
+            return t
+        if self.stage:
+            return torch.from_numpy(self._gather(t).reshape(-1).copy()).to(t.device)
+        buf = torch.empty(self.world * t.numel(), dtype=t.dtype, device=t.device)
+        self._count_gather(t)
+        self._all_gather_into(buf, t)
+        return buf
+
     def barrier(self):
         if self.world > 1:
             dist.barrier(group=self.group)

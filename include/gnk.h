@@ -235,6 +235,24 @@ int gnk_cg_step_matvec(gnk_ctx* ctx, const double* d, const double* z, const dou
  * out = {r . r, r . z} (owned)              scipy iterative.py:401-415 */
 int gnk_cg_update_xr(gnk_ctx* ctx, double alpha, const double* p, const double* q,
                      double* x, double* r, const double* dinv, double* z, double* out);
+/* The same two kernels with their coefficients read from a device CG state (8 doubles, written by
+ * gnk_cg_scalars): beta = state[0], the lagged x update's alpha = state[1] (step matvec), alpha =
+ * state[2] (update).  No host value between the kernels of an iteration; the same bits as the host-
+ * coefficient forms given the same values.          scipy iterative.py:401-415 */
+int gnk_cg_step_matvec_dev(gnk_ctx* ctx, const double* d, const double* z, const double* p_in,
+                           double* p_out, double* q, int first, double* x, const double* state,
+                           double* pq_out);
+int gnk_cg_update_xr_dev(gnk_ctx* ctx, const double* state, const double* p, const double* q,
+                         double* x, double* r, const double* dinv, double* z, double* out);
+/* The scalar recurrence of the fused iteration on the device.  parts: world ranks' compensated pairs
+ * (gnk_set_reduce_pairs on), merged in rank order exactly as slab.Comm.merge_pairs (TwoSum; one
+ * rank: s + c).  stage 0: parts = rank x {r.r, r.z} of the alpha = 0 update -> state[5] = r.r,
+ * state[3] = rho = r.z; stage 1: parts = rank x {p.q} -> state[6] = p.q, state[2] = rho / p.q;
+ * stage 2: parts = rank x {r.r, r.z} -> state[5] = r.r, state[4] = rho, state[3] = r.z,
+ * state[0] = state[3] / state[4], state[1] = state[2].  One launch of one thread.
+ * Replaces the host's alpha = rho / p.q, beta = rho / rho_prev (scipy iterative.py:401-415) and the
+ * host merge of per-rank pairs (the two host reads per CG iteration of ref:gauss_newton.py:36-58). */
+int gnk_cg_scalars(gnk_ctx* ctx, const double* parts, int world, int stage, double* state);
 /* p = z (first) or p = beta * p + z (owned rows) */
 int gnk_cg_update_p(gnk_ctx* ctx, double beta, int first, const double* z, double* p);
 /* Single-reduction CG (Chronopoulos-Gear) iteration update, the non-parity option of gauss_newton

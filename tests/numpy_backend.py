@@ -403,6 +403,34 @@ class NumpyBackend:
             xv[own] = xv[own] + xalpha * pi[own]
         self.cg_matvec(d, p_out, q, pq)
 
+    def cg_step_matvec_dev(self, d, z, p_in, p_out, q, first, x, state, pq):
+        st = state.numpy()
+        self.cg_step_matvec(d, z, p_in, p_out, q, float(st[0]), first, x, float(st[1]), pq, pairs=True)
+
+    def cg_update_xr_dev(self, state, p, q, x, r, dinv, z, out):
+        self.cg_update_xr(float(state.numpy()[2]), p, q, x, r, dinv, z, out, pairs=True)
+
+    def cg_scalars(self, parts, world, stage, state):
+        """gnk_cg_scalars: the ranks' pairs merged as slab.Comm.merge_pairs, the scipy-cg coefficients."""
+        from gauss_newton_via_generalized_krylov_subspaces_amd.slab import Comm
+        st = state.numpy()
+        P = parts.numpy().reshape(world, -1)
+        if stage == 1:
+            pq = float(Comm.merge_pairs(P[:, :2])[0])
+            st[6] = pq
+            st[2] = st[3] / pq
+            return
+        rr, rz = (float(v) for v in Comm.merge_pairs(P[:, :4]))
+        st[5] = rr
+        if stage == 0:
+            st[0] = st[1] = st[2] = st[4] = 0.0
+            st[3] = rz
+            return
+        st[4] = st[3]
+        st[3] = rz
+        st[0] = rz / st[4]
+        st[1] = st[2]
+
     def cg_update_xr(self, alpha, p, q, x, r, dinv, z, out, pairs=False):
         self._mode(pairs, out, 2, 4, 'cg_update_xr')
         own = slice(GHOST * self.N, (GHOST + self.nrows) * self.N)

@@ -54,9 +54,15 @@ def _run_gnk(N, max_iter, version):
         rec["nfev"].append(nfev)
 
     buf = io.StringIO()
+    # gauss_newton_krylow's own steps (the same GNKSolver it builds for make_res / make_jac), kept so the
+    # test can read the per-step Armijo comparisons of the trace
+    s = gnk.GNKSolver(prob, y, krylow_restart=20, max_iter=max_iter, version=version, callback=cb)
     with contextlib.redirect_stdout(buf):
-        out = gnk.gauss_newton_krylow(prob.make_res(y), u0, prob.make_jac(), krylow_restart=20, max_iter=max_iter,
-                                      version=version, callback=cb)
+        s.setup(u0)
+        while not s.step():
+            pass
+        out = s.finish()
+    rec["trace"] = s.trace
     return out, rec, buf.getvalue().splitlines()
 
 
@@ -74,14 +80,21 @@ def test_c2_full_run_vs_reference(version):
     m = n - 1 if last_tie else n
     assert rec["nfev"][:m] == ref["nfev"][:m]
     if last_tie:                   # the converged step's Armijo count is a rounding tie
-        lo, hi = T.last_nfev_range(f"c2_{version}")
         seen = T.last_nfev_values(f"c2_{version}")
-        tracked = T.DEVICE_LAST_NFEV[f"c2_{version}"]
-        print(f"C2 {version}: last step nfev {rec['nfev'][-1]} (reference {ref['nfev'][-1]}, its reorderings {seen}; "
-              f"tracked device value {tracked})")
-        assert lo <= rec["nfev"][-1] <= hi and out.nrev - rec["nfev"][-1] == case["nrev"] - ref["nfev"][-1]
-        # drift inside the band must show -- the device's own count is tracked
-        assert rec["nfev"][-1] == tracked, "the converged step's Armijo count moved inside the band: re-check, update"
+        print(f"C2 {version}: last step nfev {rec['nfev'][-1]} (reference {ref['nfev'][-1]}, the counts of its "
+              f"reorderings {seen})")
+        # the device's count is one the reference's own arithmetic, reordered, produces (tests/tolerances.py)
+        assert rec["nfev"][-1] in seen and out.nrev - rec["nfev"][-1] == case["nrev"] - ref["nfev"][-1]
+        # ... and why it is a tie: the step's Armijo threshold 0.5 t ||J d||^2 (t <= 1) is below one ulp of the
+        # loss, so every trial's decision (ref:armijo_goldstein.py:57-62) is the sign of the rounding noise of
+        # sum r^2 -- which stays within a few ulps of the previous loss at every trial point
+        last = rec["trace"][-1]
+        ulp = np.finfo(np.float64).eps * last["prev_loss"]
+        noise = [(last["prev_loss"] - c) / ulp for c in last["losses"]]
+        print(f"C2 {version}: last step 0.5 ||J d||^2 = {0.5 * last['jdd'] / ulp:.3g} ulp of the loss; "
+              f"prev - cur per trial, in ulps: {np.round(noise, 2).tolist()}")
+        assert 0.5 * last["jdd"] < ulp and len(noise) == rec["nfev"][-1] - rec["nfev"][-2]
+        assert max(abs(v) for v in noise) <= T.ARMIJO_TIE_ULPS, noise
     else:
         assert out.nrev == case["nrev"]
     tol = T.per_iteration(f"c2_{version}", n)

@@ -246,3 +246,35 @@ def test_tree_sum_is_the_subtree_fold_of_every_power_of_two_partition():
     assert reduction_segments(8192, 8, None) == 1024 and reduction_segments(8192, 1, None) == 0
     assert reduction_segments(8192, 1, True) == 1024 and reduction_segments(8192, 4, False) == 0
     assert reduction_segments(384, 3, None) == 0 and reduction_segments(100, 2, None) == 0
+
+
+def _cg_paths(backend_factory, N=64, maxiter=None, rtol=1e-8, pre=True):
+    """The fused CGLS solve three ways on one Bratu slab: host scalars (``_cg_fused``), device scalars
+    with the lagged stopping read, and device scalars read every iteration -> {name: (x, iterations)}."""
+    from gauss_newton_via_generalized_krylov_subspaces_amd.gauss_newton import BratuGNOps, DeviceCG
+    from gauss_newton_via_generalized_krylov_subspaces_amd.slab import Comm
+    ref_prob, y, u0 = O.bratu_workload(N)
+    prob = gnk.BratuPdeProblem(N + 1, 5, 10)
+    out = {}
+    for name, dev, lag in (("host", False, False), ("device_lagged", True, True), ("device", True, False)):
+        ops = BratuGNOps(prob, y, Comm(single=True), backend=backend_factory())
+        u = ops.load(u0)
+        r0 = ops.vec()
+        ops.residual(u, r0)
+        cg = DeviceCG(ops)
+        cg.device_scalars, cg.lag_reads = dev, lag
+        x, it = cg.solve(u, r0, cg_rtol=rtol, preconditioner=pre, maxiter=maxiter)
+        out[name] = (x[ops.dev.slab.own].cpu().numpy().copy(), it)
+    return out
+
+
+@pytest.mark.parametrize("maxiter,pre", [(None, True), (None, False), (7, True)])
+def test_cg_device_scalars_bit_identical(maxiter, pre):
+    """the fused CG with its scalar recurrence on the device (gnk_cg_scalars, lagged read)
+    gives the host-scalar path's iterates and counts bit for bit -- to convergence and at the cap."""
+    got = _cg_paths(NumpyBackend, maxiter=maxiter, pre=pre)
+    xh, ih = got["host"]
+    assert ih > 5
+    for name in ("device_lagged", "device"):
+        x, it = got[name]
+        assert it == ih and np.array_equal(x, xh), name
