@@ -56,6 +56,8 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=20.0, help="CPU oracle sample budget (0 = skip)")
     ap.add_argument("--jvp-reps", type=int, default=20)
     ap.add_argument("--cg-iters", type=int, default=200, help="CGLS iterations of the C3 line (0 = skip)")
+    ap.add_argument("--no-trial-timer", action="store_true",
+                    help="time only the Gram launches in the timed regions (A/B of the trial timer's event cost)")
     ap.add_argument("--segments", choices=("auto", "on", "off"), default="auto",
                     help="rank-count-independent reductions (slab.reduction_segments): auto = on for N > 1")
     return ap.parse_args()
@@ -480,7 +482,8 @@ def main():
     comm0 = dict(comm.counters)
     for _ in range(args.repeats):
         be.timer_start(_native.TIMER_GRAM, cap)
-        be.timer_add(_native.TIMER_TRIAL)
+        if not args.no_trial_timer:
+            be.timer_add(_native.TIMER_TRIAL)
         tr0 = len(solver.trace)
         comm.barrier()
         torch.cuda.synchronize()

@@ -134,6 +134,7 @@ def solve_gn(N, comm, iters, cg_maxiter):
                  backend=dev.backend, callback=cb, callback_format="device", cg_maxiter=cg_maxiter)
     buf = io.StringIO()
     t0 = time.time()
+    c0 = dict(comm.counters)
     with contextlib.redirect_stdout(buf):
         s.setup(u0)
         del u0
@@ -141,9 +142,12 @@ def solve_gn(N, comm, iters, cg_maxiter):
             pass
         r = s.finish(result_format="torch")
     torch.cuda.synchronize()
+    # collectives and host waits of the whole GN solve per CG iteration (the GN outer steps'
+    # own residual / Armijo reads included, so an upper bound on the CG iteration's)
+    per_cg = {k: (comm.counters[k] - c0[k]) / max(1, s.cg.total_iters) for k in c0}
     out = {"nit": r.nit, "nfev": r.nfev, "njev": r.njev, "success": bool(r.success), **{"it_" + k: v for k, v in rec.items()},
            "t": [t["t"] for t in s.trace], "stdout": buf.getvalue(), "cg_total": s.cg.total_iters,
-           "seconds": time.time() - t0}
+           "seconds": time.time() - t0, "comm_per_cg_iter": per_cg}
     del s, r, y, dev
     torch.cuda.synchronize()
     torch.cuda.empty_cache()
@@ -168,7 +172,7 @@ def gn_phase(a, comm, rank, world):
         log(f"single-rank GN raised {type(e).__name__}: {e}")
         one = {"error": f"{type(e).__name__}: {e}"}
     dist.barrier()
-    strip = lambda d: {k: v for k, v in d.items() if k != "seconds"}   # noqa: E731
+    strip = lambda d: {k: v for k, v in d.items() if k not in ("seconds", "comm_per_cg_iter")}   # noqa: E731
     ranks_identical = all(strip(e) == strip(mine) for e in every)
     exact = ("nit", "nfev", "njev", "success", "it_nfev", "it_cg_iter", "it_xnorm2", "it_rsumsq", "t", "stdout",
              "cg_total")
@@ -179,7 +183,8 @@ def gn_phase(a, comm, rank, world):
     ok = bool(ranks_identical and bit_identical and rel_r <= TOL and mine["nit"] == a.gn_iters)
     return {"ok": ok, "ranks_identical": ranks_identical, "bit_identical": bit_identical, "max_rel_rnorm_diff": rel_r,
             "gn_iters": a.gn_iters, "cg_maxiter": a.cg_maxiter, "multi": strip(mine), "single": strip(one),
-            "seconds_multi": mine["seconds"], "seconds_single": one.get("seconds")}
+            "seconds_multi": mine["seconds"], "seconds_single": one.get("seconds"),
+            "comm_per_cg_iter_multi": mine["comm_per_cg_iter"]}
 
 
 def main():

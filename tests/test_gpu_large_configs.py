@@ -61,6 +61,8 @@ def test_c4_32768_eight_ranks_on_one_gpu(tmp_path):
     print("GN multi:", json.dumps({k: v for k, v in gn["multi"].items() if k != "stdout"}))
     print(f"GN: bit-identical {gn['bit_identical']}, ranks identical {gn['ranks_identical']}, "
           f"max rel ||r_k|| diff {gn['max_rel_rnorm_diff']:.3g}, {gn['seconds_multi']:.1f} s on 8 ranks")
+    print("GN collectives / host waits per CG iteration on 8 ranks:", json.dumps(gn["comm_per_cg_iter_multi"]))
+    assert gn["comm_per_cg_iter_multi"]["host_wait"] <= 1.5      # device CG scalars: one (lagged) read per iteration
     assert gn["ranks_identical"] and gn["bit_identical"], gn
     assert gn["max_rel_rnorm_diff"] == 0.0 and gn["ok"], gn
     assert rep["ok"]
