@@ -1,7 +1,14 @@
 """Conditioning of J V under structured preconditioners on the oracle's GNK run:
 full P = R_prev, column scaling, and P with only its first m rows dense ("rows m") or its leading m x m block
 ("blk m"), per basis size k.  CPU only (oracle).  python tools/cond_struct.py [N]"""
-sys.path.insert(0, "/root/repo")
+import contextlib
+import io
+import os
+import sys
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from oracle import gnk_oracle as O
 N = int(sys.argv[1]) if len(sys.argv) > 1 else 1024
 prob, y, u0 = O.bratu_workload(N)
