@@ -1,12 +1,10 @@
 #!/bin/bash
-# A/B of the product libgnk.so against tools/_var/libgnk_$1.so on the Gram pass: bit-identity and time
-# per k (tools/gram_dump.py), interleaved twice.  Usage: tools/gram_ab.sh VARIANT k1,k2,... [grid]
+# Gram-pass timing per basis size at 8192^2 (tools/kbench.py gram2: the preconditioned pass with r),
+# after the GPU tests of the Gram kernels.  Usage: GRAM_KS="17 20" bash tools/gram_ab.sh
 set -o pipefail
-V=$1; KS=$2; GRID=${3:-8192}
-O=gpurun_out/gram_ab_$V
-mkdir -p $O
-for i in 1 2; do
-  timeout -k 10 300 python3 tools/gram_dump.py $O new $KS --grid $GRID >> $O/times.jsonl || exit $?
-  GNK_LIB=tools/_var/libgnk_$V.so timeout -k 10 300 python3 tools/gram_dump.py $O $V $KS --grid $GRID >> $O/times.jsonl || exit $?
+mkdir -p gpurun_out
+timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_kernels.py -k "gram" > gpurun_out/gram_tests.log 2>&1 || exit $?
+: > gpurun_out/gram_ab.jsonl
+for k in ${GRAM_KS:-9 12 16 17 20}; do
+  timeout -k 10 120 python tools/kbench.py --k $k --reps 10 --kernels ${GRAM_KERNELS:-gram2} >> gpurun_out/gram_ab.jsonl 2>> gpurun_out/gram_ab.err || exit $?
 done
-python3 tools/gram_dump.py --compare $O new $V > $O/bits.jsonl
