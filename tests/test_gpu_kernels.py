@@ -260,6 +260,9 @@ GRAM_CASES = [(24, 1, False, False), (24, 5, True, True), (100, 20, False, False
                                                   (256, 5, True, True), (1024, 6, True, True), (640, 7, True, False),
                                                   (1024, 8, True, True), (256, 9, True, True), (128, 9, True, False),
                                                   (640, 7, True, True), (512, 10, True, True),
+                                                  # k = 8..12 at more grid sizes (one-point VALU / staged MFMA)
+                                                  (256, 11, True, True), (1024, 12, True, True), (640, 10, True, False),
+                                                  (128, 12, True, True), (384, 8, True, False),
                                                   # prefetching wide-basis kernel (KP 32..64; partial tail chunks)
                                                   (64, 51, True, True), (64, 40, False, True), (96, 22, True, True),
                                                   (130, 33, True, True), (48, 60, True, True), (24, 30, True, False),
