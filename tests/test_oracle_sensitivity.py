@@ -189,3 +189,36 @@ def test_rosen2_last_cg_count_is_a_tie(golden, exact_cg):
         O.gauss_newton(res, np.array([2.0, 2.0]), jac, callback=lambda x, nfev, cg_iter: rec.append(cg_iter))
     ref = meta["cases"]["rosen2_2_2_gn"]["per_iter"]["cg_iter"]
     assert rec[:-1] == ref[:-1] and abs(rec[-1] - ref[-1]) == 1
+
+
+def test_c2_res_old_converged_step_is_a_rounding_tie():
+    """The reason C2 res_old's last Armijo count is a family of values (tests/tolerances.py): in the reference's
+    own run (the pinned oracle, one BLAS thread) the converged step's threshold 0.5 t ||J d||^2 is a fraction
+    of one ulp of the loss, so each trial's test prev - cur >= 0.5 t ||J d||^2 (ref:armijo_goldstein.py:57-62)
+    is decided by the rounding of the two sums of squares; its trials sit a few ulps from prev."""
+    prob, y, u0 = O.bratu_workload(1024)
+    rec = []
+    orig = O.armijo_goldstein
+
+    def arm(res, x, res_ev, jac_ev, args, d, max_iter=100, initial_step_length=1.0):
+        prev, jdd = np.sum(res_ev ** 2), np.sum((jac_ev @ d) ** 2)
+        out = orig(res, x, res_ev, jac_ev, args, d, max_iter, initial_step_length)
+        t, losses = 1.0, []
+        for _ in range(out[2]):
+            losses.append(np.sum(res(x + t * d) ** 2))
+            t /= 2
+        rec.append((prev, jdd, losses))
+        return out
+
+    O.armijo_goldstein = arm
+    try:
+        with contextlib.redirect_stdout(io.StringIO()):
+            O.gauss_newton_krylow(prob.make_res(y), u0, prob.make_jac(), krylow_restart=20, max_iter=100,
+                                  version="res_old")
+    finally:
+        O.armijo_goldstein = orig
+    prev, jdd, losses = rec[-1]
+    ulp = np.finfo(np.float64).eps * prev
+    assert 0.5 * jdd < 0.1 * ulp
+    assert all(abs(prev - c) <= T.ARMIJO_TIE_ULPS * ulp for c in losses)
+    assert len(losses) == 2                       # the reference's own count for this step (83 - 81)
