@@ -370,6 +370,14 @@ def launch_ranks(n, cmd, env=None, poll_s=0.2, grace_s=15.0):
     base.update(WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n), GROUP_RANK="0", MASTER_ADDR="127.0.0.1",
                 MASTER_PORT=str(_free_port()), HSA_ENABLE_IPC_MODE_LEGACY="0")
     procs = []
+
+    def _forward(signum, frame):                 # the driver's timeout / Ctrl-C reaches every rank's group
+        for p in procs:
+            with contextlib.suppress(ProcessLookupError):
+                os.killpg(p.pid, signum)
+        raise SystemExit(128 + signum)
+
+    old_handlers = {sig: signal.signal(sig, _forward) for sig in (signal.SIGTERM, signal.SIGINT, signal.SIGHUP)}
     for r in range(n):
         e = dict(base, RANK=str(r), LOCAL_RANK=str(r))
         procs.append(subprocess.Popen(cmd, env=e, start_new_session=True))
@@ -399,6 +407,8 @@ def launch_ranks(n, cmd, env=None, poll_s=0.2, grace_s=15.0):
         for p in procs:
             with contextlib.suppress(Exception):
                 p.wait(timeout=grace_s)
+        for sig, h in old_handlers.items():
+            signal.signal(sig, h)
     return failed if failed >= 0 else 1            # a rank killed by a signal: 1
 
 

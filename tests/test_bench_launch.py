@@ -72,3 +72,18 @@ def test_bench_refuses_too_few_gpus_under_rccl():
         pytest.skip("node has >= 2 GPUs")
     p = _bench(["--gpus", "2"])
     assert p.returncode != 0 and "refusing to measure fewer ranks" in p.stderr, p.stderr[-2000:]
+
+
+def test_launcher_forwards_sigterm_to_every_rank(tmp_path):
+    """A SIGTERM to ``python bench.py --gpus N`` (the driver's timeout) must end every rank, not orphan them
+    in their own sessions."""
+    import signal
+    script = ("import sys, time; sys.path.insert(0, %r); import bench; "
+              "sys.exit(bench.launch_ranks(2, [sys.executable, '-c', 'import time; time.sleep(120)']))" % ROOT)
+    p = subprocess.Popen([sys.executable, "-c", script])
+    time.sleep(3)
+    p.send_signal(signal.SIGTERM)
+    rc = p.wait(timeout=60)
+    assert rc != 0
+    out = subprocess.run(["ps", "-eo", "pid,args"], capture_output=True, text=True).stdout
+    assert "time.sleep(120)" not in out
