@@ -243,6 +243,29 @@ struct RowLaunch {
 
 #define ZSEG_ROW_LOOP_END }}
 
+// ---------------------------------------------------------------- in-row neighbours across lanes
+// Lane l <- lane l - 1 / l + 1 of the wave: DPP wave_shr:1 / wave_shl:1 (gfx9), two 32-bit VALU moves per
+// double instead of the two ds_bpermute LDS round trips __shfl_up / __shfl_down compile to (the k = 8, 9
+// VALU Gram pass 6-9 % faster, bit-identical: profiles/round5/lane_dpp_ab.jsonl).  Lanes 0 / 63 get 0:
+// every caller replaces them with the strip's outer neighbour.  Used by the VALU Gram passes only: in the
+// persistent kernels (grid sized by resident blocks) the lower VGPR count changes the occupancy, hence the
+// grid and the partial sums' rounding -- bit for bit the same per point, not per reduction.
+typedef unsigned int lane_u2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ double lane_prev(double v) {
+  const lane_u2 b = __builtin_bit_cast(lane_u2, v);
+  lane_u2 o;
+  o.x = unsigned(__builtin_amdgcn_mov_dpp(int(b.x), 0x138, 0xf, 0xf, true));
+  o.y = unsigned(__builtin_amdgcn_mov_dpp(int(b.y), 0x138, 0xf, 0xf, true));
+  return __builtin_bit_cast(double, o);
+}
+__device__ __forceinline__ double lane_next(double v) {
+  const lane_u2 b = __builtin_bit_cast(lane_u2, v);
+  lane_u2 o;
+  o.x = unsigned(__builtin_amdgcn_mov_dpp(int(b.x), 0x130, 0xf, 0xf, true));
+  o.y = unsigned(__builtin_amdgcn_mov_dpp(int(b.y), 0x130, 0xf, 0xf, true));
+  return __builtin_bit_cast(double, o);
+}
+
 // ---------------------------------------------------------------- operator kernels
 template <int VEC>
 __global__ __launch_bounds__(BLOCK) void k_jvp(const double* __restrict__ u, const double* __restrict__ v,
@@ -2833,7 +2856,7 @@ __global__ __launch_bounds__(BLOCK) void k_gram_v(const double* __restrict__ u, 
       double a[K];
 #pragma unroll
       for (int j = 0; j < K; ++j) {
-        double w = __shfl_up(vc[j].y, 1);
+        double w = lane_prev(vc[j].y);
         if (edge_w) w = eo[j];
         double s0 = c.hm2 * vn[j].x;
         s0 = fma(cw0, w, s0);
@@ -2845,7 +2868,7 @@ __global__ __launch_bounds__(BLOCK) void k_gram_v(const double* __restrict__ u, 
       gram_v_point<K>(a, rr.x, T, ldt, acc);
 #pragma unroll
       for (int j = 0; j < K; ++j) {
-        double e = __shfl_down(vc[j].x, 1);
+        double e = lane_next(vc[j].x);
         if (edge_e) e = eo[j];
         double s1 = c.hm2 * vn[j].y;
         s1 = fma(c.hm2, vc[j].x, s1);
@@ -2917,8 +2940,8 @@ __global__ __launch_bounds__(BLOCK) void k_gram_v1(const double* __restrict__ u,
       double a[K];
 #pragma unroll
       for (int j = 0; j < K; ++j) {
-        double w = __shfl_up(vc[j], 1);
-        double e = __shfl_down(vc[j], 1);
+        double w = lane_prev(vc[j]);
+        double e = lane_next(vc[j]);
         if (edge_w) w = eo[j];
         if (edge_e) e = eo[j];
         double sv = c.hm2 * vn[j];

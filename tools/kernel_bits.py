@@ -1,0 +1,83 @@
+"""Bit-level fingerprint of the Bratu operator, basis and Gram kernels on fixed random inputs, for comparing two
+library builds (GNK_LIB) kernel by kernel:  python tools/kernel_bits.py OUT.npz [--grid N] ;
+python tools/kernel_bits.py --compare A.npz B.npz"""
+import argparse
+import os
+import sys
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def run(out, N, K):
+    from gauss_newton_via_generalized_krylov_subspaces_amd import BratuPdeProblem
+    from gauss_newton_via_generalized_krylov_subspaces_amd._device import BratuDevice
+    from gauss_newton_via_generalized_krylov_subspaces_amd.slab import Comm
+    torch.cuda.set_device(0)
+    dev = BratuDevice(BratuPdeProblem(N + 1, 5, 10), Comm(single=True))
+    be, sl = dev.backend, dev.slab
+    g = torch.Generator(device=be.device).manual_seed(1)
+    n = N * N
+
+    def rnd(scale=1.0):
+        v = dev.vec()
+        v[sl.own] = scale * torch.randn(n, generator=g, device=be.device, dtype=torch.float64)
+        return v
+
+    u, v, w, y, r = rnd(0.1), rnd(), rnd(), rnd(), rnd()
+    V = be.zeros(K + 1, sl.length)
+    V[:, sl.own] = torch.randn(K + 1, n, generator=g, device=be.device, dtype=torch.float64) / np.sqrt(n)
+    res = {}
+
+    def keep(name, t):
+        torch.cuda.synchronize()
+        res[name] = t.detach().cpu().numpy().copy()
+
+    o = dev.vec(); be.jvp(u, v, o); keep("jvp", o)
+    o = dev.vec(); be.vjp(u, w, o); keep("vjp", o)
+    o = dev.vec(); be.forward(u, o); keep("forward", o)
+    o = dev.vec(); nr = be.zeros(64); be.residual(u, y, o, nr); keep("residual", o); keep("residual_n2", nr)
+    for k in (1, 5, 12):
+        c = be.to_device(np.linspace(0.5, 1.5, 64))
+        hh = be.to_device(np.linspace(-0.1, 0.1, 64))
+        gg, h, x = dev.vec(), be.zeros(256), dev.vec()
+        be.vjp_gemv_t(u, r, V, k, gg, h); keep(f"vjp_gemv_t{k}_g", gg); keep(f"vjp_gemv_t{k}_h", h)
+        gg, h, x = dev.vec(), be.zeros(256), dev.vec()
+        be.gemv_vjp_gemv_t(V, k, c, r, x, gg, h); keep(f"trial{k}_x", x); keep(f"trial{k}_g", gg); keep(f"trial{k}_h", h)
+        Vp = V.clone()
+        gg, h, x, st = dev.vec(), be.zeros(256), dev.vec(), be.zeros(64)
+        be.gemv_vjp_gemv_t_pending(Vp, k, c, hh, r, x, gg, h, st)
+        keep(f"trialp{k}_x", x); keep(f"trialp{k}_g", gg); keep(f"trialp{k}_h", h); keep(f"trialp{k}_w", Vp[k])
+    o, jn = dev.vec(), be.zeros(64)
+    be.normalize_jnorm(u, w, 3.0, o, jn); keep("normalize", o); keep("normalize_jn", jn)
+    for k in range(1, K + 1):
+        kp = be.gram_dim(k, True)
+        rinv = np.zeros((kp, kp))
+        rinv[:k + 1, :k + 1] = np.triu(np.ones((k + 1, k + 1))) * 0.1 + np.eye(k + 1)
+        G = be.zeros(kp * kp)
+        be.gram(u, V[:k], k, be.to_device(rinv.reshape(-1)), r, G); keep(f"gram{k}", G)
+    np.savez(out, **res)
+
+
+def compare(a, b):
+    A, B = np.load(a), np.load(b)
+    for key in A.files:
+        x, z = A[key], B[key]
+        same = np.array_equal(x.view(np.int64), z.view(np.int64))
+        d = float(np.max(np.abs(x - z))) if not same else 0.0
+        print(f"{key:24s} {'identical' if same else 'DIFFERS'} {d:.3e}")
+
+
+if __name__ == "__main__":
+    ap = argparse.ArgumentParser()
+    ap.add_argument("out", nargs="?")
+    ap.add_argument("--grid", type=int, default=1024)
+    ap.add_argument("--k", type=int, default=12)
+    ap.add_argument("--compare", nargs=2)
+    a = ap.parse_args()
+    if a.compare:
+        compare(*a.compare)
+    else:
+        run(a.out, a.grid, a.k)
