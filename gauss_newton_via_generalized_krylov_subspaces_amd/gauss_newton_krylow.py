@@ -406,8 +406,17 @@ class GNKSolver:
             self._settle_explicit()
         if restart:                                                       # :135-136
             xr = self._free_x(self.uJ)
-            if basis.pending and hasattr(basis, "x_settle"):
-                # the pending column's breakdown test rides on the restart point's GEMV
+            xstats = None
+            if basis.pending and hasattr(basis, "x_settle_start"):
+                # the pending column's breakdown test rides on the restart point's GEMV, and the restart
+                # point's norm comes back in the same host read
+                it_p = basis.pend["it"]
+                brk, xstats = basis.x_settle_start(self.e, self.xb[xr])
+                if brk:
+                    self._breakdown_message(it_p)
+                else:
+                    self._append_coordinate()
+            elif basis.pending and hasattr(basis, "x_settle"):
                 it_p = basis.pend["it"]
                 if basis.x_settle(self.e, self.xb[xr]):
                     self._breakdown_message(it_p)
@@ -417,7 +426,7 @@ class GNKSolver:
                 if basis.pending:
                     self._settle_explicit()
                 basis.x(self.e, self.xb[xr])
-            self.c = basis.start(self.xb[xr])
+            self.c = basis.start(self.xb[xr]) if xstats is None else basis.start(self.xb[xr], stats=xstats)
             self.e = self.c.copy()
             self.lls.on_restart()
         if self._spec is not None:

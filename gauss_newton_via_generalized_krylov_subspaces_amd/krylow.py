@@ -73,6 +73,7 @@ class DeviceKrylovBasis:
         self._hh = self.be.zeros(self.kmax)
         self._h = self.be.zeros(self.kmax + 1)
         self._stats = self.be.zeros(2)
+        self._stats2 = self.be.zeros(4)                   # x_settle_start: [sum w^2, max |w|, sum x^2, max |x|]
         # [sum r^2, sum w^2, max |w|, h_0 .. h_k] of a first trial: one collective / host read (the
         # speculative next step reads it on the device before the next trial overwrites it, in
         # stream order)
@@ -113,10 +114,14 @@ class DeviceKrylovBasis:
         the settled columns, 1 on a pending one (its step is already in raw units)."""
         return np.append(self.sc[:self.k], 1.0) if self.pend is not None else self.sc[:self.k].copy()
 
-    def start(self, x):
-        """ref:krylow.py:30-39.  ``x`` is a slab vector valid on owned +-GHOST rows; returns [||x||]."""
-        self.be.vec_stats(x, self._stats)
-        sumsq, maxabs = self.dev.comm.sum_max(self._stats)
+    def start(self, x, stats=None):
+        """ref:krylow.py:30-39.  ``x`` is a slab vector valid on owned +-GHOST rows; returns [||x||].
+        ``stats``: x's rank-summed (sum x^2, max |x|), already read (``x_settle_start``)."""
+        if stats is None:
+            self.be.vec_stats(x, self._stats)
+            sumsq, maxabs = self.dev.comm.sum_max(self._stats)
+        else:
+            sumsq, maxabs = stats
         if maxabs <= 1e-8:                                    # np.allclose(x0, 0) (:31)
             raise ValueError("x0 is not allowed to be 0 in the gauss_newton_krylow algorithm")
         nrm = math.sqrt(sumsq)                                # np.linalg.norm (:36)
@@ -229,6 +234,25 @@ class DeviceKrylovBasis:
         self.be.gemv_pending(self.V, k, self._c, self._hh, out, self._stats)
         sumsq, maxabs = self.dev.comm.sum_max(self._stats)
         return self.resolve(sumsq, maxabs)
+
+    def x_settle_start(self, e: np.ndarray, out):
+        """``x_settle`` with the stats ``start`` needs of its result read back in the same host read: the
+        restart point out = V @ e does not depend on the pending column's breakdown decision (the column
+        enters with coefficient 0), so its sum x^2 / max |x| (the kernel ``start`` would launch next) are
+        enqueued behind the settling GEMV and both [sum, max] pairs come back in one collective.  The same
+        kernels and the same rank combine as x_settle then start: bit for bit.  Returns (breakdown,
+        (sum x^2, max |x|)) -- pass the latter to ``start``."""
+        k = self.k
+        if self.pend is None or self.pend["slot"] != k:
+            raise RuntimeError("x_settle_start: no pending column in slot k")
+        if len(e) != k:
+            raise RuntimeError("x_settle_start: coefficient vector must cover the settled columns")
+        self.be.upload(self._c, np.append(e, 0.0))
+        self.be.upload(self._hh, self.pend["hh"])
+        self.be.gemv_pending(self.V, k, self._c, self._hh, out, self._stats2[0:2])
+        self.be.vec_stats(out, self._stats2[2:4])
+        (sw, mw), xs = self.dev.comm.sum_max_pairs(self._stats2, 2)
+        return self.resolve(sw, mw), xs
 
     # -- basis update ------------------------------------------------------------------------
     def update(self, u_jac, r, it=None, products=None, prod_slot=None, halo=True):

@@ -165,6 +165,22 @@ class Comm:
         sums, m = self.sum_and_max(t, 1)
         return float(sums[0]), m
 
+    def sum_max_pairs(self, t: torch.Tensor, n: int) -> list:
+        """t = [s_0, m_0, s_1, m_1, ..] (n [sum, max] pairs) per rank -> [(sum over ranks, NaN-propagating
+        max over ranks)] * n: ``sum_max``'s arithmetic for each pair, several of them in one collective and
+        one host read."""
+        parts = self._gather(t[:2 * n])
+        sums = tree_sum(parts[:, 0::2])
+        out = []
+        for i in range(n):
+            m = float(parts[0][2 * i + 1])
+            for p in range(1, parts.shape[0]):
+                v = float(parts[p][2 * i + 1])
+                if v > m or math.isnan(v):
+                    m = v
+            out.append((float(sums[i]), m))
+        return out
+
     def sum_and_max(self, t: torch.Tensor, nsum: int) -> tuple[np.ndarray, float]:
         """t = [s_0 .. s_{nsum-1}, m] per rank -> (sums over ranks, NaN-propagating max): several
         control scalars of one step in one collective and one host read."""
