@@ -1,6 +1,6 @@
 """Per-kernel microbenchmark on the 8192^2 slab (for rocprofv3 counter passes and A/B tests).
 
-python tools/kbench.py [--grid N] [--k K] [--reps R] [--kernels gram1,gram2,jvp,gemv,vjpg,norm,cgs,resid,cg]
+python tools/kbench.py [--grid N] [--k K] [--reps R] [--kernels gram1,gram2,jvp,gemv,vjpg,norm,cgs,resid,cg,gemvp]
 Prints one JSON line with the median ms and algorithmic GB/s per kernel.
 """
 import argparse
@@ -68,6 +68,8 @@ def main():
         "cg": (lambda: be.cg_matvec(d, r, q, st), 24.0 * n),
         "gram2n": (lambda: be.gram(u, V, k + 1, tf_d, r, Gn), 8.0 * n * (k + 3)),
         "trialp": (lambda: be.gemv_vjp_gemv_t_pending(V, k - 1, c, hh, r, x, V[k], h, st), 8.0 * n * (k + 5)),
+        # restart point with the pending column settled (k settled columns + the pending one: k + 1 reads, 2 writes)
+        "gemvp": (lambda: be.gemv_pending(V, k, c, hh, x, st), 8.0 * n * (k + 3)),
     }
     out = {"grid": N, "k": k}
     for name in a.kernels.split(","):

@@ -27,8 +27,8 @@ def run(out, N, K):
         return v
 
     u, v, w, y, r = rnd(0.1), rnd(), rnd(), rnd(), rnd()
-    V = be.zeros(K + 1, sl.length)
-    V[:, sl.own] = torch.randn(K + 1, n, generator=g, device=be.device, dtype=torch.float64) / np.sqrt(n)
+    V = be.zeros(max(K, 20) + 1, sl.length)
+    V[:, sl.own] = torch.randn(V.shape[0], n, generator=g, device=be.device, dtype=torch.float64) / np.sqrt(n)
     res = {}
 
     def keep(name, t):
@@ -50,6 +50,12 @@ def run(out, N, K):
         gg, h, x, st = dev.vec(), be.zeros(256), dev.vec(), be.zeros(64)
         be.gemv_vjp_gemv_t_pending(Vp, k, c, hh, r, x, gg, h, st)
         keep(f"trialp{k}_x", x); keep(f"trialp{k}_g", gg); keep(f"trialp{k}_h", h); keep(f"trialp{k}_w", Vp[k])
+    for k in (1, 5, 12, 20):
+        c = be.to_device(np.linspace(0.5, 1.5, 64))
+        hh = be.to_device(np.linspace(-0.1, 0.1, 64))
+        Vp, x, st = V.clone(), dev.vec(), be.zeros(64)
+        be.gemv_pending(Vp, k, c, hh, x, st)
+        keep(f"gemvp{k}_x", x); keep(f"gemvp{k}_w", Vp[k]); keep(f"gemvp{k}_max", st[1:2])
     o, jn = dev.vec(), be.zeros(64)
     be.normalize_jnorm(u, w, 3.0, o, jn); keep("normalize", o); keep("normalize_jn", jn)
     for k in range(1, K + 1):
