@@ -166,3 +166,51 @@ def test_slab_input_staging(world):
     F = one.vec()
     one.backend.forward(one.load(prob.u_true), F)
     np.testing.assert_array_equal(outs[0][4], F[one.slab.own].numpy())   # the same F as one rank computes
+
+
+def _sum_max_pairs_worker(rank, world, port, q):
+    """Comm.sum_max_pairs (the restart step's single read) against sum_max on each pair: the same sums in
+    tree_sum's order, the same NaN-propagating max."""
+    import sys
+    sys.path.insert(0, ROOT)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import torch
+        from gauss_newton_via_generalized_krylov_subspaces_amd.slab import Comm
+        comm = Comm()
+        rng = np.random.default_rng(100 + rank)
+        vals = [float(rng.standard_normal()) * 10.0 ** int(rng.integers(-8, 8)) for _ in range(4)]
+        if rank == world - 1:
+            vals[3] = float("nan")                # a NaN max on one rank wins
+        t = torch.tensor(vals + [7.0, 7.0], dtype=torch.float64)
+        both = comm.sum_max_pairs(t, 2)
+        one = [comm.sum_max(torch.tensor(vals[0:2], dtype=torch.float64)),
+               comm.sum_max(torch.tensor(vals[2:4], dtype=torch.float64))]
+        q.put((rank, both, one))
+    except BaseException as e:
+        q.put((rank, "error", repr(e)))
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sum_max_pairs_equals_sum_max(world):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_sum_max_pairs_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    outs = sorted([q.get(timeout=300) for _ in procs], key=lambda o: o[0])
+    for p in procs:
+        p.join(timeout=60)
+    for o in outs:
+        assert o[1] != "error", o
+        (s0, m0), (s1, m1) = o[1]
+        (t0, n0), (t1, n1) = o[2]
+        assert s0 == t0 and m0 == n0 and s1 == t1
+        assert np.isnan(m1) and np.isnan(n1)
+    assert all(o[1][0] == outs[0][1][0] for o in outs)     # every rank the same decision inputs
