@@ -1086,8 +1086,8 @@ __global__ __launch_bounds__(BLOCK) void k_cg_matvec_m(const double* __restrict_
   };
   // t = J p at this lane's two points of row x (0 outside the domain)
   auto trow = [&](int64_t xr, d2 pn, d2 pc, d2 ps, d2 xc, d2 dc) -> d2 {
-    double pw = __shfl_up(pc.y, 1);
-    double pe = __shfl_down(pc.x, 1);
+    double pw = lane_prev(pc.y);
+    double pe = lane_next(pc.x);
     if (lane == 0) pw = xc.y;
     if (lane == 63) pe = xc.x;
     const int64_t gx = geo.row0 + xr;
@@ -1120,8 +1120,8 @@ __global__ __launch_bounds__(BLOCK) void k_cg_matvec_m(const double* __restrict_
       const double te = jvp_pt(c, l0 ? eB.y : eB.x, l0 ? xA.y : xA.x, l0 ? xB.x : pC.y, l0 ? col0 - 1 > 0 : true,
                                l0 ? xB.y : xB.x, l0 ? pC.x : xB.y, l0 ? true : col0 + CGM_SW < N - 1,
                                l0 ? xC.y : xC.x);
-      double tw = __shfl_up(tc.y, 1);
-      double tE = __shfl_down(tc.x, 1);
+      double tw = lane_prev(tc.y);
+      double tE = lane_next(tc.x);
       if (lane == 0) tw = te;
       if (lane == 63) tE = te;
       if (valid) {
@@ -1153,15 +1153,42 @@ __global__ __launch_bounds__(BLOCK) void k_cg_xr(double alpha, const double* __r
   if (cst) alpha = cst[2];         // device CG state (gnk_cg_scalars)
   double acc[2] = {0.0, 0.0}, accc[2] = {0.0, 0.0};
   ROW_LOOP_BEGIN(VEC)
-  for (int qq = 0; qq < VEC && iy + qq < N; ++qq) {
-    const int64_t i = li + qq;
-    if (x) x[i] = x[i] + alpha * p[i];                 // NULL x: done by the fused matvec (lagged)
-    const double ri = r[i] - alpha * q[i];
-    r[i] = ri;
-    const double zi = dinv ? 0.0 + dinv[i] * ri : ri;
-    if (dinv) z[i] = zi;
-    comp_dot(acc[0], accc[0], ri, ri);
-    comp_dot(acc[1], accc[1], ri, zi);
+  if (VEC == 2 && iy + 1 < N) {
+    // the two points as 16-B pairs (the loop below's arithmetic and accumulation order, point by point)
+    if (x) {                                           // NULL x: done by the fused matvec (lagged)
+      const d2 pv = *reinterpret_cast<const d2*>(p + li);
+      d2 xv = *reinterpret_cast<const d2*>(x + li);
+      xv.x = xv.x + alpha * pv.x;
+      xv.y = xv.y + alpha * pv.y;
+      *reinterpret_cast<d2*>(x + li) = xv;
+    }
+    const d2 qv = *reinterpret_cast<const d2*>(q + li);
+    d2 rv = *reinterpret_cast<const d2*>(r + li);
+    rv.x = rv.x - alpha * qv.x;
+    rv.y = rv.y - alpha * qv.y;
+    *reinterpret_cast<d2*>(r + li) = rv;
+    d2 zv = rv;
+    if (dinv) {
+      const d2 dv = *reinterpret_cast<const d2*>(dinv + li);
+      zv.x = 0.0 + dv.x * rv.x;
+      zv.y = 0.0 + dv.y * rv.y;
+      *reinterpret_cast<d2*>(z + li) = zv;
+    }
+    comp_dot(acc[0], accc[0], rv.x, rv.x);
+    comp_dot(acc[1], accc[1], rv.x, zv.x);
+    comp_dot(acc[0], accc[0], rv.y, rv.y);
+    comp_dot(acc[1], accc[1], rv.y, zv.y);
+  } else {
+    for (int qq = 0; qq < VEC && iy + qq < N; ++qq) {
+      const int64_t i = li + qq;
+      if (x) x[i] = x[i] + alpha * p[i];
+      const double ri = r[i] - alpha * q[i];
+      r[i] = ri;
+      const double zi = dinv ? 0.0 + dinv[i] * ri : ri;
+      if (dinv) z[i] = zi;
+      comp_dot(acc[0], accc[0], ri, ri);
+      comp_dot(acc[1], accc[1], ri, zi);
+    }
   }
   ROW_LOOP_END
   block_sum2_store<2>(acc, accc, 2, partial + 4 * (blockIdx.y * gridDim.x + blockIdx.x), sh);
@@ -4791,7 +4818,9 @@ int gnk_flat_axpy(gnk_ctx* ctx, const double* x, double alpha, const double* d, 
 int gnk_flat_cg_update_xr(gnk_ctx* ctx, double alpha, const double* p, const double* q, double* x, double* r,
                           const double* dinv, double* z, int64_t n, double* out) {
   if (!ctx_ok(ctx)) return -1;
-  const int vec = flat_vec(n);
+  // 16-B pairs only on 16-B aligned vectors (k_cg_xr's two-point path)
+  const auto al = [](const void* ptr) { return (reinterpret_cast<uintptr_t>(ptr) & 15) == 0; };
+  const int vec = (al(p) && al(q) && al(x) && al(r) && al(dinv) && al(z)) ? flat_vec(n) : 1;
   const Geo geo{n, 0, 1};
   RowLaunch L = flat_rows(n, vec);
   FLAT_DISPATCH(vec, k_cg_xr, L, alpha, p, q, x, r, dinv, z, geo, L.lr0, L.nlr, ctx->scratch, nullptr);

@@ -56,6 +56,17 @@ def run(out, N, K):
         Vp, x, st = V.clone(), dev.vec(), be.zeros(64)
         be.gemv_pending(Vp, k, c, hh, x, st)
         keep(f"gemvp{k}_x", x); keep(f"gemvp{k}_w", Vp[k]); keep(f"gemvp{k}_max", st[1:2])
+    # CG: the normal matvec, the fused step matvec (direction update + lagged x) and the x / r update
+    d = dev.vec(); be.jdiag(u, d)
+    q, pq = dev.vec(), be.zeros(8)
+    be.cg_matvec(d, v, q, pq, pairs=True); keep("cg_matvec_q", q); keep("cg_matvec_pq", pq)
+    p_out, q2, x2, pq2 = dev.vec(), dev.vec(), w.clone(), be.zeros(8)
+    be.cg_step_matvec(d, y, v, p_out, q2, 0.7, False, x2, 0.3, pq2, pairs=True)
+    keep("cg_step_p", p_out); keep("cg_step_q", q2); keep("cg_step_x", x2); keep("cg_step_pq", pq2)
+    x3, r3, z3, o3 = w.clone(), r.clone(), dev.vec(), be.zeros(8)
+    dinv = dev.vec(); dinv[sl.own] = 1.0 / (1.0 + u[sl.own] ** 2)
+    be.cg_update_xr(0.45, v, q, x3, r3, dinv, z3, o3, pairs=True)
+    keep("cg_xr_x", x3); keep("cg_xr_r", r3); keep("cg_xr_z", z3); keep("cg_xr_dots", o3)
     o, jn = dev.vec(), be.zeros(64)
     be.normalize_jnorm(u, w, 3.0, o, jn); keep("normalize", o); keep("normalize_jn", jn)
     for k in range(1, K + 1):
