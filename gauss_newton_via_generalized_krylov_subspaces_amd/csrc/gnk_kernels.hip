@@ -874,10 +874,18 @@ __global__ __launch_bounds__(BLOCK) void k_stats(const double* __restrict__ x, G
   __shared__ double sh[BLOCK / 64][3];
   double ss = 0.0, sc = 0.0, mx = 0.0;
   ROW_LOOP_BEGIN(VEC)
-  for (int q = 0; q < VEC && iy + q < N; ++q) {
-    const double xi = x[li + q];
-    comp_dot(ss, sc, xi, xi);
-    mx = nan_max(mx, fabs(xi));
+  if (VEC == 2 && iy + 1 < N) {                     // one 16-B pair, the loop's order point by point
+    const d2 xv = *reinterpret_cast<const d2*>(x + li);
+    comp_dot(ss, sc, xv.x, xv.x);
+    mx = nan_max(mx, fabs(xv.x));
+    comp_dot(ss, sc, xv.y, xv.y);
+    mx = nan_max(mx, fabs(xv.y));
+  } else {
+    for (int q = 0; q < VEC && iy + q < N; ++q) {
+      const double xi = x[li + q];
+      comp_dot(ss, sc, xi, xi);
+      mx = nan_max(mx, fabs(xi));
+    }
   }
   ROW_LOOP_END
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -899,7 +907,12 @@ template <int VEC>
 __global__ __launch_bounds__(BLOCK) void k_div(const double* __restrict__ src, double denom, double* __restrict__ dst,
                                                Geo geo, int64_t lr0, int64_t nlr) {
   ROW_LOOP_BEGIN(VEC)
-  for (int q = 0; q < VEC && iy + q < N; ++q) dst[li + q] = src[li + q] / denom;
+  if (VEC == 2 && iy + 1 < N) {
+    const d2 sv = *reinterpret_cast<const d2*>(src + li);
+    *reinterpret_cast<d2*>(dst + li) = d2{sv.x / denom, sv.y / denom};
+  } else {
+    for (int q = 0; q < VEC && iy + q < N; ++q) dst[li + q] = src[li + q] / denom;
+  }
   ROW_LOOP_END
 }
 
@@ -957,9 +970,15 @@ template <int VEC>
 __global__ __launch_bounds__(BLOCK) void k_axpy(const double* __restrict__ x, double alpha, const double* __restrict__ d,
                                                 double* __restrict__ out, Geo geo, int64_t lr0, int64_t nlr) {
   ROW_LOOP_BEGIN(VEC)
-  for (int q = 0; q < VEC && iy + q < N; ++q) {
-    const double td = alpha * d[li + q];
-    out[li + q] = x[li + q] + td;
+  if (VEC == 2 && iy + 1 < N) {
+    const d2 dv = *reinterpret_cast<const d2*>(d + li), xv = *reinterpret_cast<const d2*>(x + li);
+    const double t0 = alpha * dv.x, t1 = alpha * dv.y;
+    *reinterpret_cast<d2*>(out + li) = d2{xv.x + t0, xv.y + t1};
+  } else {
+    for (int q = 0; q < VEC && iy + q < N; ++q) {
+      const double td = alpha * d[li + q];
+      out[li + q] = x[li + q] + td;
+    }
   }
   ROW_LOOP_END
 }
@@ -970,7 +989,12 @@ template <int VEC>
 __global__ __launch_bounds__(BLOCK) void k_jdiag(const double* __restrict__ u, double* __restrict__ d, Geo geo,
                                                  Coef c, int64_t lr0, int64_t nlr) {
   ROW_LOOP_BEGIN(VEC)
-  for (int q = 0; q < VEC && iy + q < N; ++q) d[li + q] = jdiag(c, u[li + q]);
+  if (VEC == 2 && iy + 1 < N) {
+    const d2 uv = *reinterpret_cast<const d2*>(u + li);
+    *reinterpret_cast<d2*>(d + li) = d2{jdiag(c, uv.x), jdiag(c, uv.y)};
+  } else {
+    for (int q = 0; q < VEC && iy + q < N; ++q) d[li + q] = jdiag(c, u[li + q]);
+  }
   ROW_LOOP_END
 }
 
@@ -3900,6 +3924,9 @@ int tuning(const gnk_ctx* ctx, int key) { return ctx->tune[key]; }
 // flat geometry helpers (generic problems)
 bool ctx_ok(gnk_ctx* ctx) { return ctx != nullptr; }
 int flat_vec(int64_t n, int64_t ldv = 0) { return (n % 2 == 0 && ldv % 2 == 0) ? 2 : 1; }
+// the two-point paths of the streaming kernels move 16-B pairs: a flat vector that is not 16-B aligned (a view
+// at an odd offset; NULL counts as aligned) runs one point per lane
+bool al16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
 RowLaunch flat_rows(int64_t n, int vec, int cap = MAX_RED_BLOCKS) {
   RowLaunch L;
   const int64_t per = int64_t(BLOCK) * vec;
@@ -4776,7 +4803,7 @@ int gnk_flat_cgs_update(gnk_ctx* ctx, const double* V, int64_t ldv, int k, const
 int gnk_flat_stats(gnk_ctx* ctx, const double* x, int64_t n, double* stats_out) {
   if (!ctx_ok(ctx)) return -1;
   if (n < 1) return fail(ctx, "flat_stats: n < 1");
-  const int vec = flat_vec(n);
+  const int vec = al16(x) ? flat_vec(n) : 1;
   const Geo geo{n, 0, 1};
   RowLaunch L = flat_rows(n, vec);
   FLAT_DISPATCH(vec, k_stats, L, x, geo, L.lr0, L.nlr, ctx->scratch);
@@ -4799,7 +4826,7 @@ int gnk_flat_dot(gnk_ctx* ctx, const double* a, const double* b, int64_t n, doub
 
 int gnk_flat_div(gnk_ctx* ctx, const double* src, double denom, double* dst, int64_t n) {
   if (!ctx_ok(ctx)) return -1;
-  const int vec = flat_vec(n);
+  const int vec = (al16(src) && al16(dst)) ? flat_vec(n) : 1;
   const Geo geo{n, 0, 1};
   RowLaunch L = flat_rows(n, vec, 1 << 30);
   FLAT_DISPATCH(vec, k_div, L, src, denom, dst, geo, L.lr0, L.nlr);
@@ -4808,7 +4835,7 @@ int gnk_flat_div(gnk_ctx* ctx, const double* src, double denom, double* dst, int
 
 int gnk_flat_axpy(gnk_ctx* ctx, const double* x, double alpha, const double* d, double* out, int64_t n) {
   if (!ctx_ok(ctx)) return -1;
-  const int vec = flat_vec(n);
+  const int vec = (al16(x) && al16(d) && al16(out)) ? flat_vec(n) : 1;
   const Geo geo{n, 0, 1};
   RowLaunch L = flat_rows(n, vec, 1 << 30);
   FLAT_DISPATCH(vec, k_axpy, L, x, alpha, d, out, geo, L.lr0, L.nlr);
@@ -4818,9 +4845,7 @@ int gnk_flat_axpy(gnk_ctx* ctx, const double* x, double alpha, const double* d, 
 int gnk_flat_cg_update_xr(gnk_ctx* ctx, double alpha, const double* p, const double* q, double* x, double* r,
                           const double* dinv, double* z, int64_t n, double* out) {
   if (!ctx_ok(ctx)) return -1;
-  // 16-B pairs only on 16-B aligned vectors (k_cg_xr's two-point path)
-  const auto al = [](const void* ptr) { return (reinterpret_cast<uintptr_t>(ptr) & 15) == 0; };
-  const int vec = (al(p) && al(q) && al(x) && al(r) && al(dinv) && al(z)) ? flat_vec(n) : 1;
+  const int vec = (al16(p) && al16(q) && al16(x) && al16(r) && al16(dinv) && al16(z)) ? flat_vec(n) : 1;
   const Geo geo{n, 0, 1};
   RowLaunch L = flat_rows(n, vec);
   FLAT_DISPATCH(vec, k_cg_xr, L, alpha, p, q, x, r, dinv, z, geo, L.lr0, L.nlr, ctx->scratch, nullptr);

@@ -67,6 +67,18 @@ def run(out, N, K):
     dinv = dev.vec(); dinv[sl.own] = 1.0 / (1.0 + u[sl.own] ** 2)
     be.cg_update_xr(0.45, v, q, x3, r3, dinv, z3, o3, pairs=True)
     keep("cg_xr_x", x3); keep("cg_xr_r", r3); keep("cg_xr_z", z3); keep("cg_xr_dots", o3)
+    # small streaming kernels (slab and flat forms)
+    st = be.zeros(8); be.vec_stats(r, st); keep("vec_stats", st)
+    o = dev.vec(); be.vec_div(r, 3.7, o, True); keep("vec_div", o)
+    o = dev.vec(); be.vec_axpy(w, 0.37, r, o, True); keep("vec_axpy", o)
+    o = dev.vec(); be.jdiag(u, o); keep("jdiag", o)
+    fl = r[sl.own].clone()
+    st = be.zeros(8); be.flat_stats(fl, st); keep("flat_stats", st)
+    o = torch.empty_like(fl); be.flat_div(fl, 3.7, o); keep("flat_div", o)
+    o = torch.empty_like(fl); be.flat_axpy(fl, 0.37, fl.flip(0).contiguous(), o); keep("flat_axpy", o)
+    fx, frr, fz, fo = fl.clone(), fl.flip(0).contiguous(), torch.empty_like(fl), be.zeros(8)
+    be.flat_cg_update_xr(0.45, fl, fl * 0.5, fx, frr, torch.ones_like(fl) * 0.9, fz, fo, pairs=True)
+    keep("flat_xr_x", fx); keep("flat_xr_r", frr); keep("flat_xr_z", fz); keep("flat_xr_dots", fo)
     o, jn = dev.vec(), be.zeros(64)
     be.normalize_jnorm(u, w, 3.0, o, jn); keep("normalize", o); keep("normalize_jn", jn)
     for k in range(1, K + 1):
