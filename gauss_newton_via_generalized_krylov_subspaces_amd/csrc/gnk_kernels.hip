@@ -4914,13 +4914,20 @@ int gnk_flat_gram(gnk_ctx* ctx, const double* W, int64_t ldw, int k, const doubl
   return check_launch(ctx, "flat_gram scatter");
 }
 
+// Row ranges of the row-marching normal matvec: one round of its resident workgroups (nbc strips of 4 waves
+// per range), not a fixed 8 per CU -- at 5 resident workgroups per CU a fixed 8 is 1.6 rounds.  The p.q partials
+// are compensated pairs (Dot2), so the sum's value does not follow the decomposition.
+int64_t cgm_ranges(gnk_ctx* ctx, const void* fn, int64_t nbc, int64_t nrows) {
+  return std::max<int64_t>(1, std::min<int64_t>(nrows, int64_t(resident_blocks(ctx, fn)) / nbc));
+}
+
 int gnk_cg_normal_matvec(gnk_ctx* ctx, const double* d, const double* p, double* q, double* pq_out) {
   if (!ready(ctx)) return -1;
   int nblk;
   if (ctx->geo.N % 2 == 0 && tuning(ctx, GNK_TUNE_CG_MATVEC) != 1) {
     const int64_t nbc = (ctx->geo.N + 4 * CGM_SW - 1) / (4 * CGM_SW);
     const int64_t nrows = ctx->geo.nrows;
-    int64_t nranges = std::max<int64_t>(1, std::min<int64_t>(nrows, int64_t(ctx->num_cus) * 8 / nbc));
+    int64_t nranges = cgm_ranges(ctx, (const void*)&k_cg_matvec_m<false>, nbc, nrows);
     const int64_t rpr = (nrows + nranges - 1) / nranges;
     nranges = (nrows + rpr - 1) / rpr;
     if (nbc * nranges > MAX_RED_BLOCKS) return fail(ctx, "cg_normal_matvec: grid too large");
@@ -4947,7 +4954,7 @@ static int cg_step_matvec(gnk_ctx* ctx, const double* d, const double* z, const 
   if (!d || !z || !p_in || !p_out || !q || p_in == p_out) return fail(ctx, "cg_step_matvec: bad buffers");
   const int64_t nbc = (ctx->geo.N + 4 * CGM_SW - 1) / (4 * CGM_SW);
   const int64_t nrows = ctx->geo.nrows;
-  int64_t nranges = std::max<int64_t>(1, std::min<int64_t>(nrows, int64_t(ctx->num_cus) * 8 / nbc));
+  int64_t nranges = cgm_ranges(ctx, (const void*)&k_cg_matvec_m<true>, nbc, nrows);
   const int64_t rpr = (nrows + nranges - 1) / nranges;
   nranges = (nrows + rpr - 1) / rpr;
   if (nbc * nranges > MAX_RED_BLOCKS) return fail(ctx, "cg_step_matvec: grid too large");
