@@ -1231,19 +1231,50 @@ __global__ __launch_bounds__(BLOCK) void k_cg_sr(double alpha, double beta, int 
   __shared__ double sh[(BLOCK / 64) * 2];
   double acc[2] = {0.0, 0.0};
   ROW_LOOP_BEGIN(VEC)
-  for (int qq = 0; qq < VEC && iy + qq < N; ++qq) {
-    const int64_t i = li + qq;
-    const double pi = first ? u[i] : u[i] + beta * p[i];
-    const double si = first ? w[i] : w[i] + beta * sv[i];
-    p[i] = pi;
-    sv[i] = si;
-    x[i] = x[i] + alpha * pi;
-    const double ri = r[i] - alpha * si;
-    r[i] = ri;
-    const double ui = dinv ? 0.0 + dinv[i] * ri : ri;
-    u[i] = ui;
-    acc[0] += ri * ui;
-    acc[1] += ri * ri;
+  if (VEC == 2 && iy + 1 < N) {
+    // 16-B pairs; the loop's arithmetic and accumulation order point by point
+    const d2 uv = *reinterpret_cast<const d2*>(u + li), wv = *reinterpret_cast<const d2*>(w + li);
+    d2 pv = uv, sv2 = wv;
+    if (!first) {
+      const d2 po = *reinterpret_cast<const d2*>(p + li), so = *reinterpret_cast<const d2*>(sv + li);
+      pv = d2{uv.x + beta * po.x, uv.y + beta * po.y};
+      sv2 = d2{wv.x + beta * so.x, wv.y + beta * so.y};
+    }
+    *reinterpret_cast<d2*>(p + li) = pv;
+    *reinterpret_cast<d2*>(sv + li) = sv2;
+    d2 xv = *reinterpret_cast<const d2*>(x + li);
+    xv.x = xv.x + alpha * pv.x;
+    xv.y = xv.y + alpha * pv.y;
+    *reinterpret_cast<d2*>(x + li) = xv;
+    d2 rv = *reinterpret_cast<const d2*>(r + li);
+    rv.x = rv.x - alpha * sv2.x;
+    rv.y = rv.y - alpha * sv2.y;
+    *reinterpret_cast<d2*>(r + li) = rv;
+    d2 un = rv;
+    if (dinv) {
+      const d2 dv = *reinterpret_cast<const d2*>(dinv + li);
+      un = d2{0.0 + dv.x * rv.x, 0.0 + dv.y * rv.y};
+    }
+    *reinterpret_cast<d2*>(u + li) = un;
+    acc[0] += rv.x * un.x;
+    acc[1] += rv.x * rv.x;
+    acc[0] += rv.y * un.y;
+    acc[1] += rv.y * rv.y;
+  } else {
+    for (int qq = 0; qq < VEC && iy + qq < N; ++qq) {
+      const int64_t i = li + qq;
+      const double pi = first ? u[i] : u[i] + beta * p[i];
+      const double si = first ? w[i] : w[i] + beta * sv[i];
+      p[i] = pi;
+      sv[i] = si;
+      x[i] = x[i] + alpha * pi;
+      const double ri = r[i] - alpha * si;
+      r[i] = ri;
+      const double ui = dinv ? 0.0 + dinv[i] * ri : ri;
+      u[i] = ui;
+      acc[0] += ri * ui;
+      acc[1] += ri * ri;
+    }
   }
   ROW_LOOP_END
   block_sum_store<2>(acc, 2, partial + 2 * (blockIdx.y * gridDim.x + blockIdx.x), sh);
@@ -1253,9 +1284,19 @@ template <int VEC>
 __global__ __launch_bounds__(BLOCK) void k_cg_p(double beta, int first, const double* __restrict__ z,
                                                 double* __restrict__ p, Geo geo, int64_t lr0, int64_t nlr) {
   ROW_LOOP_BEGIN(VEC)
-  for (int qq = 0; qq < VEC && iy + qq < N; ++qq) {
-    const int64_t i = li + qq;
-    p[i] = first ? z[i] : p[i] * beta + z[i];
+  if (VEC == 2 && iy + 1 < N) {
+    const d2 zv = *reinterpret_cast<const d2*>(z + li);
+    if (first) {
+      *reinterpret_cast<d2*>(p + li) = zv;
+    } else {
+      const d2 pv = *reinterpret_cast<const d2*>(p + li);
+      *reinterpret_cast<d2*>(p + li) = d2{pv.x * beta + zv.x, pv.y * beta + zv.y};
+    }
+  } else {
+    for (int qq = 0; qq < VEC && iy + qq < N; ++qq) {
+      const int64_t i = li + qq;
+      p[i] = first ? z[i] : p[i] * beta + z[i];
+    }
   }
   ROW_LOOP_END
 }
@@ -4856,7 +4897,7 @@ int gnk_flat_cg_update_xr(gnk_ctx* ctx, double alpha, const double* p, const dou
 
 int gnk_flat_cg_update_p(gnk_ctx* ctx, double beta, int first, const double* z, double* p, int64_t n) {
   if (!ctx_ok(ctx)) return -1;
-  const int vec = flat_vec(n);
+  const int vec = (al16(z) && al16(p)) ? flat_vec(n) : 1;
   const Geo geo{n, 0, 1};
   RowLaunch L = flat_rows(n, vec, 1 << 30);
   FLAT_DISPATCH(vec, k_cg_p, L, beta, first, z, p, geo, L.lr0, L.nlr);

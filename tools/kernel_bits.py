@@ -67,6 +67,12 @@ def run(out, N, K):
     dinv = dev.vec(); dinv[sl.own] = 1.0 / (1.0 + u[sl.own] ** 2)
     be.cg_update_xr(0.45, v, q, x3, r3, dinv, z3, o3, pairs=True)
     keep("cg_xr_x", x3); keep("cg_xr_r", r3); keep("cg_xr_z", z3); keep("cg_xr_dots", o3)
+    # single-reduction CG update and the plain direction update
+    sp, ss_, sx, sr, su, so = v.clone(), w.clone(), u.clone(), r.clone(), y.clone(), be.zeros(8)
+    be.cg_sr_update(0.3, 0.6, False, r, sp, ss_, sx, sr, dinv, su, so)
+    keep("cg_sr_p", sp); keep("cg_sr_s", ss_); keep("cg_sr_x", sx); keep("cg_sr_r", sr); keep("cg_sr_u", su)
+    keep("cg_sr_dots", so)
+    pp = v.clone(); be.cg_update_p(0.6, False, w, pp); keep("cg_p", pp)
     # small streaming kernels (slab and flat forms)
     st = be.zeros(8); be.vec_stats(r, st); keep("vec_stats", st)
     o = dev.vec(); be.vec_div(r, 3.7, o, True); keep("vec_div", o)
