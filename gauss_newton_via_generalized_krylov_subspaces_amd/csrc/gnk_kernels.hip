@@ -1784,16 +1784,22 @@ __device__ __forceinline__ double bld(__amdgpu_buffer_rsrc_t rs, unsigned off) {
   return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rs, off, 0, 0));
 }
 
+// Pair tile p of the upper triangle (row-major: (0,0), (0,1), ..., (0,nb-1), (1,1), ...) -> (a, b).
+// A fixed-trip-count sum of comparisons, not a data-dependent loop: inside the unrolled tile loops p is
+// a constant and the whole index folds away.  (A while loop here was left as a scalar loop in front of
+// every Gram MFMA for nb >= 3, serialising each tile's LDS reads behind it.)
+constexpr int pair_start(int a, int nb) { return a * nb - a * (a - 1) / 2; }
 constexpr int pair_a(int p, int nb) {
   int a = 0;
-  while (p >= nb - a) { p -= nb - a; ++a; }
+  for (int i = 1; i < 16; ++i) a += (i < nb && p >= pair_start(i, nb)) ? 1 : 0;
   return a;
 }
 constexpr int pair_b(int p, int nb) {
-  int a = 0;
-  while (p >= nb - a) { p -= nb - a; ++a; }
-  return a + p;
+  const int a = pair_a(p, nb);
+  return a + p - pair_start(a, nb);
 }
+static_assert(pair_a(0, 7) == 0 && pair_b(6, 7) == 6 && pair_a(7, 7) == 1 && pair_b(7, 7) == 1 &&
+              pair_a(27, 7) == 6 && pair_b(27, 7) == 6 && pair_a(12, 7) == 1 && pair_b(12, 7) == 6, "pair_a/b");
 
 __device__ __forceinline__ double dpp_row_shr1(double v) {     // lane l <- lane l-1 of its 16-lane row
   const u2v b = __builtin_bit_cast(u2v, v);
@@ -1895,6 +1901,7 @@ __device__ __forceinline__ void gram_x_wave(const double* __restrict__ u, const 
 
   const int pp = tid & (TT / 2 - 1), jh = tid >> 4;
   const bool ew = pp == 0, ee = pp == TT / 2 - 1;
+  const double up = -c.j_lin_up;
   const double* src = rinv ? Yt : Wt;       // what the Gram reads
   const bool rthr = r && (k % TPR) == jh;   // the threads that stage r (column k)
 
@@ -1904,6 +1911,7 @@ __device__ __forceinline__ void gram_x_wave(const double* __restrict__ u, const 
     const int64_t cs = (item % nstrips) * TT;
     const int64_t iy = cs + 2 * pp;
     const bool hw = iy > 0, he = iy + 2 < N;
+    const double cw = hw ? c.hm2 : 0.0, ce = he ? c.hm2 : 0.0;   // s + 0*v == s (v finite: in-grid values)
     if (x0 >= x1) continue;
     auto colp = [&](int m, int64_t xr) {
       return V + int64_t(min(jh + TPR * m, k - 1)) * ldv + (G + xr) * N + iy;
@@ -1929,14 +1937,24 @@ __device__ __forceinline__ void gram_x_wave(const double* __restrict__ u, const 
 
     for (int64_t x = x0; x < x1; ++x) {
       const int bsel = int((x - x0) & 1);
-      const double dd0 = ddb[bsel * TT + 2 * pp], dd1 = ddb[bsel * TT + 2 * pp + 1];
+      const double dn0 = -ddb[bsel * TT + 2 * pp], dn1 = -ddb[bsel * TT + 2 * pp + 1];
 #pragma unroll
       for (int m = 0; m < MJ; ++m) {
         const double wl = dpp_row_shr1(vc[m].y);   // lane pp-1's second point
         const double er = dpp_row_shl1(vc[m].x);   // lane pp+1's first point
         const double w = ew ? eo[m] : wl, e = ee ? eo[m] : er;
-        const double w0 = jvp_pt(c, dd0, vn[m].x, hw ? w : 0.0, hw, vc[m].x, vc[m].y, true, vs[m].x);
-        const double w1 = jvp_pt(c, dd1, vn[m].y, vc[m].x, true, vc[m].y, he ? e : 0.0, he, vs[m].y);
+        // J V with explicit FMAs in the CSR term order, as k_gram_w (the Gram's own summation order
+        // already differs from the reference's, so the per-element rounding is not observable)
+        double w0 = c.hm2 * vn[m].x;
+        w0 = fma(cw, w, w0);
+        w0 = fma(dn0, vc[m].x, w0);
+        w0 = fma(c.hm2, vc[m].y, w0);
+        w0 = fma(up, vs[m].x, w0);
+        double w1 = c.hm2 * vn[m].y;
+        w1 = fma(c.hm2, vc[m].x, w1);
+        w1 = fma(dn1, vc[m].y, w1);
+        w1 = fma(ce, e, w1);
+        w1 = fma(up, vs[m].y, w1);
         if (jh + TPR * m < k) {
           Wt[(2 * pp) * S + jh + TPR * m] = w0;
           Wt[(2 * pp + 1) * S + jh + TPR * m] = w1;
@@ -4570,18 +4588,23 @@ int gnk_gram(gnk_ctx* ctx, const double* u, const double* V, int64_t ldv, int k,
   }
   // the wide passes below reduce over their own slab decomposition (not segmented)
   if (seg_on(ctx)) ++ctx->seg_fallbacks;
-  // 5..7 column blocks on a grid of 32-point strips: k_gram_x (marching, RinvAug in VGPRs); tuning
-  // GNK_TUNE_GRAM_WIDE 3 keeps the pair-split k_gram below (tooling A/B).  At 2..4 blocks (k = 21..63)
-  // the barrier-free chunked / prefetching kernels stay 1.1-1.5x faster (profiles/round3/gram_wide_ab.jsonl)
-  if (nb >= 5 && nb <= 7 && ctx->geo.N % GX_T == 0 && ldv % 2 == 0 && tuning(ctx, GNK_TUNE_GRAM_WIDE) != 3) {
+  // 4..7 column blocks on a grid of 32-point strips: k_gram_x (marching, RinvAug in VGPRs); tuning
+  // GNK_TUNE_GRAM_WIDE 3 keeps the pair-split k_gram below for 5..7 blocks, 4 takes k_gram_x from 2 blocks,
+  // 5 from 5 blocks (tooling A/B).  At 2..3 blocks (k = 21..47) the barrier-free chunked kernel stays
+  // 1.4-2.5x faster (profiles/round5/gram_x_blocks_ab.jsonl); at 4 blocks k_gram_x matches the prefetching
+  // chunked kernel (k = 48..63: 22.6-23.1 vs 22.5-24.4 ms at 8192^2) and is flat in k.
+  const int wide_t = tuning(ctx, GNK_TUNE_GRAM_WIDE);
+  const int xmin = wide_t == 4 ? 2 : wide_t == 5 ? 5 : 4;
+  if (nb >= xmin && nb <= 7 && ctx->geo.N % GX_T == 0 && ldv % 2 == 0 && !(wide_t == 3 && nb >= 5)) {
     const size_t ldsx = size_t(2) * GX_T * (KP + 1) * 8 + size_t(2) * GX_T * 8;    // W, Y tiles + jdiag rows
     if (size_t(4 * ((P + 3) / 4)) * 256 * 8 > ldsx) return fail(ctx, "gram: reduction staging does not fit (x)");
     const int64_t nstrips = ctx->geo.N / GX_T;
     const int64_t nrows = ctx->geo.nrows;
     // a persistent grid of the resident workgroups over (row range, strip) items; items = lcm(strips,
     // workgroups) when the rows allow, so every workgroup gets the same number
-    const void* fnx = nb == 5 ? (const void*)&k_gram_x<5> : nb == 6 ? (const void*)&k_gram_x<6>
-                                : (const void*)&k_gram_x<7>;
+    const void* fnx = nb == 2 ? (const void*)&k_gram_x<2> : nb == 3 ? (const void*)&k_gram_x<3>
+                    : nb == 4 ? (const void*)&k_gram_x<4> : nb == 5 ? (const void*)&k_gram_x<5>
+                    : nb == 6 ? (const void*)&k_gram_x<6> : (const void*)&k_gram_x<7>;
     // resident 8-wave workgroups: one per CU (marching rows, B fragments, pair tiles: ~2 waves per SIMD)
     const int64_t nwg = resident_blocks(ctx, fnx, 64 * GX_NW, ldsx);
     int64_t gcd = nstrips, bb = nwg;
@@ -4597,7 +4620,8 @@ int gnk_gram(gnk_ctx* ctx, const double* u, const double* V, int64_t ldv, int k,
 #define GRAMX(NBV)                                                                                                \
   hipLaunchKernelGGL(k_gram_x<NBV>, dim3(unsigned(nwg)), dim3(64 * GX_NW), ldsx, ctx->stream, u, V, ldv, k, rinv, r, \
                      ctx->geo, ctx->coef, rpr, nitems, ctx->scratch)
-    if (nb == 5) GRAMX(5); else if (nb == 6) GRAMX(6); else GRAMX(7);
+    if (nb == 2) GRAMX(2); else if (nb == 3) GRAMX(3); else if (nb == 4) GRAMX(4);
+    else if (nb == 5) GRAMX(5); else if (nb == 6) GRAMX(6); else GRAMX(7);
 #undef GRAMX
     tlx.done();
     int rcx = check_launch(ctx, "gram_x");

@@ -1,7 +1,7 @@
 """Dump the Gram of [J V P^-1 | r] (gnk_gram, kbench's gram2 inputs) for several basis sizes k, and time it:
 A/B of two builds of libgnk.so for bit-identity and speed (load the other with GNK_LIB=...).
 
-  python tools/gram_dump.py OUTDIR TAG k1,k2,... [--grid N] [--reps R]
+  python tools/gram_dump.py OUTDIR TAG k1,k2,... [--grid N] [--reps R] [--tune key=value,...]
 writes OUTDIR/G_TAG_k.npy and prints one JSON line per k (median ms).  Compare two tags with
   python tools/gram_dump.py --compare OUTDIR TAG_A TAG_B
 """
@@ -25,6 +25,9 @@ def dump(a):
     n = N * N
     dev = BratuDevice(BratuPdeProblem(N + 1, 5, 10), Comm(single=True))
     be, sl = dev.backend, dev.slab
+    for kv in filter(None, a.tune.split(",")):
+        key, val = kv.split("=")
+        be.set_tuning(key, int(val))
     ks = [int(k) for k in a.ks.split(",")]
     kmax = max(ks)
     g = torch.Generator(device=be.device).manual_seed(0)
@@ -74,4 +77,5 @@ if __name__ == "__main__":
         ap.add_argument("ks")
         ap.add_argument("--grid", type=int, default=8192)
         ap.add_argument("--reps", type=int, default=5)
+        ap.add_argument("--tune", default="", help="gnk_set_tuning overrides, e.g. gram_wide=4")
         dump(ap.parse_args())
