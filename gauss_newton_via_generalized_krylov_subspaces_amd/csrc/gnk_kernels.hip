@@ -624,7 +624,10 @@ __global__ __launch_bounds__(BLOCK) void k_gemv_p(const double* __restrict__ V, 
 // g = -(J^T r) on owned rows (chunk 0 stores it), h[j0 + j] partial = V_j . g.
 // KCT columns per chunk (compile time): every V load is unconditional (clamped column),
 // surplus accumulators are discarded by the block reduction (no loads under a branch).
-template <int VEC, int KCT>
+// GREAD: g is read back (stored by an earlier launch of the same row decomposition) instead of
+// recomputed from u and r -- the wide-basis split of gnk_vjp_gemv_t; the same products in the same
+// order, so the same partials.
+template <int VEC, int KCT, bool GREAD = false>
 __global__ __launch_bounds__(BLOCK) void k_vjp_gemv_t(const double* __restrict__ u, const double* __restrict__ r,
                                                       const double* __restrict__ V, int64_t ldv, int k,
                                                       double* __restrict__ g, Geo geo, Coef c, int64_t lr0,
@@ -640,18 +643,25 @@ __global__ __launch_bounds__(BLOCK) void k_vjp_gemv_t(const double* __restrict__
   for (int j = 0; j < KCT; ++j) acc[j] = 0.0;
   ROW_LOOP_BEGIN(VEC)
   if (VEC == 2 && iy + 1 < N) {
-    const d2 uc = *reinterpret_cast<const d2*>(u + li);
-    const d2 rc = *reinterpret_cast<const d2*>(r + li);
-    const d2 rn = *reinterpret_cast<const d2*>(r + li - N);
-    const d2 rs = *reinterpret_cast<const d2*>(r + li + N);
-    const bool hw = iy > 0, he = iy + 2 < N;
-    double rw = __shfl_up(rc.y, 1);
-    double re = __shfl_down(rc.x, 1);
-    if (lane == 0) rw = hw ? r[li - 1] : 0.0;
-    if (lane == 63 || iy + 2 >= N) re = he ? r[li + 2] : 0.0;
-    const double g0 = -vjp_pt(c, jdiag(c, uc.x), rn.x, rw, hw, rc.x, rc.y, true, rs.x);
-    const double g1 = -vjp_pt(c, jdiag(c, uc.y), rn.y, rc.x, true, rc.y, re, he, rs.y);
-    if (zc == 0) st_nt(g + li, d2{g0, g1});
+    double g0, g1;
+    if constexpr (GREAD) {
+      const d2 gg = *reinterpret_cast<const d2*>(g + li);
+      g0 = gg.x;
+      g1 = gg.y;
+    } else {
+      const d2 uc = *reinterpret_cast<const d2*>(u + li);
+      const d2 rc = *reinterpret_cast<const d2*>(r + li);
+      const d2 rn = *reinterpret_cast<const d2*>(r + li - N);
+      const d2 rs = *reinterpret_cast<const d2*>(r + li + N);
+      const bool hw = iy > 0, he = iy + 2 < N;
+      double rw = __shfl_up(rc.y, 1);
+      double re = __shfl_down(rc.x, 1);
+      if (lane == 0) rw = hw ? r[li - 1] : 0.0;
+      if (lane == 63 || iy + 2 >= N) re = he ? r[li + 2] : 0.0;
+      g0 = -vjp_pt(c, jdiag(c, uc.x), rn.x, rw, hw, rc.x, rc.y, true, rs.x);
+      g1 = -vjp_pt(c, jdiag(c, uc.y), rn.y, rc.x, true, rc.y, re, he, rs.y);
+      if (zc == 0) st_nt(g + li, d2{g0, g1});
+    }
     if (k > 0) {
 #pragma unroll
       for (int j = 0; j < KCT; ++j) {
@@ -665,11 +675,16 @@ __global__ __launch_bounds__(BLOCK) void k_vjp_gemv_t(const double* __restrict__
       const int64_t i = li + q;
       const int64_t yy = iy + q;
       if (yy >= N) break;
-      const bool hw = yy > 0, he = yy < N - 1;
-      const double d = jdiag(c, u[i]);
-      const double rw = hw ? r[i - 1] : 0.0, re = he ? r[i + 1] : 0.0;
-      const double gi = -vjp_pt(c, d, r[i - N], rw, hw, r[i], re, he, r[i + N]);
-      if (zc == 0) g[i] = gi;
+      double gi;
+      if constexpr (GREAD) {
+        gi = g[i];
+      } else {
+        const bool hw = yy > 0, he = yy < N - 1;
+        const double d = jdiag(c, u[i]);
+        const double rw = hw ? r[i - 1] : 0.0, re = he ? r[i + 1] : 0.0;
+        gi = -vjp_pt(c, d, r[i - N], rw, hw, r[i], re, he, r[i + N]);
+        if (zc == 0) g[i] = gi;
+      }
       if (k > 0) {
 #pragma unroll
         for (int j = 0; j < KCT; ++j) acc[j] = acc[j] + V[min(j0 + j, jmax) * ldv + i] * gi;
@@ -4224,6 +4239,40 @@ int gnk_vjp_gemv_t(gnk_ctx* ctx, const double* u, const double* r, const double*
   const int zt = tuning(ctx, GNK_TUNE_VJPG_ZMAX);
   const int zmax = int(std::min<size_t>(std::min<size_t>(size_t(nchunk), room / (size_t(nblk) * kct)),
                                         zt > 0 ? size_t(zt) : size_t(nchunk)));
+  // several 16-column chunks: chunk 0 computes and stores g, the rest read it back in 32-column chunks
+  // (each chunk recomputing g from u and r re-read 4 grid vectors: 28 of 128 at k = 100), on the same
+  // row decomposition -- every column's partials, and so h, bit for bit those of the one-launch form
+  if (nchunk > 1 && zt == 0 && g && vec_of(ctx) == 2 && size_t(nblk) * 32 <= room) {
+    L.grid.z = 1;
+    hipLaunchKernelGGL((k_vjp_gemv_t<2, 16>), L.grid, dim3(BLOCK), 0, ctx->stream, u, r, V, ldv, std::min(k, 16), g,
+                       ctx->geo, ctx->coef, L.lr0, L.nlr, ctx->scratch, 0);
+    int rc = check_launch(ctx, "vjp_gemv_t (chunk 0)");
+    if (rc) return rc;
+    if (h_out) {
+      rc = seg_on(ctx) ? sreduce(ctx, ctx->scratch, int(ctx->seg * L.grid.x), 16, 16, 16, int64_t(nblk) * 16, nullptr,
+                                 h_out)
+                       : wreduce(ctx, ctx->scratch, nblk, 16, 16, 16, int64_t(nblk) * 16, nullptr, h_out);
+      if (rc) return rc;
+    }
+    const int kr = k - 16, nc32 = (kr + 31) / 32;
+    const int zm = int(std::min<size_t>(size_t(nc32), room / (size_t(nblk) * 32)));
+    for (int z0 = 0; z0 < nc32; z0 += zm) {
+      const int nz = std::min(zm, nc32 - z0);
+      L.grid.z = unsigned(nz);
+      hipLaunchKernelGGL((k_vjp_gemv_t<2, 32, true>), L.grid, dim3(BLOCK), 0, ctx->stream, u, r, V + 16 * ldv, ldv, kr,
+                         g, ctx->geo, ctx->coef, L.lr0, L.nlr, ctx->scratch, z0);
+      rc = check_launch(ctx, "vjp_gemv_t (read g)");
+      if (rc) return rc;
+      if (!h_out) continue;
+      const int len = std::min(kr - z0 * 32, nz * 32);
+      double* ho = h_out + 16 + int64_t(z0) * 32;
+      rc = seg_on(ctx) ? sreduce(ctx, ctx->scratch, int(ctx->seg * L.grid.x), len, 32, 32, int64_t(nblk) * 32, nullptr,
+                                 ho)
+                       : wreduce(ctx, ctx->scratch, nblk, len, 32, 32, int64_t(nblk) * 32, nullptr, ho);
+      if (rc) return rc;
+    }
+    return 0;
+  }
   for (int z0 = 0; z0 < nchunk; z0 += zmax) {
     const int nz = std::min(zmax, nchunk - z0);
     L.grid.z = unsigned(nz);

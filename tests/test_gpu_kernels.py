@@ -81,7 +81,7 @@ def test_jvp_bitwise_vs_oracle_small(N):
     close(own(dev, out), ref.pde_operator(x), rtol=1e-14)
 
 
-@pytest.mark.parametrize("N,k", [(24, 1), (24, 7), (100, 33), (1024, 20), (25, 5)])
+@pytest.mark.parametrize("N,k", [(24, 1), (24, 7), (100, 33), (1024, 20), (25, 5), (128, 70), (96, 41)])
 def test_basis_kernels(N, k):
     prob, dev, ref = make(N)
     be = dev.backend

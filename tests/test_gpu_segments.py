@@ -147,14 +147,17 @@ def test_segment_reductions_rank_count_invariant(N):
     np.testing.assert_allclose(one["trial_h"], hn, rtol=1e-10, atol=1e-12 * np.max(np.abs(hn)))
 
 
-def test_vjp_gemv_t_chunk_launches_bit_identical():
-    """Wide bases with segments: gnk_vjp_gemv_t gives every owned row its own block row, so at C5's k (up to 200)
-    on a large slab its partials would overflow the workspace; it then splits the column chunks over launches.
-    One chunk per launch (GNK_TUNE_VJPG_ZMAX 1) must give the one-launch g = -J^T r and h = V^T g bit for bit
-    (ref:krylow.py:62-64)."""
-    N, k = 512, 40                                    # three 16-column chunks
+@pytest.mark.parametrize("segments,N,k", [(True, 512, 40), (False, 512, 40), (True, 256, 100), (False, 1024, 100),
+                                          (False, 384, 25), (False, 255, 57)])
+def test_vjp_gemv_t_chunk_launches_bit_identical(segments, N, k):
+    """Wide bases: gnk_vjp_gemv_t (k > 24) computes and stores g = -J^T r with the first 16 columns' h = V^T g,
+    then reads g back for the other columns in 32-column chunks, on one row decomposition; with segments it
+    gives every owned row its own block row, so at C5's k (up to 200) on a large slab the partials may not fit
+    the workspace and the chunks go over several launches.  Both must give the one-chunk-per-launch form
+    (GNK_TUNE_VJPG_ZMAX 1: every 16-column chunk recomputing g) bit for bit (ref:krylow.py:62-64).  N = 255:
+    odd rows, the one-point path."""
     prob = gnk.BratuPdeProblem(N + 1, 5, 10)
-    dev = BratuDevice(prob, Comm(single=True, segments=True))
+    dev = BratuDevice(prob, Comm(single=True, segments=segments))
     be = dev.backend
     rng = np.random.default_rng(7)
     u, r = dev.load(0.3 * rng.standard_normal(N * N)), dev.load(rng.standard_normal(N * N))

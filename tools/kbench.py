@@ -35,7 +35,8 @@ def main():
         be.set_tuning(key, int(val))
     g = torch.Generator(device=be.device).manual_seed(0)
     V = be.zeros(k + 1, sl.length)
-    V[:, sl.own] = torch.randn(k + 1, n, generator=g, device=be.device, dtype=torch.float64) / np.sqrt(n)
+    for j in range(k + 1):                   # a column at a time: no (k + 1) x n temporary at 16384^2
+        V[j, sl.own] = torch.randn(n, generator=g, device=be.device, dtype=torch.float64) / np.sqrt(n)
     u, r, x, y, t1 = (dev.vec() for _ in range(5))
     u[sl.own] = 0.1 * torch.randn(n, generator=g, device=be.device, dtype=torch.float64)
     r[sl.own] = torch.randn(n, generator=g, device=be.device, dtype=torch.float64)

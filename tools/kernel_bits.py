@@ -50,6 +50,12 @@ def run(out, N, K):
         gg, h, x, st = dev.vec(), be.zeros(256), dev.vec(), be.zeros(64)
         be.gemv_vjp_gemv_t_pending(Vp, k, c, hh, r, x, gg, h, st)
         keep(f"trialp{k}_x", x); keep(f"trialp{k}_g", gg); keep(f"trialp{k}_h", h); keep(f"trialp{k}_w", Vp[k])
+    Vw = be.zeros(101, sl.length)                     # wide bases: the split gnk_vjp_gemv_t (k > 24)
+    Vw[:, sl.own] = torch.randn(101, n, generator=g, device=be.device, dtype=torch.float64) / np.sqrt(n)
+    for k in (25, 40, 57, 100):
+        gg, h = dev.vec(), be.zeros(128)
+        be.vjp_gemv_t(u, r, Vw, k, gg, h); keep(f"vjp_gemv_t{k}_g", gg); keep(f"vjp_gemv_t{k}_h", h)
+    del Vw
     for k in (1, 5, 12, 20):
         c = be.to_device(np.linspace(0.5, 1.5, 64))
         hh = be.to_device(np.linspace(-0.1, 0.1, 64))
