@@ -4227,8 +4227,10 @@ int gnk_vjp_gemv_t(gnk_ctx* ctx, const double* u, const double* r, const double*
   const int kct = k <= 24 ? std::max(4, (k + 3) / 4 * 4) : 16;
   const int nchunk = std::max(1, (k + kct - 1) / kct);
   const int cap = tuning(ctx, GNK_TUNE_VJPG_BLOCKS);
+  // blocks per chunk: ~2048 in all, at least 512 per chunk (the first chunk, which computes g, runs alone in
+  // the wide split below: at 2048 / 7 = 292 it kept ~1 workgroup per CU)
   RowLaunch L = rows(ctx, G, ctx->geo.nrows, vec_of(ctx),
-                     seg_on(ctx) ? (1 << 30) : (cap > 0 ? cap : std::max(64, 2048 / nchunk)));
+                     seg_on(ctx) ? (1 << 30) : (cap > 0 ? cap : std::max(512, 2048 / nchunk)));
   const int nblk = L.grid.x * L.grid.y;
   // column chunks per launch: with segments every owned row has its own block row (nblk = grid.x * rows), and
   // a wide basis (C5: k up to 200) on a large slab would overflow the partials' workspace -- then the chunks
