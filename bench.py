@@ -553,18 +553,18 @@ def main():
     gram_share = sum(g_ms) * 1e-3 / elapsed_all if g_ms else float("nan")
     # per basis size: columns = bytes / (8 n_rank) - 2 (V, u, r); kernel as gnk_gram dispatches a pass
     # with P^-1 and r: VALU k <= 9 (one point per lane from 8), staged k <= 20 (N % 128 == 0), chunked
-    # k_gram_w up to 47 columns (+ r), the marching k_gram_x for 4..7 column blocks (N % 32 == 0; else the
-    # prefetching k_gram_wp at 4 blocks), the pair-split k_gram beyond
+    # k_gram_w up to 31 columns (+ r), the marching k_gram_x for 3..7 column blocks (N % 32 == 0; else the
+    # chunked k_gram_w at 3 blocks and the prefetching k_gram_wp at 4), the pair-split k_gram beyond
     def gram_kernel(kk):
         if kk <= 9:
             return "k_gram_v" if kk <= 7 else "k_gram_v1"
         if kk <= 20 and N % 128 == 0:
             return "k_gram_s"
-        if kk + 1 <= 48:
+        if kk + 1 <= 32:
             return "k_gram_w"
         if (kk + 16) // 16 <= 7 and N % 32 == 0:
             return "k_gram_x"
-        return "k_gram_wp" if kk + 1 <= 64 else "k_gram"
+        return "k_gram_w" if kk + 1 <= 48 else "k_gram_wp" if kk + 1 <= 64 else "k_gram"
 
     n_rank = solver.dev.slab.nrows * N
     by_k = {}

@@ -2054,8 +2054,12 @@ __device__ __forceinline__ void gram_x_wave(const double* __restrict__ u, const 
   }
 }
 
+// At 2..4 column blocks two workgroups per CU (4 waves per SIMD, <= 128 VGPRs: NB = 3 / 4 spill 80 / 176 B per
+// lane and still run 1.55 / 1.1-1.15x faster than at one workgroup, profiles/round5/gram_x_occupancy_ab.jsonl);
+// at 5..7 the spills would cost more than the occupancy gives (k = 64: 27.6 -> 40.5 ms).
 template <int NB>
-__global__ __launch_bounds__(64 * GX_NW) void k_gram_x(const double* __restrict__ u, const double* __restrict__ V,
+__global__ __launch_bounds__(64 * GX_NW) __attribute__((amdgpu_waves_per_eu(NB <= 4 ? 4 : 1)))
+void k_gram_x(const double* __restrict__ u, const double* __restrict__ V,
                                                        int64_t ldv, int k, const double* __restrict__ rinv,
                                                        const double* __restrict__ r, Geo geo, Coef c, int64_t rpr,
                                                        int64_t nitems, double* __restrict__ partial) {
@@ -4639,13 +4643,13 @@ int gnk_gram(gnk_ctx* ctx, const double* u, const double* V, int64_t ldv, int k,
   }
   // the wide passes below reduce over their own slab decomposition (not segmented)
   if (seg_on(ctx)) ++ctx->seg_fallbacks;
-  // 4..7 column blocks on a grid of 32-point strips: k_gram_x (marching, RinvAug in VGPRs); tuning
+  // 3..7 column blocks on a grid of 32-point strips: k_gram_x (marching, RinvAug in VGPRs); tuning
   // GNK_TUNE_GRAM_WIDE 3 keeps the pair-split k_gram below for 5..7 blocks, 4 takes k_gram_x from 2 blocks,
-  // 5 from 5 blocks (tooling A/B).  At 2..3 blocks (k = 21..47) the barrier-free chunked kernel stays
-  // 1.4-2.5x faster (profiles/round5/gram_x_blocks_ab.jsonl); at 4 blocks k_gram_x matches the prefetching
-  // chunked kernel (k = 48..63: 22.6-23.1 vs 22.5-24.4 ms at 8192^2) and is flat in k.
+  // 5 from 5 blocks (tooling A/B).  At 2 blocks (k = 21..31) the barrier-free chunked kernel stays 1.4x faster
+  // (profiles/round5/gram_x_blocks_ab.jsonl); at 3 / 4 blocks k_gram_x at two workgroups per CU beats the
+  // chunked / prefetching kernels (8192^2, k = 47 / 63: 12.2 / 20.3 vs 13.5 / 24.4 ms) and is flat in k.
   const int wide_t = tuning(ctx, GNK_TUNE_GRAM_WIDE);
-  const int xmin = wide_t == 4 ? 2 : wide_t == 5 ? 5 : 4;
+  const int xmin = wide_t == 4 ? 2 : wide_t == 5 ? 5 : 3;
   if (nb >= xmin && nb <= 7 && ctx->geo.N % GX_T == 0 && ldv % 2 == 0 && !(wide_t == 3 && nb >= 5)) {
     const size_t ldsx = size_t(2) * GX_T * (KP + 1) * 8 + size_t(2) * GX_T * 8;    // W, Y tiles + jdiag rows
     if (size_t(4 * ((P + 3) / 4)) * 256 * 8 > ldsx) return fail(ctx, "gram: reduction staging does not fit (x)");
@@ -4656,7 +4660,8 @@ int gnk_gram(gnk_ctx* ctx, const double* u, const double* V, int64_t ldv, int k,
     const void* fnx = nb == 2 ? (const void*)&k_gram_x<2> : nb == 3 ? (const void*)&k_gram_x<3>
                     : nb == 4 ? (const void*)&k_gram_x<4> : nb == 5 ? (const void*)&k_gram_x<5>
                     : nb == 6 ? (const void*)&k_gram_x<6> : (const void*)&k_gram_x<7>;
-    // resident 8-wave workgroups: one per CU (marching rows, B fragments, pair tiles: ~2 waves per SIMD)
+    // resident 8-wave workgroups: one per CU at 5..7 blocks (marching rows, B fragments, pair tiles: ~2 waves
+    // per SIMD), two at 2..4
     const int64_t nwg = resident_blocks(ctx, fnx, 64 * GX_NW, ldsx);
     int64_t gcd = nstrips, bb = nwg;
     while (bb) { const int64_t t2 = gcd % bb; gcd = bb; bb = t2; }

@@ -77,8 +77,8 @@ int64_t gnk_segment_fallbacks(const gnk_ctx* ctx);
  *   GNK_TUNE_VJPG_BLOCKS cap on the blocks of gnk_vjp_gemv_t
  *   GNK_TUNE_GRAM_WIDE   1 = never the prefetching wide Gram kernel, 2 = also for 2..3 column blocks,
  *                        3 = the pair-split kernel instead of the VGPR-RinvAug one for 5..7 blocks,
- *                        4 = the VGPR-RinvAug (marching) kernel from 2 column blocks, 5 = from 5 blocks
- *                        (4 blocks on the prefetching kernel, the round-4 choice)
+ *                        4 = the VGPR-RinvAug (marching) kernel from 2 column blocks (default: from 3),
+ *                        5 = from 5 blocks (3 / 4 blocks on the chunked / prefetching kernels, the round-4 choice)
  *   GNK_TUNE_GRAM_RPR    > 0: grid rows per row range of the staged / VALU Gram kernels (a finer,
  *                        fixed decomposition; A/B of what rank-count-independent partials cost)
  *   GNK_TUNE_LLS         1 = the device least-squares solve on one wave, a column per lane (k_lls), instead of
