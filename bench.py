@@ -56,6 +56,8 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=20.0, help="CPU oracle sample budget (0 = skip)")
     ap.add_argument("--jvp-reps", type=int, default=20)
     ap.add_argument("--cg-iters", type=int, default=200, help="CGLS iterations of the C3 line (0 = skip)")
+    ap.add_argument("--c5-steps", type=int, default=99,
+                    help="capped-C5 line (16384^2, restart 100) outer iterations at N = 1 (0 = skip)")
     ap.add_argument("--no-trial-timer", action="store_true",
                     help="time only the Gram launches in the timed regions (A/B of the trial timer's event cost)")
     ap.add_argument("--segments", choices=("auto", "on", "off"), default="auto",
@@ -165,7 +167,8 @@ def cpu_baseline(N, seconds, version, restart, c2_steps=20, grid_c2=1024):
 
 
 CG_BYTES_PER_ITER = 112     # SURVEY §8d model, bytes per unknown: p update 24, J^T J p 24, x/r/z update 64
-                            # (the fused iteration moves 96: step matvec 56 + r/z update 40)
+CG_BYTES_MOVED = 96         # what the fused iteration moves: step matvec 56 (d, z, p, x in; p', q, x out)
+                            # + r / z update 40 (q, r, dinv in; r, z out)
 
 
 def gn_cg_line(args, prob, u0, y, comm, device, world, backend):
@@ -213,6 +216,34 @@ def gn_cg_line(args, prob, u0, y, comm, device, world, backend):
         t = torch.tensor([el_sr], dtype=torch.float64, device=device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el_sr = t.item()
+    # the iteration's split: every CG kernel class timed per launch (event pairs around each), in a solve of
+    # its own so the timed solve above keeps one event pair per iteration
+    cap6 = 6 * (args.cg_iters + 8)
+    be.timer_start(_native.TIMER_CG_MATVEC, cap6)
+    be.timer_add(_native.TIMER_CG_XR)
+    be.timer_add(_native.TIMER_CG_AUX)
+    torch.cuda.synchronize()
+    t2 = time.perf_counter()
+    _, iters_split = cg.solve(u, r0, cg_rtol=1e-8, preconditioner=True, maxiter=args.cg_iters)
+    torch.cuda.synchronize()
+    el_split = time.perf_counter() - t2
+    sl_ = be.timer_collect_ids(cap6)
+    split = {}
+    for name, tid in (("matvec", _native.TIMER_CG_MATVEC), ("xr", _native.TIMER_CG_XR), ("aux", _native.TIMER_CG_AUX)):
+        got = [(m, b) for i, m, b in sl_ if i == tid]
+        tot = sum(m for m, _ in got)
+        split[name] = {"launches": len(got), "ms_per_iter": tot / max(iters_split, 1),
+                       "avg_launch_ms": tot / max(len(got), 1)}
+        if name != "aux" and got:
+            by = float(np.mean([b for _, b in got]))
+            split[name]["algorithmic_bytes_per_launch"] = by
+            split[name]["GBs"] = by / (split[name]["avg_launch_ms"] * 1e-3) / 1e9
+    busy = sum(v["ms_per_iter"] for v in split.values())
+    split["wall_ms_per_iter"] = 1e3 * el_split / max(iters_split, 1)
+    split["gaps_ms_per_iter"] = split["wall_ms_per_iter"] - busy
+    split["note"] = ("every CG launch bracketed by HIP events (a separate solve): matvec = k_cg_matvec_m, xr = k_cg_xr, "
+                     "aux = the partial-sum reductions and k_cg_scalars; gaps = wall - kernels (launch gaps, the "
+                     "lagged host read)")
     m_ms = float(np.mean([m for m, _ in ml])) if ml else float("nan")
     m_by = float(np.mean([b for _, b in ml])) if ml else float("nan")
     m_gbs = m_by / (m_ms * 1e-3) / 1e9 if ml else float("nan")
@@ -220,6 +251,9 @@ def gn_cg_line(args, prob, u0, y, comm, device, world, backend):
             "value": iters / elapsed, "unit": "cg_iters/s", "ms_per_iter": 1e3 * elapsed / max(iters, 1),
             "algorithmic_GBs": CG_BYTES_PER_ITER * n * iters / elapsed / 1e9,
             "bytes_per_iter": CG_BYTES_PER_ITER * n,
+            "bytes_per_iter_moved": CG_BYTES_MOVED * n,
+            "moved_GBs": CG_BYTES_MOVED * n * iters / elapsed / 1e9,
+            "split": split,
             "single_reduction": {"cg_iters": iters_sr, "value": iters_sr / el_sr, "unit": "cg_iters/s",
                                  "ms_per_iter": 1e3 * el_sr / max(iters_sr, 1),
                                  "note": "cg_variant='single_reduction' (Chronopoulos-Gear, non-parity option): "
@@ -230,6 +264,74 @@ def gn_cg_line(args, prob, u0, y, comm, device, world, backend):
                                  "row marching)", "avg_launch_ms": m_ms,
                        "GBs": m_gbs, "frac_of_peak": m_gbs / HBM_PEAK_GBS,
                        "algorithmic_bytes_per_launch": m_by}}
+
+
+FP64_MFMA_PEAK_TFS = 78.6   # MI355X fp64 matrix peak (the MFMA probe measures 72 TF/s)
+
+
+def gram_useful_flops(n, k):
+    """Useful fp64 flops of one Gram pass over [J V T | r] (k basis columns, n points): the triangular
+    transform W = (J V) T (k (k + 1) per point) and the symmetric Gram of the k + 1 columns
+    ((k + 1) (k + 2) per point, one triangle)."""
+    return float(n) * (k * (k + 1) + (k + 1) * (k + 2))
+
+
+def c5_capped_line(args, comm, device, grid=16384, restart=100):
+    """SURVEY §8d C5 with k capped (16384^2, Krylov dim 100; k = 200 needs 429 GB, more than one GPU holds):
+    one whole restart cycle after one warm-up step -- basis sizes k = 2..100 -- timed as one region, with every
+    Gram pass timed per launch (HIP events): outer it/s, the Gram pass by k, and its fp64-MFMA fraction
+    (useful flops / time / peak) -- the wide-basis MFMA path of ref:krylow.py:72-73 / gauss_newton_krylow.py:81-82."""
+    import gauss_newton_via_generalized_krylov_subspaces_amd as gnk
+    from gauss_newton_via_generalized_krylov_subspaces_amd import _native
+    from gauss_newton_via_generalized_krylov_subspaces_amd._device import BratuDevice
+    from gauss_newton_via_generalized_krylov_subspaces_amd.inputs import slab_inputs
+    prob = gnk.BratuPdeProblem(grid + 1, 5, 10)
+    stage = BratuDevice(prob, comm, device)
+    u0, y, _ = slab_inputs(stage)
+    s = gnk.GNKSolver(prob, y, krylow_restart=restart, tol=1e-8, max_iter=10 ** 9, version=args.version,
+                      comm=comm, device=device, backend=stage.backend)
+    s.setup(u0)
+    be = s.be
+    steps = min(args.c5_steps, restart - 1)
+    with contextlib.redirect_stdout(io.StringIO()):
+        s.step()                                                   # warm-up: k = 1
+        cap = 4 * (steps + 2)
+        be.timer_start(_native.TIMER_GRAM, cap)
+        tr0 = len(s.trace)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            if s.step():
+                break
+        torch.cuda.synchronize()
+        el = time.perf_counter() - t0
+    got = be.timer_collect_ids(cap)
+    done = len(s.trace) - tr0
+    n = s.dev.slab.nrows * grid
+    by_k, flops, gms = {}, 0.0, 0.0
+    for _, m, b in got:
+        kk = int(round(b / (8.0 * n))) - 2
+        by_k.setdefault(kk, []).append(m)
+        flops += gram_useful_flops(n, kk)
+        gms += m
+    tr = s.trace[tr0:]
+    del s, stage, u0, y
+    torch.cuda.empty_cache()
+    tfs = flops / (gms * 1e-3) / 1e12 if gms else float("nan")
+    return {"workload": f"bratu_{grid}x{grid}_gnk_krylov_dim{restart}_capped", "value": done / el,
+            "unit": "outer_iters/s", "steps": done, "ms_per_step": 1e3 * el / max(done, 1),
+            "basis_k_range": [min(t["k"] for t in tr), max(t["k"] for t in tr)] if tr else None,
+            "armijo_trials": int(sum(t["trials"] for t in tr)),
+            "gram": {"share_of_step_time": gms * 1e-3 / el, "launches": len(got), "useful_TFLOPs": tfs,
+                     "fp64_mfma_frac": tfs / FP64_MFMA_PEAK_TFS, "peak_TFLOPs": FP64_MFMA_PEAK_TFS,
+                     "flops_model": "n [k (k + 1) + (k + 1) (k + 2)] per pass (triangular transform + one Gram "
+                                    "triangle of k + 1 columns)",
+                     "by_k": {str(kk): {"ms": float(np.mean(v)),
+                                        "GBs": 8.0 * n * (kk + 2) / (np.mean(v) * 1e-3) / 1e9,
+                                        "TFLOPs": gram_useful_flops(n, kk) / (np.mean(v) * 1e-3) / 1e12}
+                              for kk, v in sorted(by_k.items())}},
+            "note": "C5 at 16384^2 with the basis capped at 100 columns (restart 100): V = 101 x 2.15 GB; the literal "
+                    "k = 200 (429 GB) does not fit one GPU. One warm-up step (k = 1), then the cycle's steps timed."}
 
 
 def prewarm(args, comm, device):
@@ -599,6 +701,10 @@ def main():
     torch.cuda.empty_cache()
     cg_line = gn_cg_line(args, prob, u0, y, comm, device, world, stage.backend) if args.cg_iters > 0 else None
 
+    c5_line = None
+    if world == 1 and args.c5_steps > 0:
+        torch.cuda.empty_cache()
+        c5_line = c5_capped_line(args, comm, device)
     config_key = f"bratu{N}_gnk_restart{args.restart}_{args.version}_ranks{world}"
     traffic, traffic_src = pmc_traffic(config_key, window)
     t_traffic, t_traffic_src = pmc_traffic(config_key, twindow, section="trial")
@@ -661,6 +767,8 @@ def main():
     }
     if cg_line is not None:
         result["gn_cg"] = cg_line
+    if c5_line is not None:
+        result["c5_capped"] = c5_line
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
         try:
             cb_ = cpu_baseline(N, args.cpu_seconds, args.version, args.restart)

@@ -3,7 +3,7 @@
 
 Public surface (mirrors mariusbaehr/gauss_newton_via_generalized_krylov_subspaces):
   gauss_newton_krylow, gauss_newton, cg_least_squares, BratuPdeProblem,
-  RegressionResult, StepLengthConvergenceError, benchmark_method,
+  RegressionResult, StepLengthConvergenceError, benchmark_method, Problem,
   GeneralizedKrylowSubspaceBreakdown, GeneralizedKrylowSubspaceSpansEntireSpace.
 Hot path: libgnk.so (HIP, gfx950) via ctypes -- see include/gnk.h.
 """
@@ -12,6 +12,7 @@ from .benchmark import benchmark_method, reverse_accumulation
 from .bratu_pde_problem import BratuJacobian, BratuPdeProblem, default_u
 from .gauss_newton import GNSolver, cg_least_squares, gauss_newton
 from .gauss_newton_krylow import GNKSolver, gauss_newton_krylow
+from .problem import Problem, ProblemJacobian
 from .krylow import GeneralizedKrylowSubspaceBreakdown, GeneralizedKrylowSubspaceSpansEntireSpace
 from .regression_result import RegressionResult
 from .slab import Comm, SlabVector, row_partition
@@ -20,4 +21,5 @@ __all__ = [
     "gauss_newton_krylow", "gauss_newton", "cg_least_squares", "BratuPdeProblem", "BratuJacobian",
     "default_u", "RegressionResult", "StepLengthConvergenceError", "GeneralizedKrylowSubspaceBreakdown",
     "GeneralizedKrylowSubspaceSpansEntireSpace", "GNKSolver", "GNSolver", "Comm", "row_partition", "benchmark_method", "reverse_accumulation",
+    "Problem", "ProblemJacobian",
 ]

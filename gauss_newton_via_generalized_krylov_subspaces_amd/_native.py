@@ -18,7 +18,7 @@ import torch
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("GNK_LIB", os.path.join(_HERE, "libgnk.so"))
 GHOST = 2  # GNK_GHOST_ROWS
-TIMER_GRAM, TIMER_JVP, TIMER_CG_MATVEC, TIMER_TRIAL, TIMER_PROBE = 1, 2, 3, 4, 5  # GNK_TIMER_*
+TIMER_GRAM, TIMER_JVP, TIMER_CG_MATVEC, TIMER_TRIAL, TIMER_PROBE, TIMER_CG_XR, TIMER_CG_AUX = 1, 2, 3, 4, 5, 6, 7  # GNK_TIMER_*
 ABI_VERSION = 6  # GNK_ABI_VERSION
 # GNK_TUNE_* keys of gnk_set_tuning (tests / A/B tooling only; the solver never sets them)
 TUNE = {"gram_path": 0, "gram_ring": 1, "gram_v1min": 2, "cg_matvec": 3, "vjpg_blocks": 4, "gram_wide": 5, "gram_rpr": 6, "lls": 7, "vjpg_zmax": 8}

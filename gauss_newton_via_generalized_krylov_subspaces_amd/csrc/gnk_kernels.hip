@@ -5064,7 +5064,10 @@ int gnk_cg_normal_matvec(gnk_ctx* ctx, const double* d, const double* p, double*
   }
   int rc = check_launch(ctx, "cg_normal_matvec");
   if (rc) return rc;
-  return wreduce2(ctx, ctx->scratch, nblk, 1, 2, pq_out);
+  TimedLaunch ta(ctx, GNK_TIMER_CG_AUX, 0.0);
+  rc = wreduce2(ctx, ctx->scratch, nblk, 1, 2, pq_out);
+  ta.done();
+  return rc;
 }
 
 static int cg_step_matvec(gnk_ctx* ctx, const double* d, const double* z, const double* p_in, double* p_out,
@@ -5086,7 +5089,10 @@ static int cg_step_matvec(gnk_ctx* ctx, const double* d, const double* z, const 
   tl.done();
   int rc = check_launch(ctx, "cg_step_matvec");
   if (rc) return rc;
-  return wreduce2(ctx, ctx->scratch, nblk, 1, 2, pq_out);
+  TimedLaunch ta(ctx, GNK_TIMER_CG_AUX, 0.0);
+  rc = wreduce2(ctx, ctx->scratch, nblk, 1, 2, pq_out);
+  ta.done();
+  return rc;
 }
 
 int gnk_cg_step_matvec(gnk_ctx* ctx, const double* d, const double* z, const double* p_in, double* p_out, double* q,
@@ -5105,10 +5111,16 @@ static int cg_update_xr(gnk_ctx* ctx, double alpha, const double* cst, const dou
   if (!ready(ctx)) return -1;
   RowLaunch L = rows(ctx, G, ctx->geo.nrows, vec_of(ctx));
   const int nblk = L.grid.x * L.grid.y;
+  // r -= alpha q, z = M r (+ x += alpha p): q, r, dinv in, r, z out (+ x, p in, x out)
+  TimedLaunch tl(ctx, GNK_TIMER_CG_XR, ((x && p) ? 64.0 : 40.0) * double(ctx->geo.nrows) * double(ctx->geo.N));
   DISPATCH_VEC(ctx, k_cg_xr, L, 0, alpha, p, q, x, r, dinv, z, ctx->geo, L.lr0, L.nlr, ctx->scratch, cst);
+  tl.done();
   int rc = check_launch(ctx, "cg_update_xr");
   if (rc) return rc;
-  return wreduce2(ctx, ctx->scratch, nblk, 2, 4, out);
+  TimedLaunch ta(ctx, GNK_TIMER_CG_AUX, 0.0);
+  rc = wreduce2(ctx, ctx->scratch, nblk, 2, 4, out);
+  ta.done();
+  return rc;
 }
 
 int gnk_cg_update_xr(gnk_ctx* ctx, double alpha, const double* p, const double* q, double* x, double* r,
@@ -5125,7 +5137,9 @@ int gnk_cg_update_xr_dev(gnk_ctx* ctx, const double* state, const double* p, con
 int gnk_cg_scalars(gnk_ctx* ctx, const double* parts, int world, int stage, double* state) {
   if (!ready(ctx)) return -1;
   if (!parts || !state || world < 1 || stage < 0 || stage > 2) return fail(ctx, "cg_scalars: bad arguments");
+  TimedLaunch ta(ctx, GNK_TIMER_CG_AUX, 0.0);
   hipLaunchKernelGGL(k_cg_scalars, dim3(1), dim3(64), 0, ctx->stream, parts, world, stage, state);
+  ta.done();
   return check_launch(ctx, "cg_scalars");
 }
 

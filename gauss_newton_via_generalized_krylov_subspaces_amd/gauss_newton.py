@@ -580,10 +580,9 @@ def gauss_newton(res, x0, jac, args: tuple = (), tol: float = 1e-8, max_iter=100
         problem, y = bratu
         ops = None
     else:
-        from .generic import HostCallableOps
+        from .problem import make_generic_ops
         problem, y = None, None
-        x0h = x0.detach().cpu().numpy() if torch.is_tensor(x0) else np.asarray(x0, dtype=np.float64)
-        ops = HostCallableOps(res, jac, x0h.size, args, device=device, backend=_backend)
+        ops = make_generic_ops(res, jac, x0, args, device=device, backend=_backend)
     if cg_variant != "scipy" and ops is not None:
         raise NotImplementedError("cg_variant='single_reduction' is implemented for the matrix-free Bratu path")
     solver = GNSolver(problem, y, tol=tol, max_iter=max_iter, cg_preconditioner=cg_preconditioner, cg_rtol=cg_rtol,

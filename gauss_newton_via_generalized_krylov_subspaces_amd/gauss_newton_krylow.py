@@ -468,10 +468,9 @@ def gauss_newton_krylow(res, x0, jac, krylow_restart: Optional[int] = None, args
         problem, y = bratu
         ops = None
     else:
-        from .generic import HostCallableOps
+        from .problem import make_generic_ops
         problem, y = None, None
-        x0h = x0.detach().cpu().numpy() if torch.is_tensor(x0) else np.asarray(x0, dtype=np.float64)
-        ops = HostCallableOps(res, jac, x0h.size, args, device=device, backend=_backend)
+        ops = make_generic_ops(res, jac, x0, args, device=device, backend=_backend)
     solver = GNKSolver(problem, y, krylow_restart=krylow_restart, tol=tol, max_iter=max_iter, version=version,
                        comm=comm, device=device, backend=_backend, callback=cb, callback_format=callback_format,
                        ops=ops)

@@ -74,6 +74,83 @@ class DeviceCSR:
         ip, ix, _ = self._arrays[1]
         self.be.csr_spmv(self.shape[1], ip, ix, self._At_data_sq, ones_m, dinv, reciprocal=True)
 
+    def matmat_rows(self, V, k, W):
+        """W[j] = J V[j] for the k basis rows (the reference's ``jac_ev @ krylow.basis``)."""
+        for j in range(k):
+            self.matvec(V[j], W[j])
+
+
+PROBE_NMAX = 1 << 16           # operator Jacobians: diag(J^T J) by probing J with unit vectors up to this n
+
+
+def _host_vec(t):
+    return t.detach().cpu().numpy()
+
+
+class HostOperatorJacobian:
+    """``jac(x)`` returned an operator -- a ``scipy.sparse.linalg.LinearOperator`` or any object with
+    ``J @ v``, ``J @ V`` and ``J.T @ w`` -- which is all the reference ever does with it
+    (ref:gauss_newton_krylow.py:86, ref:krylow.py:62, ref:armijo_goldstein.py:50, ref:gauss_newton.py:36).
+    The products run in the user's object on host arrays, with the reference's call shapes (``J @ V`` on
+    the (n, k) C-ordered basis, ``J.T @ r``), and their results are uploaded; everything else of the
+    loop stays on the device.  Negation is applied on the device (exact, as the reference's ``-J.T @ r``)."""
+
+    def __init__(self, be, J, m, n):
+        self.J, self.be = J, be
+        shape = getattr(J, "shape", None)
+        self.shape = (int(shape[0]), int(shape[1])) if shape is not None else (m, n)
+
+    def _put(self, a, y, negate, what, size):
+        a = np.asarray(a, dtype=np.float64).reshape(-1)
+        if a.size != size:
+            raise ValueError(f"jac(x) {what} returned {a.size} values, expected {size}")
+        y.copy_(self.be.to_device(a))
+        if negate:
+            y.neg_()
+
+    def matvec(self, x, y, negate=False):
+        self._put(self.J @ _host_vec(x), y, negate, "@ v", y.numel())
+
+    def rmatvec(self, w, y, negate=False):
+        self._put(self.J.T @ _host_vec(w), y, negate, ".T @ w", y.numel())
+
+    def matmat_rows(self, V, k, W):
+        Vh = np.ascontiguousarray(_host_vec(V[:k]).T)          # the reference's (n, k) basis layout
+        Y = np.asarray(self.J @ Vh, dtype=np.float64)
+        if Y.shape != (W.shape[1], k):
+            raise ValueError(f"jac(x) @ V returned shape {Y.shape}, expected {(W.shape[1], k)}")
+        W[:k].copy_(self.be.to_device(np.ascontiguousarray(Y.T)))
+
+    def jacobi(self, ones_m, dinv):
+        """dinv = 1 / diag(J^T J) for ``cg_least_squares``' Jacobi preconditioner (ref:gauss_newton.py:50-54;
+        the reference's ``(A.T @ A).diagonal()`` needs a sparse matrix).  The operator is probed with blocks
+        of unit vectors (``J @ E``: the columns of J, exactly), and each column's squares are summed in
+        ascending row order on the device (gnk_csr_spmv, reciprocal mode) -- the order of the sparse path."""
+        n = dinv.numel()
+        if n > PROBE_NMAX:
+            raise NotImplementedError(f"gauss_newton with an operator Jacobian of {n} columns: diag(J^T J) is "
+                                      f"probed column by column up to n = {PROBE_NMAX}; return a sparse matrix, "
+                                      "or use generic.Problem with diag_jtj")
+        b = max(1, min(256, (1 << 24) // max(1, n)))
+        for j0 in range(0, n, b):
+            nb = min(b, n - j0)
+            E = np.zeros((n, nb))
+            E[j0 + np.arange(nb), np.arange(nb)] = 1.0
+            Jb = np.asarray(self.J @ E, dtype=np.float64).reshape(-1, nb)
+            Bt = scipy.sparse.csr_array(np.ascontiguousarray(Jb.T))          # column j of J as row j
+            dev = self.be.device
+            ip = torch.as_tensor(Bt.indptr.astype(np.int32), device=dev)
+            ix = torch.as_tensor(Bt.indices.astype(np.int32), device=dev)
+            dsq = torch.as_tensor(Bt.data * Bt.data, device=dev)
+            self.be.csr_spmv(nb, ip, ix, dsq, ones_m, dinv[j0:j0 + nb], reciprocal=True)
+
+
+def is_operator(J) -> bool:
+    """The reference's duck typing of ``jac(x)``: anything with ``@`` and ``.T`` that is not an array."""
+    if scipy.sparse.issparse(J) or isinstance(J, np.ndarray) or torch.is_tensor(J):
+        return False
+    return hasattr(J, "__matmul__") and hasattr(J, "T")
+
 
 class FlatKrylovBasis:
     """ref:krylow.py:16-73 on flat device vectors (same interface as krylow.DeviceKrylovBasis)."""
@@ -213,10 +290,19 @@ class HostCallableOps:
         return float(self._st[0].item())
 
     def on_jacobian(self, u):
-        """jac(u, *args) (the user's function) -> device CSR of J and J^T, kept for u's buffer."""
+        """jac(u, *args) (the user's function) -> device CSR of J and J^T, kept for u's buffer; an
+        operator (``is_operator``) is kept as it is and applied through ``@`` / ``.T @``."""
         Jh = self.jac(self.to_host(u), *self.args)
-        self._dense[u.data_ptr()] = not scipy.sparse.issparse(Jh)
-        J = DeviceCSR(self.be, Jh)
+        if is_operator(Jh):
+            # the CGLS branch of gauss_newton: the reference's is_sparse test fails for an operator and its
+            # lstsq then raises (tests/golden/operator.json); matrix-free J is what CGLS is for
+            self._dense[u.data_ptr()] = False
+            J = HostOperatorJacobian(self.be, Jh, self.m, self.n)
+        else:
+            if torch.is_tensor(Jh):
+                Jh = Jh.detach().cpu().numpy()
+            self._dense[u.data_ptr()] = not scipy.sparse.issparse(Jh)
+            J = DeviceCSR(self.be, Jh)
         if J.shape[1] != self.n:
             raise ValueError(f"jac returned shape {J.shape}, expected (m, {self.n})")
         if self.m is None:
@@ -256,9 +342,7 @@ class HostCallableOps:
                                       f"<= {self.max_arena_k(r is not None)})")
         if self._W is None or self._W.shape[0] < k:
             self._W = self.be.zeros(max(k, 8), self.m)
-        J = self._jac_of(u)
-        for j in range(k):
-            J.matvec(V[j], self._W[j])
+        self._jac_of(u).matmat_rows(V, k, self._W)
         self.be.flat_gram(self._W, k, rinv, r, self.m, G)
 
     # -- Gauss-Newton / CGLS (gauss_newton.GNSolver, DeviceCG) -----------------------------

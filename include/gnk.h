@@ -307,6 +307,8 @@ int gnk_flat_gram(gnk_ctx* ctx, const double* W, int64_t ldw, int k, const doubl
 #define GNK_TIMER_CG_MATVEC 3
 #define GNK_TIMER_TRIAL 4   /* first Armijo trial + update products, k_gemv_vjpg */
 #define GNK_TIMER_PROBE 5   /* gnk_probe_stream */
+#define GNK_TIMER_CG_XR 6   /* CG r -= alpha q, z = M r (+ x += alpha p), k_cg_xr */
+#define GNK_TIMER_CG_AUX 7  /* CG reductions of the partials (wreduce2) and k_cg_scalars; 0 bytes */
 int gnk_timer_start(gnk_ctx* ctx, int kernel_id, int capacity);
 int gnk_timer_add(gnk_ctx* ctx, int kernel_id);
 int gnk_timer_collect(gnk_ctx* ctx, double* ms_out, double* bytes_out, int capacity);
