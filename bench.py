@@ -592,6 +592,7 @@ def main():
     passes0 = solver.lls.passes
     regions, launches, tlaunches = [], [], []
     comm0 = dict(comm.counters)
+    fb0 = be.segment_fallbacks()
     for _ in range(args.repeats):
         be.timer_start(_native.TIMER_GRAM, cap)
         if not args.no_trial_timer:
@@ -615,6 +616,7 @@ def main():
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             el = t.item()
         regions.append((len(solver.trace) - tr0, el))
+    fallbacks = be.segment_fallbacks() - fb0            # the timed steps' unsegmented reductions only
     comm_steps = max(1, sum(st for st, _ in regions))
     comm_per_step = {key: (comm.counters[key] - comm0[key]) / comm_steps for key in comm0}
     rates = [st / el for st, el in regions]
@@ -729,9 +731,9 @@ def main():
                    "parallelism": f"slab{world}",
                    "transport": (dist.get_backend() if world > 1 else "none"),
                    "reduction_segments": int(stage.seg_rows),
-                   # reductions that ran unsegmented while segments were on (wide Gram passes): 0 = the
-                   # timed steps' bits do not depend on the rank count (same GPU model)
-                   "segment_fallbacks": int(be.segment_fallbacks())},
+                   # reductions of the timed steps that ran unsegmented while segments were on (wide Gram
+                   # passes): 0 = the timed steps' bits do not depend on the rank count
+                   "segment_fallbacks": int(fallbacks)},
         "roofline": {"kernel": "Gram pass of the CholeskyQR solve, J V T on the fly (k_gram_v: VALU, k <= 9; "
                                "k_gram_s: staged fp64 MFMA, k > 9)", "bound": "hbm",
                      "achieved": g_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": g_gbs / HBM_PEAK_GBS,

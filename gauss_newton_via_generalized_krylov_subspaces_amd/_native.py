@@ -21,7 +21,8 @@ GHOST = 2  # GNK_GHOST_ROWS
 TIMER_GRAM, TIMER_JVP, TIMER_CG_MATVEC, TIMER_TRIAL, TIMER_PROBE, TIMER_CG_XR, TIMER_CG_AUX = 1, 2, 3, 4, 5, 6, 7  # GNK_TIMER_*
 ABI_VERSION = 6  # GNK_ABI_VERSION
 # GNK_TUNE_* keys of gnk_set_tuning (tests / A/B tooling only; the solver never sets them)
-TUNE = {"gram_path": 0, "gram_ring": 1, "gram_v1min": 2, "cg_matvec": 3, "vjpg_blocks": 4, "gram_wide": 5, "gram_rpr": 6, "lls": 7, "vjpg_zmax": 8}
+TUNE = {"gram_path": 0, "gram_ring": 1, "gram_v1min": 2, "cg_matvec": 3, "vjpg_blocks": 4, "gram_wide": 5, "gram_rpr": 6, "lls": 7, "vjpg_zmax": 8,
+        "decomp_lds": 9}
 
 _c_int, _c_i64, _c_dbl, _c_vp = ctypes.c_int, ctypes.c_int64, ctypes.c_double, ctypes.c_void_p
 
@@ -85,6 +86,7 @@ SIGNATURES = {
     "gnk_lls_next": (_c_int, [_c_vp, _c_int, _c_int, _c_vp, _c_vp, _c_vp, _c_vp, _c_int, _c_vp, _c_vp, _c_vp, _c_vp,
                               _c_vp, _c_vp]),
     "gnk_probe_mfma_f64": (_c_int, [_c_vp, _c_vp, _c_int, _c_int]),
+    "gnk_decomp_check": (_c_int, [_c_vp, ctypes.POINTER(_c_int), ctypes.POINTER(_c_int), _c_int]),
     "gnk_probe_stream": (_c_int, [_c_vp, _c_vp, _c_vp, _c_vp, _c_dbl, _c_i64, _c_int]),
     "gnk_timer_start": (_c_int, [_c_vp, _c_int, _c_int]),
     "gnk_timer_add": (_c_int, [_c_vp, _c_int]),
@@ -94,6 +96,10 @@ SIGNATURES = {
 }
 
 _LIB = None
+
+
+# tooling exports (not on the solver path) an A/B variant build (GNK_LIB) may lack
+TOOLING_SYMBOLS = {"gnk_decomp_check"}
 
 
 class NativeLibraryError(RuntimeError):
@@ -110,7 +116,10 @@ def load_library(path: str = LIB_PATH):
             f"libgnk.so not found at {path}: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
             "or `make -C gauss_newton_via_generalized_krylov_subspaces_amd/csrc`")
     lib = ctypes.CDLL(path)
+    variant = "GNK_LIB" in os.environ          # tooling A/B against an older build (tools/lib_ab.sh)
     for name, (res, args) in SIGNATURES.items():
+        if variant and name in TOOLING_SYMBOLS and not hasattr(lib, name):
+            continue                           # an older variant build may predate a tooling export
         fn = getattr(lib, name)  # AttributeError = missing export
         fn.restype = res
         fn.argtypes = args
@@ -430,6 +439,15 @@ class HipBackend:
 
     def probe_stream(self, a, b, c, s, n, mode):
         self._call("gnk_probe_stream", _p(a), _p(b), _p(c), float(s), int(n), int(mode))
+
+    def decomp_check(self):
+        """[(table workgroups per CU, live occupancy)] of the persistent kernels' fixed grids (gnk_decomp_check)."""
+        cap = 256
+        t, l = (ctypes.c_int * cap)(), (ctypes.c_int * cap)()
+        n = self.lib.gnk_decomp_check(self.ctx, t, l, cap)
+        if n < 0:
+            self._chk(n, "decomp_check")
+        return [(t[i], l[i]) for i in range(min(n, cap))]
 
     def probe_mfma(self, out, blocks, iters):
         self._call("gnk_probe_mfma_f64", _p(out), int(blocks), int(iters))

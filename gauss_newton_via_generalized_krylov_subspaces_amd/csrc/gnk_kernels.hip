@@ -247,9 +247,10 @@ struct RowLaunch {
 // Lane l <- lane l - 1 / l + 1 of the wave: DPP wave_shr:1 / wave_shl:1 (gfx9), two 32-bit VALU moves per
 // double instead of the two ds_bpermute LDS round trips __shfl_up / __shfl_down compile to (the k = 8, 9
 // VALU Gram pass 6-9 % faster, bit-identical: profiles/round5/lane_dpp_ab.jsonl).  Lanes 0 / 63 get 0:
-// every caller replaces them with the strip's outer neighbour.  Used by the VALU Gram passes only: in the
-// persistent kernels (grid sized by resident blocks) the lower VGPR count changes the occupancy, hence the
-// grid and the partial sums' rounding -- bit for bit the same per point, not per reduction.
+// every caller replaces them with the strip's outer neighbour.  Used by the VALU Gram passes and the row-marching
+// CG normal matvec.  (Round 5 kept them out of the persistent trial kernels, whose grid then followed the
+// occupancy; since round 6 every grid carrying partial sums is a fixed table, so a VGPR change no longer moves
+// any reduction's bits -- DESIGN.md §7d, tests/test_gpu_decomp.py.)
 typedef unsigned int lane_u2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ double lane_prev(double v) {
   const lane_u2 b = __builtin_bit_cast(lane_u2, v);
@@ -2660,10 +2661,12 @@ __global__ __launch_bounds__(64 * GS_NW) __attribute__((amdgpu_waves_per_eu(WPE)
   // This wave's DMA instructions q = wave + 8m (a q past the end re-loads the u row: same bytes,
   // same place): a per-lane source at row 0 and the LDS offset of slot 0 are fixed; a step only adds
   // the row offset and the slot's.
-  // R = 4 (EB): the u ring row runs 3 grid rows ahead (slot of row y holds u(y + 3)), so every 4th
-  // step one jdiag per lane covers 4 rows (lane group g: row x + 2 + g) -- the other steps take their
-  // diagonal from that batch by a lane shuffle, not 4 lanes computing the same exp
-  constexpr bool EB = R == 4;
+  // EB (both ring depths): the u ring row runs 3 grid rows ahead (slot of row y holds u(y + 3)), so every
+  // 4th row one jdiag per lane covers 4 rows (lane group g: row x + 2 + g) -- the other rows take their
+  // diagonal from that batch by a lane shuffle, not 4 lanes computing the same exp.  R = 5 (two column
+  // blocks) batches over its 5-step loop with a runtime batch phase (round 6: one exp per lane every 4 rows
+  // instead of every row; the same exp of the same u, so the same bits)
+  constexpr bool EB = true;
   const double* dsrc[L];
   int ddst[L];
   bool isu[L];
@@ -2827,23 +2830,28 @@ __global__ __launch_bounds__(64 * GS_NW) __attribute__((amdgpu_waves_per_eu(WPE)
     double dn = EB ? 0.0 : -jdiag(cf, lds[2 * SS + ou]);        // row x0 + 1
     __builtin_amdgcn_s_waitcnt(waitcnt_vm_lgkm0(L * INF));         // row x0 + 2 landed
     __builtin_amdgcn_s_barrier();
+    int bph = 0;                                     // R = 5: batch phase of the next row
     for (int64_t xb = x0; xb < x1; xb += R) {
 #pragma unroll
       for (int st = 0; st < R; ++st) {
         const int64_t x = xb + st;
         if (x >= x1) break;
         if (EB) {
-          if (st == 0) {
+          // batch phase of row x, (x - x0) mod 4: compile-time for R = 4, a wave-uniform counter for R = 5
+          const int bs = R == 4 ? st : bph;
+          bph = (bph + 1) & 3;
+          if (bs == 0) {
             dn = __shfl(dnb, 48 + (lane & 15));       // dn(x+1): group 3 of the previous batch
-            // the new batch: group g = dn(x+2+g); u(x+2+g) sits in the slot of row x-1+g (slot g).  Every
-            // wave reads it before any wave's DMA below refills slot 0 (one more barrier per 4 rows: the
-            // u row is DMA'd by one wave, read by all)
-            double ug = lds[cq * SS + ou];
+            // the new batch: group g = dn(x+2+g); u(x+2+g) sits in the slot of row x-1+g (slot (x - x0 + g)
+            // mod R).  Every wave reads it before any wave's DMA below refills the slot of row x-1 (one more
+            // barrier per 4 rows: the u row is DMA'd by one wave, read by all)
+            const int sg = (st + cq) % R;        // (x - x0) = st mod R: the ring's slot of row x - 1 + g
+            double ug = lds[sg * SS + ou];
             asm volatile("" : "+v"(ug));
             __builtin_amdgcn_s_barrier();
             dnb = -jdiag(cf, ug);
           } else {
-            dn = __shfl(dnb, (st - 1) * 16 + (lane & 15));
+            dn = __shfl(dnb, (bs - 1) * 16 + (lane & 15));
           }
         }
         issue_row(x + R - 1, st);                     // into the slot of row x-1
@@ -3787,6 +3795,32 @@ int resident_blocks(gnk_ctx* ctx, const void* fn, int block = BLOCK, size_t lds 
 
 int vec_of(const gnk_ctx* ctx) { return (ctx->geo.N % 2 == 0) ? 2 : 1; }
 
+// ---------------------------------------------------------------- fixed reduction decompositions
+// Every reduction's partial-sum decomposition is a function of the problem geometry (N, the slab's rows,
+// seg_rows) and of the kernel instance only -- never of the occupancy query or the device's CU count (VERDICT r5
+// #2: the persistent kernels once sized their grids from hipOccupancyMaxActiveBlocksPerMultiprocessor, so a
+// register-allocation change of 130 -> 128 VGPRs re-decomposed h = V^T g and moved C2's converged-step tie).
+// The grids of the persistent kernels are the tables below (workgroups per CU) times DECOMP_CUS: the occupancy
+// of each instance at the round-6 build on MI355X (256 CUs), so the default grid is one full round of resident
+// workgroups there.  A build whose occupancy differs runs the same grid in more (or partly filled) rounds --
+// performance only; gnk_decomp_check reports table and live occupancy side by side.
+constexpr int DECOMP_CUS = 256;
+// k_gemv_vjpg<VEC, KCT, PEND>: [VEC - 1][PEND][KCT - 1]
+constexpr unsigned char VJPG_PER_CU[2][2][24] = {
+    {{8, 7, 6, 5, 5, 4, 4, 4, 4, 3, 3, 3, 3, 3, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2},
+     {7, 6, 5, 4, 4, 4, 3, 3, 3, 3, 2, 2, 2, 2, 2, 2, 2, 2, 2, 1, 1, 1, 1, 1}},
+    {{7, 7, 6, 5, 5, 5, 4, 4, 4, 4, 4, 3, 3, 3, 3, 3, 3, 3, 2, 2, 2, 2, 2, 2},
+     {6, 6, 5, 5, 5, 4, 4, 4, 4, 4, 3, 3, 3, 3, 2, 2, 3, 2, 2, 2, 2, 2, 2, 2}}};
+constexpr int GEMVP_PER_CU = 8;                              // k_gemv_p<1>, k_gemv_p<2>
+constexpr int GRAMX_PER_CU[8] = {0, 0, 2, 2, 2, 1, 1, 1};    // k_gram_x<NB> (8-wave workgroups, LDS included)
+constexpr int CGM_PER_CU = 5;                                // k_cg_matvec_m<false / true>
+
+int vjpg_decomp_blocks(int vec, bool pend, int kct) { return int(VJPG_PER_CU[vec - 1][pend ? 1 : 0][kct - 1]) * DECOMP_CUS; }
+
+// GNK_TUNE_DECOMP_LDS: extra dynamic LDS per workgroup of the persistent kernels (tests: fewer resident workgroups,
+// the same grid, so the same bits)
+size_t decomp_lds(const gnk_ctx* ctx);
+
 // k_jvp2 / k_forward2 apply (whole waves of two-point lanes, one block per row segment): turn L (a
 // one-pass row launch) into their grid of row pairs; false leaves L as it was
 bool rows2(const gnk_ctx* ctx, RowLaunch& L) {
@@ -3998,6 +4032,8 @@ int reduce_stats(gnk_ctx* ctx, const double* partial, int nblk, double* stats_ou
 }
 
 int tuning(const gnk_ctx* ctx, int key) { return ctx->tune[key]; }
+
+size_t decomp_lds(const gnk_ctx* ctx) { return size_t(std::max(0, std::min(ctx->tune[GNK_TUNE_DECOMP_LDS], 96 * 1024))); }
 
 // flat geometry helpers (generic problems)
 bool ctx_ok(gnk_ctx* ctx) { return ctx != nullptr; }
@@ -4342,12 +4378,13 @@ static int gemv_vjpg_launch(gnk_ctx* ctx, const char* what, const double* V, int
   const int kct = kk;
   const void* fn = vec_of(ctx) == 2 ? (pend ? vjpg_pick<2, true>(kct) : vjpg_pick<2, false>(kct))
                                     : (pend ? vjpg_pick<1, true>(kct) : vjpg_pick<1, false>(kct));
-  RowLaunch L = rows(ctx, 0, ctx->geo.nrows + 2 * G, vec_of(ctx), resident_blocks(ctx, fn));
-  // segments: the resident grid once per segment (grid.z = nseg + 1: the segments, then the ghost rows);
-  // a segment's partials then depend on the resident count only, not on the slab
+  const int dblk = vjpg_decomp_blocks(vec_of(ctx), pend, kct);     // the fixed grid (one round on MI355X)
+  RowLaunch L = rows(ctx, 0, ctx->geo.nrows + 2 * G, vec_of(ctx), dblk);
+  // segments: that grid once per segment (grid.z = nseg + 1: the segments, then the ghost rows);
+  // a segment's partials then depend on the kernel instance only, not on the slab
   const int ns = seg_on(ctx) ? ctx->nseg + 1 : 1;                  // partial sets
   L.grid.z = unsigned(ns);
-  if (seg_on(ctx)) L.grid.y = unsigned(std::min<int64_t>(resident_blocks(ctx, fn) / L.grid.x, ctx->seg));
+  if (seg_on(ctx)) L.grid.y = unsigned(std::min<int64_t>(dblk / L.grid.x, ctx->seg));
   const int nblk = L.grid.x * L.grid.y;
   const size_t soff = (size_t(nblk) * ns * kct + 1) & ~size_t(1);  // stats partials after the h partials
   if (soff + 2 * size_t(nblk) * ns > SCRATCH_DOUBLES / 2) return fail(ctx, std::string(what) + ": scratch too small");
@@ -4360,7 +4397,7 @@ static int gemv_vjpg_launch(gnk_ctx* ctx, const char* what, const double* V, int
   void* args[] = {&V, &ldv, &k, &c, &hh, &wcol, &r, &x, &g, &geo, &coef, &L.lr0, &L.nlr, &part, &spart, &seg, &nseg};
   // algorithmic bytes (owned rows): the k settled columns, r in, x and g out; pending: w read + written
   TimedLaunch tl(ctx, GNK_TIMER_TRIAL, 8.0 * double(ctx->geo.nrows) * double(ctx->geo.N) * double(k + 3 + (pend ? 2 : 0)));
-  (void)hipLaunchKernel(fn, L.grid, dim3(BLOCK), args, 0, ctx->stream);
+  (void)hipLaunchKernel(fn, L.grid, dim3(BLOCK), args, decomp_lds(ctx), ctx->stream);
   tl.done();
   int rc = check_launch(ctx, what);
   if (rc) return rc;
@@ -4392,15 +4429,15 @@ int gnk_basis_gemv_pending(gnk_ctx* ctx, const double* V, int64_t ldv, int k, co
   if (vec_of(ctx) == 2 && (ldv % 2 != 0)) return fail(ctx, "basis_gemv_pending: ldv must be even");
   double* w = const_cast<double*>(V) + int64_t(k) * ldv;
   if (x == w) return fail(ctx, "basis_gemv_pending: x aliases the pending column");
-  const void* fnp = vec_of(ctx) == 2 ? (const void*)&k_gemv_p<2> : (const void*)&k_gemv_p<1>;
-  RowLaunch L = rows(ctx, 0, ctx->geo.nrows + 2 * G, vec_of(ctx), resident_blocks(ctx, fnp));
+  const int dblk = GEMVP_PER_CU * DECOMP_CUS;
+  RowLaunch L = rows(ctx, 0, ctx->geo.nrows + 2 * G, vec_of(ctx), dblk);
   if (seg_on(ctx)) {                                      // as gemv_vjpg_launch
     L.grid.z = unsigned(ctx->nseg + 1);
-    L.grid.y = unsigned(std::min<int64_t>(resident_blocks(ctx, fnp) / L.grid.x, ctx->seg));
+    L.grid.y = unsigned(std::min<int64_t>(dblk / L.grid.x, ctx->seg));
   }
   const int nblk = L.grid.x * L.grid.y;
-  DISPATCH_VEC(ctx, k_gemv_p, L, 0, V, ldv, k, c, hh, w, x, ctx->geo, L.lr0, L.nlr, ctx->scratch, ctx->seg,
-               ctx->nseg);
+  DISPATCH_VEC(ctx, k_gemv_p, L, decomp_lds(ctx), V, ldv, k, c, hh, w, x, ctx->geo, L.lr0, L.nlr, ctx->scratch,
+               ctx->seg, ctx->nseg);
   int rc = check_launch(ctx, "basis_gemv_pending");
   if (rc) return rc;
   return sreduce_rows(ctx, ctx->scratch, nblk, 2, 2, sum_max_flags(), stats_out);
@@ -4487,11 +4524,11 @@ int gnk_gram(gnk_ctx* ctx, const double* u, const double* V, int64_t ldv, int k,
     const int64_t nstrips = ctx->geo.N / (one_pt ? 64 : GV_SW);
     const int64_t nrows = ctx->geo.nrows;
     // about 8 waves per CU, whole row ranges per strip
-    int64_t nranges = std::max<int64_t>(1, std::min<int64_t>(nrows, int64_t(ctx->num_cus) * 8 / nstrips));
+    int64_t nranges = std::max<int64_t>(1, std::min<int64_t>(nrows, int64_t(DECOMP_CUS) * 8 / nstrips));
     const int rpr_t = tuning(ctx, GNK_TUNE_GRAM_RPR);
     // segments: the decomposition of a one-segment slab, in every segment (0: this grid cannot, per rank)
     const int64_t rpr_s = seg_on(ctx) ? seg_rpr(ctx->seg, std::max<int64_t>(1, std::min<int64_t>(
-                                                    ctx->seg, int64_t(ctx->num_cus) * 8 / nstrips)), nstrips,
+                                                    ctx->seg, int64_t(DECOMP_CUS) * 8 / nstrips)), nstrips,
                                                 BLOCK / 64)
                                       : 0;
     const int64_t rpr = rpr_s > 0 ? rpr_s : rpr_t > 0 ? int64_t(rpr_t) : (nrows + nranges - 1) / nranges;
@@ -4576,10 +4613,10 @@ int gnk_gram(gnk_ctx* ctx, const double* u, const double* V, int64_t ldv, int k,
       const int wgpc = std::max(1, std::min(2, int((160 * 1024) / lds)));
       const int64_t nstrips = ctx->geo.N / GS_SW;
       const int64_t nrows = ctx->geo.nrows;
-      int64_t nranges = std::max<int64_t>(1, std::min<int64_t>(nrows, int64_t(ctx->num_cus) * wgpc / nstrips));
+      int64_t nranges = std::max<int64_t>(1, std::min<int64_t>(nrows, int64_t(DECOMP_CUS) * wgpc / nstrips));
       const int rpr_t = tuning(ctx, GNK_TUNE_GRAM_RPR);
       const int64_t rpr_s = seg_on(ctx) ? seg_rpr(ctx->seg, std::max<int64_t>(1, std::min<int64_t>(
-                                                      ctx->seg, int64_t(ctx->num_cus) * wgpc / nstrips)), nstrips, 1)
+                                                      ctx->seg, int64_t(DECOMP_CUS) * wgpc / nstrips)), nstrips, 1)
                                         : 0;
       const int64_t rpr = rpr_s > 0 ? rpr_s : rpr_t > 0 ? int64_t(rpr_t) : (nrows + nranges - 1) / nranges;
       if (seg_on(ctx) && rpr_s <= 0) ++ctx->seg_fallbacks;
@@ -4657,12 +4694,10 @@ int gnk_gram(gnk_ctx* ctx, const double* u, const double* V, int64_t ldv, int k,
     const int64_t nrows = ctx->geo.nrows;
     // a persistent grid of the resident workgroups over (row range, strip) items; items = lcm(strips,
     // workgroups) when the rows allow, so every workgroup gets the same number
-    const void* fnx = nb == 2 ? (const void*)&k_gram_x<2> : nb == 3 ? (const void*)&k_gram_x<3>
-                    : nb == 4 ? (const void*)&k_gram_x<4> : nb == 5 ? (const void*)&k_gram_x<5>
-                    : nb == 6 ? (const void*)&k_gram_x<6> : (const void*)&k_gram_x<7>;
-    // resident 8-wave workgroups: one per CU at 5..7 blocks (marching rows, B fragments, pair tiles: ~2 waves
-    // per SIMD), two at 2..4
-    const int64_t nwg = resident_blocks(ctx, fnx, 64 * GX_NW, ldsx);
+    // 8-wave workgroups, the fixed grid of GRAMX_PER_CU: one per CU at 5..7 blocks (marching rows, B fragments,
+    // pair tiles: ~2 waves per SIMD), two at 2..4
+    const int64_t nwg = int64_t(GRAMX_PER_CU[nb]) * DECOMP_CUS;
+    const size_t ldsx_l = std::min<size_t>(160 * 1024, ldsx + decomp_lds(ctx));
     int64_t gcd = nstrips, bb = nwg;
     while (bb) { const int64_t t2 = gcd % bb; gcd = bb; bb = t2; }
     int64_t nranges = std::max<int64_t>(1, std::min<int64_t>(nrows, nwg / gcd));
@@ -4674,7 +4709,7 @@ int gnk_gram(gnk_ctx* ctx, const double* u, const double* V, int64_t ldv, int k,
     const int64_t nown = nrows * ctx->geo.N;
     TimedLaunch tlx(ctx, GNK_TIMER_GRAM, 8.0 * double(nown) * double(k + 1 + (r ? 1 : 0)));
 #define GRAMX(NBV)                                                                                                \
-  hipLaunchKernelGGL(k_gram_x<NBV>, dim3(unsigned(nwg)), dim3(64 * GX_NW), ldsx, ctx->stream, u, V, ldv, k, rinv, r, \
+  hipLaunchKernelGGL(k_gram_x<NBV>, dim3(unsigned(nwg)), dim3(64 * GX_NW), ldsx_l, ctx->stream, u, V, ldv, k, rinv, r, \
                      ctx->geo, ctx->coef, rpr, nitems, ctx->scratch)
     if (nb == 2) GRAMX(2); else if (nb == 3) GRAMX(3); else if (nb == 4) GRAMX(4);
     else if (nb == 5) GRAMX(5); else if (nb == 6) GRAMX(6); else GRAMX(7);
@@ -4699,7 +4734,7 @@ int gnk_gram(gnk_ctx* ctx, const double* u, const double* V, int64_t ldv, int k,
     const int64_t nown = ctx->geo.nrows * ctx->geo.N;
     const int64_t nch = (nown + chv - 1) / chv;
     const int wg_per_cu = std::max<int>(1, std::min<int>(8, int((160 * 1024) / ldsw)));
-    int64_t nblk = std::min<int64_t>((nch + nwave - 1) / nwave, int64_t(ctx->num_cus) * wg_per_cu);
+    int64_t nblk = std::min<int64_t>((nch + nwave - 1) / nwave, int64_t(DECOMP_CUS) * wg_per_cu);
     nblk = std::max<int64_t>(nblk, 1);
     if (size_t(nblk) * P * 256 > SCRATCH_DOUBLES) return fail(ctx, "gram: scratch too small");
     const int bc = chv == 64 ? (nb == 1 ? 2 : 4) : 2;
@@ -4714,7 +4749,7 @@ int gnk_gram(gnk_ctx* ctx, const double* u, const double* V, int64_t ldv, int k,
       ldsm = std::max(ldsm, size_t(P) * 256 * 8);
       ldsm = (ldsm + 15) & ~size_t(15);
       const int wgm = std::max<int>(1, std::min<int>(8, int((160 * 1024) / ldsm)));
-      int64_t nbm = int64_t(ctx->num_cus) * wgm;
+      int64_t nbm = int64_t(DECOMP_CUS) * wgm;
       // whole number of row ranges per strip, at least one wave per strip
       int64_t nwv = nbm * nwm;
       if (nwv >= nstrips) {
@@ -4763,7 +4798,7 @@ int gnk_gram(gnk_ctx* ctx, const double* u, const double* V, int64_t ldv, int k,
       ldsp = (ldsp + 15) & ~size_t(15);
       const int64_t nchp = (nown + chp - 1) / chp;
       const int wgp = std::max<int>(1, std::min<int>(8, int((160 * 1024) / ldsp)));
-      int64_t nbp = std::min<int64_t>((nchp + nwave - 1) / nwave, int64_t(ctx->num_cus) * wgp);
+      int64_t nbp = std::min<int64_t>((nchp + nwave - 1) / nwave, int64_t(DECOMP_CUS) * wgp);
       nbp = std::max<int64_t>(nbp, 1);
       if (size_t(nbp) * P * 256 > SCRATCH_DOUBLES) return fail(ctx, "gram: scratch too small");
       TimedLaunch tlp(ctx, GNK_TIMER_GRAM, 8.0 * double(nown) * double(k + 1 + (r ? 1 : 0)));
@@ -4838,7 +4873,7 @@ int gnk_gram(gnk_ctx* ctx, const double* u, const double* V, int64_t ldv, int k,
   const int64_t nown = ctx->geo.nrows * ctx->geo.N;
   const int64_t ntiles = (nown + T - 1) / T;
   const int wg_per_cu = std::max<int>(1, std::min<int>(4, int((160 * 1024) / lds)));
-  int64_t nblk = std::min<int64_t>(ntiles, int64_t(ctx->num_cus) * wg_per_cu);
+  int64_t nblk = std::min<int64_t>(ntiles, int64_t(DECOMP_CUS) * wg_per_cu);
   nblk = std::max<int64_t>(nblk, 1);
   const size_t per_group_pairs = rowsplit ? P : 4 * ppw;
   if (size_t(nblk) * groups * per_group_pairs * 256 > SCRATCH_DOUBLES) return fail(ctx, "gram: scratch too small");
@@ -5035,11 +5070,12 @@ int gnk_flat_gram(gnk_ctx* ctx, const double* W, int64_t ldw, int k, const doubl
   return check_launch(ctx, "flat_gram scatter");
 }
 
-// Row ranges of the row-marching normal matvec: one round of its resident workgroups (nbc strips of 4 waves
-// per range), not a fixed 8 per CU -- at 5 resident workgroups per CU a fixed 8 is 1.6 rounds.  The p.q partials
-// are compensated pairs (Dot2), so the sum's value does not follow the decomposition.
-int64_t cgm_ranges(gnk_ctx* ctx, const void* fn, int64_t nbc, int64_t nrows) {
-  return std::max<int64_t>(1, std::min<int64_t>(nrows, int64_t(resident_blocks(ctx, fn)) / nbc));
+// Row ranges of the row-marching normal matvec: the fixed grid of CGM_PER_CU (one round of its resident
+// workgroups on MI355X; nbc strips of 4 waves per range), not a fixed 8 per CU -- at 5 resident workgroups per CU
+// a fixed 8 is 1.6 rounds.  The p.q partials are compensated pairs (Dot2, about twice working precision, not
+// exact): their bits follow this decomposition, which depends on N and the slab's rows only.
+int64_t cgm_ranges(int64_t nbc, int64_t nrows) {
+  return std::max<int64_t>(1, std::min<int64_t>(nrows, int64_t(CGM_PER_CU) * DECOMP_CUS / nbc));
 }
 
 int gnk_cg_normal_matvec(gnk_ctx* ctx, const double* d, const double* p, double* q, double* pq_out) {
@@ -5048,13 +5084,13 @@ int gnk_cg_normal_matvec(gnk_ctx* ctx, const double* d, const double* p, double*
   if (ctx->geo.N % 2 == 0 && tuning(ctx, GNK_TUNE_CG_MATVEC) != 1) {
     const int64_t nbc = (ctx->geo.N + 4 * CGM_SW - 1) / (4 * CGM_SW);
     const int64_t nrows = ctx->geo.nrows;
-    int64_t nranges = cgm_ranges(ctx, (const void*)&k_cg_matvec_m<false>, nbc, nrows);
+    int64_t nranges = cgm_ranges(nbc, nrows);
     const int64_t rpr = (nrows + nranges - 1) / nranges;
     nranges = (nrows + rpr - 1) / rpr;
     if (nbc * nranges > MAX_RED_BLOCKS) return fail(ctx, "cg_normal_matvec: grid too large");
     nblk = int(nbc * nranges);
     TimedLaunch tl(ctx, GNK_TIMER_CG_MATVEC, 24.0 * double(nrows) * double(ctx->geo.N));
-    hipLaunchKernelGGL(k_cg_matvec_m<false>, dim3(unsigned(nblk)), dim3(BLOCK), 0, ctx->stream, d, p, q, ctx->geo,
+    hipLaunchKernelGGL(k_cg_matvec_m<false>, dim3(unsigned(nblk)), dim3(BLOCK), decomp_lds(ctx), ctx->stream, d, p, q, ctx->geo,
                        ctx->coef, rpr, ctx->scratch, nullptr, nullptr, 0.0, 0, nullptr, 0.0, nullptr);
     tl.done();
   } else {
@@ -5078,13 +5114,13 @@ static int cg_step_matvec(gnk_ctx* ctx, const double* d, const double* z, const 
   if (!d || !z || !p_in || !p_out || !q || p_in == p_out) return fail(ctx, "cg_step_matvec: bad buffers");
   const int64_t nbc = (ctx->geo.N + 4 * CGM_SW - 1) / (4 * CGM_SW);
   const int64_t nrows = ctx->geo.nrows;
-  int64_t nranges = cgm_ranges(ctx, (const void*)&k_cg_matvec_m<true>, nbc, nrows);
+  int64_t nranges = cgm_ranges(nbc, nrows);
   const int64_t rpr = (nrows + nranges - 1) / nranges;
   nranges = (nrows + rpr - 1) / rpr;
   if (nbc * nranges > MAX_RED_BLOCKS) return fail(ctx, "cg_step_matvec: grid too large");
   const int nblk = int(nbc * nranges);
   TimedLaunch tl(ctx, GNK_TIMER_CG_MATVEC, (x ? 56.0 : 40.0) * double(nrows) * double(ctx->geo.N));
-  hipLaunchKernelGGL(k_cg_matvec_m<true>, dim3(unsigned(nblk)), dim3(BLOCK), 0, ctx->stream, d, p_in, q, ctx->geo,
+  hipLaunchKernelGGL(k_cg_matvec_m<true>, dim3(unsigned(nblk)), dim3(BLOCK), decomp_lds(ctx), ctx->stream, d, p_in, q, ctx->geo,
                      ctx->coef, rpr, ctx->scratch, z, p_out, beta, first, x, xalpha, cst);
   tl.done();
   int rc = check_launch(ctx, "cg_step_matvec");
@@ -5160,6 +5196,44 @@ int gnk_cg_update_p(gnk_ctx* ctx, double beta, int first, const double* z, doubl
   RowLaunch L = rows(ctx, G, ctx->geo.nrows, vec_of(ctx), 1 << 30);
   DISPATCH_VEC(ctx, k_cg_p, L, 0, beta, first, z, p, ctx->geo, L.lr0, L.nlr);
   return check_launch(ctx, "cg_update_p");
+}
+
+int gnk_decomp_check(gnk_ctx* ctx, int* table_out, int* live_out, int capacity) {
+  if (!ctx) return -1;
+  std::vector<std::pair<int, const void*>> inst;      // (table workgroups per CU, kernel) in a fixed order
+  std::vector<std::pair<int, size_t>> geom;           // (threads per workgroup, dynamic LDS)
+  for (int v = 1; v <= 2; ++v)
+    for (int p = 0; p <= 1; ++p)
+      for (int kct = 1; kct <= 24; ++kct) {
+        const void* fn = v == 2 ? (p ? vjpg_pick<2, true>(kct) : vjpg_pick<2, false>(kct))
+                                : (p ? vjpg_pick<1, true>(kct) : vjpg_pick<1, false>(kct));
+        inst.push_back({VJPG_PER_CU[v - 1][p][kct - 1], fn});
+        geom.push_back({BLOCK, 0});
+      }
+  inst.push_back({GEMVP_PER_CU, (const void*)&k_gemv_p<1>});
+  geom.push_back({BLOCK, 0});
+  inst.push_back({GEMVP_PER_CU, (const void*)&k_gemv_p<2>});
+  geom.push_back({BLOCK, 0});
+  const void* gx[8] = {nullptr, nullptr, (const void*)&k_gram_x<2>, (const void*)&k_gram_x<3>, (const void*)&k_gram_x<4>,
+                       (const void*)&k_gram_x<5>, (const void*)&k_gram_x<6>, (const void*)&k_gram_x<7>};
+  for (int nb = 2; nb <= 7; ++nb) {
+    const int KP = 16 * nb;
+    inst.push_back({GRAMX_PER_CU[nb], gx[nb]});
+    geom.push_back({64 * GX_NW, size_t(2) * GX_T * (KP + 1) * 8 + size_t(2) * GX_T * 8});
+  }
+  inst.push_back({CGM_PER_CU, (const void*)&k_cg_matvec_m<false>});
+  geom.push_back({BLOCK, 0});
+  inst.push_back({CGM_PER_CU, (const void*)&k_cg_matvec_m<true>});
+  geom.push_back({BLOCK, 0});
+  const int n = int(inst.size());
+  for (int i = 0; i < std::min(n, capacity); ++i) {
+    int per = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, inst[i].second, geom[i].first, geom[i].second) != hipSuccess)
+      per = -1;
+    if (table_out) table_out[i] = inst[i].first;
+    if (live_out) live_out[i] = per;
+  }
+  return n;
 }
 
 int gnk_timer_start(gnk_ctx* ctx, int kernel_id, int capacity) {

@@ -362,6 +362,8 @@ class DeviceCG:
             self.x.copy_(self.b)
             return 0
         maxiter = ops.n_global * 10 if maxiter is None else min(int(maxiter), ops.n_global * 10)
+        if maxiter <= 0:                               # scipy's loop does not run: x = x0 = 0, no callback
+            return maxiter
         if getattr(self, "_st", None) is None:
             self._st = ops.cgd_state()
         st = self._st

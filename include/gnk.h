@@ -55,8 +55,9 @@ int gnk_set_reduce_pairs(gnk_ctx* ctx, int on);
  * GNK path -- the Gram passes of gnk_gram at k <= 20 (N % 128 == 0), the first-trial / pending-column
  * sums (gnk_basis_gemv_vjp_gemv_t*, gnk_basis_gemv_pending), gnk_bratu_residual, gnk_vec_stats,
  * gnk_cgs_update, gnk_vjp_gemv_t, gnk_normalize_jnorm -- is then computed per segment with a block
- * decomposition that depends on N, seg_rows and the device model (its CU count and resident workgroups
- * size some grids: equal bits need the same GPU model on every rank), and the segment values are folded pairwise in
+ * decomposition that depends on N and seg_rows only (every grid that carries partial sums is a fixed
+ * function of the geometry and the kernel instance -- never of occupancy or the CU count: gnk_decomp_check),
+ * and the segment values are folded pairwise in
  * a fixed tree: v[i] += v[i + w] for w = 1, 2, 4, ... (i a multiple of 2w, i + w < n).  With
  * seg_rows = N / P and P / w segments per rank, combining the w ranks' values in the same tree
  * order (slab.Comm) gives the same bits for every w dividing P.  Compensated pairs
@@ -84,7 +85,10 @@ int64_t gnk_segment_fallbacks(const gnk_ctx* ctx);
  *   GNK_TUNE_LLS         1 = the device least-squares solve on one wave, a column per lane (k_lls), instead of
  *                        one entry per thread on 32 x 32 threads (k_lls_2d); the same bits
  *   GNK_TUNE_VJPG_ZMAX   > 0: at most this many column chunks per gnk_vjp_gemv_t launch (tests: the split
- *                        that wide bases with segments need; the same bits) */
+ *                        that wide bases with segments need; the same bits)
+ *   GNK_TUNE_DECOMP_LDS  > 0: bytes of extra dynamic LDS per workgroup of the persistent kernels (first trial,
+ *                        pending column, marching Gram, CG normal matvec): fewer resident workgroups, the same
+ *                        grid -- tests that no result depends on occupancy (the same bits) */
 #define GNK_TUNE_GRAM_PATH 0
 #define GNK_TUNE_GRAM_RING 1
 #define GNK_TUNE_GRAM_V1MIN 2
@@ -94,7 +98,8 @@ int64_t gnk_segment_fallbacks(const gnk_ctx* ctx);
 #define GNK_TUNE_GRAM_RPR 6
 #define GNK_TUNE_LLS 7
 #define GNK_TUNE_VJPG_ZMAX 8
-#define GNK_TUNE_COUNT 9
+#define GNK_TUNE_DECOMP_LDS 9
+#define GNK_TUNE_COUNT 10
 int gnk_set_tuning(gnk_ctx* ctx, int key, int value);
 /* doubles in the context's scratch arena (bounds the wide generic Gram: kp * m <= this) */
 int64_t gnk_scratch_doubles(void);
@@ -313,6 +318,11 @@ int gnk_timer_start(gnk_ctx* ctx, int kernel_id, int capacity);
 int gnk_timer_add(gnk_ctx* ctx, int kernel_id);
 int gnk_timer_collect(gnk_ctx* ctx, double* ms_out, double* bytes_out, int capacity);
 int gnk_timer_collect_ids(gnk_ctx* ctx, double* ms_out, double* bytes_out, int* ids_out, int capacity);
+/* The persistent reduction kernels' fixed grids (workgroups per CU x 256, a table per kernel instance, see
+ * GNK_TUNE_DECOMP_LDS) beside this device's live occupancy (hipOccupancyMaxActiveBlocksPerMultiprocessor) for
+ * the same instances: table_out[i] / live_out[i] for i < min(return value, capacity); returns the instance
+ * count.  A mismatch costs time (partly filled rounds), never bits. */
+int gnk_decomp_check(gnk_ctx* ctx, int* table_out, int* live_out, int capacity);
 /* back-to-back v_mfma_f64_16x16x4_f64 issue-rate probe: blocks x 256 threads,
  * 4 independent accumulators per wave, iters x 4 MFMAs per wave */
 int gnk_probe_mfma_f64(gnk_ctx* ctx, double* out, int blocks, int iters);

@@ -10,7 +10,7 @@ from tests.test_host_logic import _cg_paths
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("N,maxiter,pre", [(512, None, True), (512, 40, True), (256, None, False)])
+@pytest.mark.parametrize("N,maxiter,pre", [(512, None, True), (512, 40, True), (256, None, False), (256, 0, False)])
 def test_cg_device_scalars_bit_identical_hip(N, maxiter, pre):
     from gauss_newton_via_generalized_krylov_subspaces_amd._native import HipBackend
     import torch

@@ -268,13 +268,17 @@ def _cg_paths(backend_factory, N=64, maxiter=None, rtol=1e-8, pre=True):
     return out
 
 
-@pytest.mark.parametrize("maxiter,pre", [(None, True), (None, False), (7, True)])
+@pytest.mark.parametrize("maxiter,pre", [(None, True), (None, False), (7, True), (0, True), (0, False)])
 def test_cg_device_scalars_bit_identical(maxiter, pre):
     """the fused CG with its scalar recurrence on the device (gnk_cg_scalars, lagged read)
-    gives the host-scalar path's iterates and counts bit for bit -- to convergence and at the cap."""
+    gives the host-scalar path's iterates and counts bit for bit -- to convergence and at the cap (maxiter 0:
+    scipy runs no iteration, x = 0)."""
     got = _cg_paths(NumpyBackend, maxiter=maxiter, pre=pre)
     xh, ih = got["host"]
-    assert ih > 5
+    if maxiter == 0:
+        assert ih == 0 and not np.any(xh)
+    else:
+        assert ih > 5
     for name in ("device_lagged", "device"):
         x, it = got[name]
         assert it == ih and np.array_equal(x, xh), name
