@@ -629,7 +629,8 @@ def main():
     passes = solver.lls.passes - passes0
     ppi = passes / max(len(tr), 1)
     fuse_ok = args.version == "res_old"
-    total_bytes = sum(step_bytes(n, s["k"], s["trials"], ppi, fused=fuse_ok and s["k"] <= 24, pending=s["k"] > 1)
+    total_bytes = sum(step_bytes(n, s["k"], s["trials"], ppi, fused=fuse_ok and s["k"] <= solver.basis.FUSE_KMAX,
+                                 pending=s["k"] > 1)
                       for s in tr)
     # dominant kernel: Gram pass (per-launch events; bytes are this rank's slab)
     g_ms = [m for m, _ in launches]

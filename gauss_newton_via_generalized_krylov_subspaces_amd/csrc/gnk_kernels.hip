@@ -834,6 +834,149 @@ __global__ __launch_bounds__(BLOCK) void k_gemv_vjpg(const double* __restrict__ 
   if (PEND) block_sum_max_store(ss, mx, spart + 2 * zb);
 }
 
+// ---------------------------------------------------------------- wide fused first trial (25..208 columns)
+// k_gemv_vjpg for bases too wide to hold a point's basis row in VGPRs (C5 grows the basis to 100 columns, 200 on
+// 8 GPUs): the same products -- the pending column w = g - V hh materialised in place, x = V c, g = -J(x)^T r on
+// owned rows, h = V^T g and {sum w^2, max |w|} over owned rows -- from ONE read of V, through LDS, where the
+// unfused path streams V twice more (gnk_basis_gemv_pending, then gnk_vjp_gemv_t; ref:krylow.py:62-64,
+// ref:armijo_goldstein.py:56).  A workgroup (4 waves) walks 64-point tiles of one grid row, tiles
+// t = blockIdx.x + i gridDim.x of a fixed grid (the reduction decomposition: a function of N, the slab and the
+// width class only); the kk columns of tile t + 1 are loaded as 16-B pairs into VGPRs while tile t is computed
+// from LDS:
+//   A. wave w, lane = point: its quarter of the settled columns, s_w = sum V_j hh_j and xs_w = sum V_j c_j;
+//   B. wave 0: w = wcol - (((s_0 + s_1) + s_2) + s_3), x = (((xs_0 + xs_1) + xs_2) + xs_3) + w c_k (stored, w
+//      written over its column, in LDS too), on owned rows g = -J(x)^T r at the point -> store and LDS;
+//   C. thread j < kk: h_j += the tile's sum of V'_j g (V'_k = w): four point chains, combined in a fixed order.
+// Block partials: h at partial[blk * kk + j], {sum w^2, max |w|} at spart[2 blk].
+constexpr int TW_P = 64;                  // points per tile (32 16-B pairs per column)
+constexpr int TW_LD = TW_P + 2;           // LDS column stride in doubles (16-B aligned; spreads stage C's reads)
+constexpr int TW_KMAX = 208;              // widest basis (kk = k + pending) of the kernel
+template <int ROUNDS, bool PEND>
+__global__ __launch_bounds__(BLOCK) void k_trial_w(const double* __restrict__ V, int64_t ldv, int k,
+                                                   const double* __restrict__ cvec, const double* __restrict__ hh,
+                                                   double* __restrict__ wcol, const double* __restrict__ r,
+                                                   double* __restrict__ x, double* __restrict__ g, Geo geo, Coef c,
+                                                   int64_t ntiles, double* __restrict__ partial,
+                                                   double* __restrict__ spart) {
+  extern __shared__ __attribute__((aligned(16))) double tw[];
+  const int kk = PEND ? k + 1 : k;                    // columns entering x and h
+  const int ks = k;                                   // settled columns read in stage A (PEND: w separately)
+  double* Vt = tw;                                    // [kk][TW_LD]
+  double* gl = Vt + size_t(kk) * TW_LD;               // g of the tile's points
+  double* sp = gl + TW_P;                             // stage-A partials [2][4][TW_P]: s, then xs
+  double* cl = sp + 8 * TW_P;                         // c[0 .. kk)
+  double* hl = cl + kk;                               // hh[0 .. k)
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int64_t N = geo.N;
+  const int64_t tpr = N / TW_P;                       // tiles per grid row
+  for (int j = tid; j < kk; j += BLOCK) cl[j] = cvec[j];
+  if (PEND)
+    for (int j = tid; j < k; j += BLOCK) hl[j] = hh[j];
+  // this thread's pair of every load round: column 8 rho + tid / 32, points 2 (tid % 32) .. + 1
+  const int jc0 = tid >> 5, q2 = 2 * (tid & 31);
+  d2 st[ROUNDS];
+  double rc = 0.0, rn = 0.0, rs = 0.0, redge = 0.0;   // wave 0: r of the tile row / the rows above and below
+  auto load = [&](int64_t t) {
+    const int64_t lr = t / tpr, li0 = lr * N + (t % tpr) * TW_P;
+#pragma unroll
+    for (int rho = 0; rho < ROUNDS; ++rho) {
+      const int j = 8 * rho + jc0;
+      if (j < kk) st[rho] = __builtin_nontemporal_load(reinterpret_cast<const d2*>(V + int64_t(j) * ldv + li0 + q2));
+    }
+    if (wave == 0 && lr >= G && lr < G + geo.nrows) {
+      const int64_t i = li0 + lane;
+      rc = r[i];
+      rn = r[i - N];
+      rs = r[i + N];
+      // lane 0: the west neighbour of the tile's first point, lane 63: the east one of its last (0 at the domain edge)
+      const int64_t iy0 = (t % tpr) * TW_P;
+      redge = lane == 0 ? (iy0 > 0 ? r[i - 1] : 0.0) : (lane == 63 ? (iy0 + TW_P < N ? r[i + 1] : 0.0) : 0.0);
+    }
+  };
+  auto stage = [&]() {
+#pragma unroll
+    for (int rho = 0; rho < ROUNDS; ++rho) {
+      const int j = 8 * rho + jc0;
+      if (j < kk) *reinterpret_cast<d2*>(Vt + j * TW_LD + q2) = st[rho];
+    }
+  };
+  double acc = 0.0, ss = 0.0, mx = 0.0;
+  int64_t t = blockIdx.x;
+  if (t < ntiles) {
+    load(t);
+    stage();
+  }
+  __syncthreads();
+  for (; t < ntiles; t += gridDim.x) {
+    const int64_t lr = t / tpr, li0 = lr * N + (t % tpr) * TW_P;
+    const bool owned = lr >= G && lr < G + geo.nrows;          // block-uniform
+    const double rct = rc, rnt = rn, rst = rs, ret = redge;    // this tile's r (the next load overwrites)
+    const int64_t tn = t + gridDim.x;
+    if (tn < ntiles) load(tn);                                 // in flight during A..C
+    // A: lane = point, wave w sums columns [w Q, (w + 1) Q) of the settled ones in column order
+    {
+      const int Q = (ks + 3) / 4;
+      const int j0 = wave * Q, j1 = min(ks, j0 + Q);
+      double s = 0.0, xs = 0.0;
+      for (int j = j0; j < j1; ++j) {
+        const double v = Vt[j * TW_LD + lane];
+        if (PEND) s = s + v * hl[j];
+        xs = xs + v * cl[j];
+      }
+      sp[wave * TW_P + lane] = s;
+      sp[(4 + wave) * TW_P + lane] = xs;
+    }
+    __syncthreads();
+    // B: wave 0 combines, materialises w, stores x, forms g on owned rows
+    if (wave == 0) {
+      double xs = ((sp[4 * TW_P + lane] + sp[5 * TW_P + lane]) + sp[6 * TW_P + lane]) + sp[7 * TW_P + lane];
+      if (PEND) {
+        const double sw = ((sp[lane] + sp[TW_P + lane]) + sp[2 * TW_P + lane]) + sp[3 * TW_P + lane];
+        const double wv = Vt[k * TW_LD + lane] - sw;
+        Vt[k * TW_LD + lane] = wv;
+        st_nt(wcol + li0 + lane, wv);
+        xs = xs + wv * cl[k];
+        if (owned) {
+          ss += wv * wv;
+          mx = nan_max(mx, fabs(wv));
+        }
+      }
+      st_nt(x + li0 + lane, xs);
+      if (owned) {
+        const int64_t iy = (t % tpr) * TW_P + lane;
+        const bool hw = iy > 0, he = iy + 1 < N;
+        double rw = __shfl_up(rct, 1), re = __shfl_down(rct, 1);
+        if (lane == 0) rw = ret;
+        if (lane == 63) re = ret;
+        const double gv = -vjp_pt(c, jdiag(c, xs), rnt, rw, hw, rct, re, he, rst);
+        st_nt(g + li0 + lane, gv);
+        gl[lane] = gv;
+      }
+    }
+    __syncthreads();
+    // C: thread j accumulates V'_j . g over the tile's points: four chains (points p = 4i + m, i ascending),
+    // ((a_0 + a_1) + a_2) + a_3 added to the running sum -- short dependency chains, a fixed order
+    if (owned && tid < kk) {
+      const double* col = Vt + tid * TW_LD;
+      double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+#pragma unroll 4
+      for (int p = 0; p < TW_P; p += 4) {
+        a0 = a0 + col[p] * gl[p];
+        a1 = a1 + col[p + 1] * gl[p + 1];
+        a2 = a2 + col[p + 2] * gl[p + 2];
+        a3 = a3 + col[p + 3] * gl[p + 3];
+      }
+      acc = acc + (((a0 + a1) + a2) + a3);
+    }
+    __syncthreads();
+    if (tn < ntiles) stage();
+    __syncthreads();
+  }
+  if (tid < kk) partial[size_t(blockIdx.x) * kk + tid] = acc;
+  if (PEND) block_sum_max_store(wave == 0 ? ss : 0.0, wave == 0 ? mx : 0.0, spart);
+}
+
 // g -= V[:, :k] @ h ; partial {sum g^2, max|g|}
 template <int VEC>
 __global__ __launch_bounds__(BLOCK) void k_cgs(const double* __restrict__ V, int64_t ldv, int k,
@@ -1112,11 +1255,13 @@ __global__ __launch_bounds__(BLOCK) void k_cg_matvec_m(const double* __restrict_
     const d2 pv = pnew(ld(z, xr), pi);
     const bool own = xr >= x0 && xr < x1;
     const bool ghost = (x0 == 0 && xr < 0) || (x1 == geo.nrows && xr >= geo.nrows);
-    if (valid && (own || ghost)) *reinterpret_cast<d2*>(p + (G + xr) * N + y0) = pv;
+    // non-temporal stores (p, x, q are re-read only by the next kernels, after other streams): -0.9 % per CG
+    // iteration at 8192^2, bit-identical (profiles/round6/cg_nt_ab.jsonl)
+    if (valid && (own || ghost)) st_nt(p + (G + xr) * N + y0, pv);
     if (x && valid && own) {
-      d2* xp = reinterpret_cast<d2*>(x + (G + xr) * N + y0);
-      const d2 xv = *xp;
-      *xp = d2{xv.x + xalpha * pi.x, xv.y + xalpha * pi.y};
+      double* xp = x + (G + xr) * N + y0;
+      const d2 xv = *reinterpret_cast<const d2*>(xp);
+      st_nt(xp, d2{xv.x + xalpha * pi.x, xv.y + xalpha * pi.y});
     }
     return pv;
   };
@@ -1168,7 +1313,7 @@ __global__ __launch_bounds__(BLOCK) void k_cg_matvec_m(const double* __restrict_
         d2 qo;
         qo.x = vjp_pt(c, dB.x, tn.x, tw, hw0, tc.x, tc.y, true, ts.x);
         qo.y = vjp_pt(c, dB.y, tn.y, tc.x, true, tc.y, tE, he1, ts.y);
-        *reinterpret_cast<d2*>(q + (G + xs) * N + y0) = qo;
+        st_nt(q + (G + xs) * N + y0, qo);
         comp_dot(acc[0], accc[0], pC.x, qo.x);
         comp_dot(acc[0], accc[0], pC.y, qo.y);
       }
@@ -2661,12 +2806,12 @@ __global__ __launch_bounds__(64 * GS_NW) __attribute__((amdgpu_waves_per_eu(WPE)
   // This wave's DMA instructions q = wave + 8m (a q past the end re-loads the u row: same bytes,
   // same place): a per-lane source at row 0 and the LDS offset of slot 0 are fixed; a step only adds
   // the row offset and the slot's.
-  // EB (both ring depths): the u ring row runs 3 grid rows ahead (slot of row y holds u(y + 3)), so every
-  // 4th row one jdiag per lane covers 4 rows (lane group g: row x + 2 + g) -- the other rows take their
-  // diagonal from that batch by a lane shuffle, not 4 lanes computing the same exp.  R = 5 (two column
-  // blocks) batches over its 5-step loop with a runtime batch phase (round 6: one exp per lane every 4 rows
-  // instead of every row; the same exp of the same u, so the same bits)
-  constexpr bool EB = true;
+  // EB (R = 4): the u ring row runs 3 grid rows ahead (slot of row y holds u(y + 3)), so every 4th row one
+  // jdiag per lane covers 4 rows (lane group g: row x + 2 + g) -- the other rows take their diagonal from
+  // that batch by a lane shuffle, not 4 lanes computing the same exp.  (The same batching in the 5-slot ring of
+  // the two-block instances, with a run-time batch phase, was bit-identical and 1-4 % slower at k = 17..20:
+  // profiles/round6/gram_s_eb5_ab.txt; not kept.  The code below handles both.)
+  constexpr bool EB = R == 4;
   const double* dsrc[L];
   int ddst[L];
   bool isu[L];
@@ -4364,11 +4509,52 @@ const void* vjpg_pick(int kct) { return vjpg_table<V_, P_>(kct, std::make_intege
 }  // namespace
 extern "C" {
 
+// The wide fused first trial (k_trial_w, 25..208 columns): a fixed grid of TW_PER_CU workgroups per CU (two fit
+// LDS and VGPRs up to 104 columns, one above) -- the decomposition of its h partials -- capped by the tiles.
+constexpr int TW_PER_CU = 2;
+
+static int trial_w_launch(gnk_ctx* ctx, const char* what, const double* V, int64_t ldv, int k, const double* c,
+                          const double* hh, const double* r, double* x, double* g, double* h_out, double* stats_out) {
+  const bool pend = hh != nullptr;
+  const int kk = k + (pend ? 1 : 0);
+  if (kk > TW_KMAX || seg_on(ctx) || ctx->geo.N % TW_P != 0 || ldv % 2 != 0)
+    return fail(ctx, std::string(what) + ": more than 24 columns need N % 64 == 0, even ldv, no segments, <= 208");
+  double* wcol = pend ? const_cast<double*>(V) + int64_t(k) * ldv : nullptr;
+  if (pend && (g == wcol || x == wcol)) return fail(ctx, std::string(what) + ": g / x alias the pending column");
+  const int need = (kk + 7) / 8;
+  const int R = need <= 4 ? 4 : need <= 7 ? 7 : need <= 13 ? 13 : 26;
+  const int64_t ntiles = (ctx->geo.nrows + 2 * G) * (ctx->geo.N / TW_P);
+  const int nblk = int(std::max<int64_t>(1, std::min<int64_t>(ntiles, int64_t(R <= 13 ? TW_PER_CU : 1) * DECOMP_CUS)));
+  const size_t soff = (size_t(nblk) * kk + 1) & ~size_t(1);
+  if (soff + 2 * size_t(nblk) > SCRATCH_DOUBLES / 2) return fail(ctx, std::string(what) + ": scratch too small");
+  double* spart = ctx->scratch + soff;
+  const size_t lds = (size_t(kk) * TW_LD + 9 * TW_P + 2 * size_t(kk)) * sizeof(double) + decomp_lds(ctx);
+  if (lds > 160 * 1024) return fail(ctx, std::string(what) + ": LDS tile too large");
+  TimedLaunch tl(ctx, GNK_TIMER_TRIAL, 8.0 * double(ctx->geo.nrows) * double(ctx->geo.N) * double(k + 3 + (pend ? 2 : 0)));
+#define TRIALW(RV, PV)                                                                                          \
+  hipLaunchKernelGGL((k_trial_w<RV, PV>), dim3(unsigned(nblk)), dim3(BLOCK), lds, ctx->stream, V, ldv, k, c, hh, wcol, \
+                     r, x, g, ctx->geo, ctx->coef, ntiles, ctx->scratch, spart)
+  if (pend) {
+    if (R == 4) TRIALW(4, true); else if (R == 7) TRIALW(7, true); else if (R == 13) TRIALW(13, true); else TRIALW(26, true);
+  } else {
+    if (R == 4) TRIALW(4, false); else if (R == 7) TRIALW(7, false); else if (R == 13) TRIALW(13, false); else TRIALW(26, false);
+  }
+#undef TRIALW
+  tl.done();
+  int rc = check_launch(ctx, what);
+  if (rc) return rc;
+  const RedDesc dh{ctx->scratch, nblk, kk, kk, int64_t(nblk) * kk, nullptr, h_out, kk};
+  const RedDesc ds{spart, nblk, 2, 2, 0, sum_max_flags(), stats_out, pend ? 2 : 0};
+  return sreduce_n(ctx, dh, ds);
+}
+
 // shared body of gnk_basis_gemv_vjp_gemv_t (hh == nullptr) and its pending-column form
 static int gemv_vjpg_launch(gnk_ctx* ctx, const char* what, const double* V, int64_t ldv, int k, const double* c,
                      const double* hh, const double* r, double* x, double* g, double* h_out, double* stats_out) {
   const bool pend = hh != nullptr;
   const int kk = k + (pend ? 1 : 0);
+  if (k >= 1 && kk > 24 && V && c && r && x && g && h_out && (!pend || stats_out))
+    return trial_w_launch(ctx, what, V, ldv, k, c, hh, r, x, g, h_out, stats_out);
   if (k < 1 || kk > 24) return fail(ctx, std::string(what) + ": columns must be in [1, 24]");
   if (!V || !c || !r || !x || !g || !h_out || (pend && !stats_out)) return fail(ctx, std::string(what) + ": NULL argument");
   if (vec_of(ctx) == 2 && (ldv % 2 != 0)) return fail(ctx, std::string(what) + ": ldv must be even");

@@ -56,14 +56,21 @@ def is_breakdown(sumsq: float, maxabs: float) -> bool:
     return maxabs <= 1e-8 and not math.isnan(sumsq)
 
 
+FUSE_KMAX_NARROW = 24               # k_gemv_vjpg: a point's basis row in VGPRs
+FUSE_KMAX_WIDE = 208                # k_trial_w: 64-point tiles of the basis through LDS (N % 64 == 0, no segments)
+
+
 class DeviceKrylovBasis:
     deferred = True
-    FUSE_KMAX = 24                   # columns the first-trial kernel with the update products covers
 
     def __init__(self, dev, kmax: int):
         self.dev = dev
         self.be = dev.backend
         self.kmax = int(kmax)
+        # columns the first-trial kernel with the update products covers (gnk_basis_gemv_vjp_gemv_t*): the
+        # narrow register kernel up to 24, the wide LDS kernel beyond when the grid allows it
+        wide = dev.slab.N % 64 == 0 and not getattr(dev, "seg_rows", 0)
+        self.FUSE_KMAX = FUSE_KMAX_WIDE if wide else FUSE_KMAX_NARROW
         self.V = self.be.zeros(self.kmax, dev.slab.length)
         self.k = 0                       # settled columns
         self.sc = np.ones(self.kmax)     # reference column j = sc[j] * V[j]

@@ -144,7 +144,9 @@ int gnk_vjp_gemv_t(gnk_ctx* ctx, const double* u, const double* r,
 /* Fused first Armijo trial + basis-update products (version "res_old"): x = V[:, :k] @ c on
  * the whole slab (rounding of gnk_basis_gemv), then on owned rows g = -(J(x)^T r) and
  * h = V[:, :k]^T g -- gnk_basis_gemv followed by gnk_vjp_gemv_t(u = x) from one read of V.
- * 1 <= k <= 24.                      ref:krylow.py:42, :62, :64 + gauss_newton_krylow.py:91,115 */
+ * 1 <= k <= 24 (a point's basis row in VGPRs); 25 <= k <= 208 when N % 64 == 0, ldv is even and
+ * segments are off (64-point tiles of V through LDS; x and w then sum the columns in four blocked
+ * quarters, not in one sequence).   ref:krylow.py:42, :62, :64 + gauss_newton_krylow.py:91,115 */
 int gnk_basis_gemv_vjp_gemv_t(gnk_ctx* ctx, const double* V, int64_t ldv, int k, const double* c, const double* r,
                               double* x, double* g, double* h_out);
 
@@ -159,8 +161,8 @@ int gnk_basis_gemv_vjp_gemv_t(gnk_ctx* ctx, const double* V, int64_t ldv, int k,
 int gnk_basis_gemv_pending(gnk_ctx* ctx, const double* V, int64_t ldv, int k, const double* c, const double* hh,
                            double* x, double* stats_out);
 /* gnk_basis_gemv_vjp_gemv_t with the pending column k materialised as in gnk_basis_gemv_pending:
- * x and h_out cover k + 1 columns (h_out[k] = w . g), stats_out as above.  1 <= k + 1 <= 24;
- * g must not alias column k.        ref:krylow.py:42, :62-71 + gauss_newton_krylow.py:91,115 */
+ * x and h_out cover k + 1 columns (h_out[k] = w . g), stats_out as above.  1 <= k + 1 <= 24, or up to
+ * 208 as gnk_basis_gemv_vjp_gemv_t; g must not alias column k.        ref:krylow.py:42, :62-71 + gauss_newton_krylow.py:91,115 */
 int gnk_basis_gemv_vjp_gemv_t_pending(gnk_ctx* ctx, const double* V, int64_t ldv, int k, const double* c,
                                       const double* hh, const double* r, double* x, double* g, double* h_out,
                                       double* stats_out);

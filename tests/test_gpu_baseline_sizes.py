@@ -85,6 +85,8 @@ def test_c2_full_run_vs_reference(version):
               f"reorderings {seen})")
         # the device's count is one the reference's own arithmetic, reordered, produces (tests/tolerances.py)
         assert rec["nfev"][-1] in seen and out.nrev - rec["nfev"][-1] == case["nrev"] - ref["nfev"][-1]
+        # ... and it is the device's own tracked count: drift inside the family's range is seen too
+        assert rec["nfev"][-1] == T.DEVICE_LAST_NFEV[f"c2_{version}"], rec["nfev"][-1]
         # ... and why it is a tie: the step's Armijo threshold 0.5 t ||J d||^2 (t <= 1) is below one ulp of the
         # loss, so every trial's decision (ref:armijo_goldstein.py:57-62) is the sign of the rounding noise of
         # sum r^2 -- which stays within a few ulps of the previous loss at every trial point

@@ -79,8 +79,16 @@ def last_nfev_range(case):
 # The converged step of C2 res_old is a tie by measurement: its Armijo threshold 0.5 t ||J d||^2 is below one
 # ulp of the loss (the reference's own: 0.01 ulp), so each trial is accepted or halved on the sign of the
 # rounding noise of the two sums of squares.  Bound on that noise, in ulps of the previous loss, for the GPU
-# test's check that every trial of the step sits at it (the reference's own trials: -3.3 and +1.6 ulps).
-ARMIJO_TIE_ULPS = 16.0
+# test's check that every trial of the step sits at it: the reference's own trials sit at -3.3 and +1.6 ulps, the
+# device's at -3.27, -1.64, -1.64, -2.46, +1.64 (round 6, profiles/round6/c2_tie.log) -- 4 ulps covers both.
+ARMIJO_TIE_ULPS = 4.0
+
+
+# The device's own count for C2 res_old's converged last step: tracked, so a kernel or decomposition
+# change that re-rolls the tie is seen; such a change updates this value deliberately, and the same test checks the
+# new count against the counts the reference's reordering family produces (last_nfev_values).  86 since round 4 (the
+# round-6 fixed decompositions keep every reduction's bits: tests/test_gpu_decomp.py).
+DEVICE_LAST_NFEV = {"c2_res_old": 86}
 
 
 def last_nfev_values(case):
