@@ -295,8 +295,9 @@ def c5_capped_line(args, comm, device, grid=16384, restart=100):
     steps = min(args.c5_steps, restart - 1)
     with contextlib.redirect_stdout(io.StringIO()):
         s.step()                                                   # warm-up: k = 1
-        cap = 4 * (steps + 2)
+        cap = 8 * (steps + 2)
         be.timer_start(_native.TIMER_GRAM, cap)
+        be.timer_add(_native.TIMER_TRIAL)
         tr0 = len(s.trace)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
@@ -308,6 +309,8 @@ def c5_capped_line(args, comm, device, grid=16384, restart=100):
     got = be.timer_collect_ids(cap)
     done = len(s.trace) - tr0
     n = s.dev.slab.nrows * grid
+    trials = [(m, b) for i, m, b in got if i == _native.TIMER_TRIAL]
+    got = [(i, m, b) for i, m, b in got if i == _native.TIMER_GRAM]
     by_k, flops, gms = {}, 0.0, 0.0
     for _, m, b in got:
         kk = int(round(b / (8.0 * n))) - 2
@@ -330,6 +333,13 @@ def c5_capped_line(args, comm, device, grid=16384, restart=100):
                                         "GBs": 8.0 * n * (kk + 2) / (np.mean(v) * 1e-3) / 1e9,
                                         "TFLOPs": gram_useful_flops(n, kk) / (np.mean(v) * 1e-3) / 1e12}
                               for kk, v in sorted(by_k.items())}},
+            "trial": {"kernel": "first Armijo trial + update products: k_gemv_vjpg (<= 24 columns), k_trial_w (25..208, "
+                                "LDS tiles)", "launches": len(trials),
+                      "share_of_step_time": sum(m for m, _ in trials) * 1e-3 / el,
+                      "by_vectors": {str(v): {"ms": float(np.mean([m for m, b in trials if int(round(b / (8.0 * n))) == v])),
+                                              "GBs": 8.0 * n * v / (np.mean([m for m, b in trials
+                                                                             if int(round(b / (8.0 * n))) == v]) * 1e-3) / 1e9}
+                                     for v in sorted({int(round(b / (8.0 * n))) for _, b in trials})}},
             "note": "C5 at 16384^2 with the basis capped at 100 columns (restart 100): V = 101 x 2.15 GB; the literal "
                     "k = 200 (429 GB) does not fit one GPU. One warm-up step (k = 1), then the cycle's steps timed."}
 

@@ -839,129 +839,167 @@ __global__ __launch_bounds__(BLOCK) void k_gemv_vjpg(const double* __restrict__ 
 // 8 GPUs): the same products -- the pending column w = g - V hh materialised in place, x = V c, g = -J(x)^T r on
 // owned rows, h = V^T g and {sum w^2, max |w|} over owned rows -- from ONE read of V, through LDS, where the
 // unfused path streams V twice more (gnk_basis_gemv_pending, then gnk_vjp_gemv_t; ref:krylow.py:62-64,
-// ref:armijo_goldstein.py:56).  A workgroup (4 waves) walks 64-point tiles of one grid row, tiles
-// t = blockIdx.x + i gridDim.x of a fixed grid (the reduction decomposition: a function of N, the slab and the
-// width class only); the kk columns of tile t + 1 are loaded as 16-B pairs into VGPRs while tile t is computed
-// from LDS:
-//   A. wave w, lane = point: its quarter of the settled columns, s_w = sum V_j hh_j and xs_w = sum V_j c_j;
+// ref:armijo_goldstein.py:56).  A workgroup (4 waves) walks TP-point tiles of one grid row (TP = 128 up to 104
+// columns, 64 beyond: the tile's kk columns fit LDS), tiles t = blockIdx.x + i gridDim.x of a fixed grid (the
+// reduction decomposition: a function of N, the slab and the width class only); the kk columns of the next DEPTH
+// tiles are loaded as 16-B pairs into VGPRs while tile t is computed from LDS:
+//   A. wave w, lane = TP / 64 consecutive points: its quarter of the settled columns, s_w = sum V_j hh_j and
+//      xs_w = sum V_j c_j;
 //   B. wave 0: w = wcol - (((s_0 + s_1) + s_2) + s_3), x = (((xs_0 + xs_1) + xs_2) + xs_3) + w c_k (stored, w
 //      written over its column, in LDS too), on owned rows g = -J(x)^T r at the point -> store and LDS;
 //   C. thread j < kk: h_j += the tile's sum of V'_j g (V'_k = w): four point chains, combined in a fixed order.
 // Block partials: h at partial[blk * kk + j], {sum w^2, max |w|} at spart[2 blk].
-constexpr int TW_P = 64;                  // points per tile (32 16-B pairs per column)
-constexpr int TW_LD = TW_P + 2;           // LDS column stride in doubles (16-B aligned; spreads stage C's reads)
 constexpr int TW_KMAX = 208;              // widest basis (kk = k + pending) of the kernel
-template <int ROUNDS, bool PEND>
-__global__ __launch_bounds__(BLOCK) void k_trial_w(const double* __restrict__ V, int64_t ldv, int k,
+template <int TP, int ROUNDS, int DEPTH, bool PEND, int WPE>
+__global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) void k_trial_w(const double* __restrict__ V,
+                                                   int64_t ldv, int k,
                                                    const double* __restrict__ cvec, const double* __restrict__ hh,
                                                    double* __restrict__ wcol, const double* __restrict__ r,
                                                    double* __restrict__ x, double* __restrict__ g, Geo geo, Coef c,
                                                    int64_t ntiles, double* __restrict__ partial,
                                                    double* __restrict__ spart) {
+  constexpr int LD = TP + 2;                          // LDS column stride (doubles): 16-B aligned, spreads stage C
+  constexpr int PPL = TP / 64;                        // points per lane in stages A and B (consecutive)
+  constexpr int HALF = TP / 2;                        // 16-B pairs per column
+  constexpr int CPR = BLOCK / HALF;                   // columns per load round
   extern __shared__ __attribute__((aligned(16))) double tw[];
   const int kk = PEND ? k + 1 : k;                    // columns entering x and h
   const int ks = k;                                   // settled columns read in stage A (PEND: w separately)
-  double* Vt = tw;                                    // [kk][TW_LD]
-  double* gl = Vt + size_t(kk) * TW_LD;               // g of the tile's points
-  double* sp = gl + TW_P;                             // stage-A partials [2][4][TW_P]: s, then xs
-  double* cl = sp + 8 * TW_P;                         // c[0 .. kk)
+  double* Vt = tw;                                    // [kk][LD]
+  double* gl = Vt + size_t(kk) * LD;                  // g of the tile's points
+  double* sp = gl + TP;                               // stage-A partials [2][4][TP]: s, then xs
+  double* cl = sp + 8 * TP;                           // c[0 .. kk)
   double* hl = cl + kk;                               // hh[0 .. k)
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int64_t N = geo.N;
-  const int64_t tpr = N / TW_P;                       // tiles per grid row
+  const int64_t tpr = N / TP;                         // tiles per grid row
+  const int64_t GS = gridDim.x;                       // tile stride
   for (int j = tid; j < kk; j += BLOCK) cl[j] = cvec[j];
   if (PEND)
     for (int j = tid; j < k; j += BLOCK) hl[j] = hh[j];
-  // this thread's pair of every load round: column 8 rho + tid / 32, points 2 (tid % 32) .. + 1
-  const int jc0 = tid >> 5, q2 = 2 * (tid & 31);
-  d2 st[ROUNDS];
-  double rc = 0.0, rn = 0.0, rs = 0.0, redge = 0.0;   // wave 0: r of the tile row / the rows above and below
-  auto load = [&](int64_t t) {
-    const int64_t lr = t / tpr, li0 = lr * N + (t % tpr) * TW_P;
+  // this thread's pair of every load round: column CPR rho + tid / HALF, points 2 (tid % HALF) .. + 1
+  const int jc0 = tid / HALF, q2 = 2 * (tid % HALF);
+  // DEPTH tiles' columns in flight in VGPRs (buffer b: st_b; r_b = wave 0's r of the tile's points (PPL), the
+  // rows above / below, and the strip's outer neighbour for lanes 0 / 63)
+  d2 st0[ROUNDS], st1[DEPTH == 2 ? ROUNDS : 1];
+  double r0[3 * PPL + 1] = {}, r1[3 * PPL + 1] = {};
+  auto load = [&](int64_t t, d2* st, double* rr) {
+    const int64_t lr = t / tpr, li0 = lr * N + (t % tpr) * TP;
 #pragma unroll
     for (int rho = 0; rho < ROUNDS; ++rho) {
-      const int j = 8 * rho + jc0;
+      const int j = CPR * rho + jc0;
       if (j < kk) st[rho] = __builtin_nontemporal_load(reinterpret_cast<const d2*>(V + int64_t(j) * ldv + li0 + q2));
     }
     if (wave == 0 && lr >= G && lr < G + geo.nrows) {
-      const int64_t i = li0 + lane;
-      rc = r[i];
-      rn = r[i - N];
-      rs = r[i + N];
+      const int64_t i = li0 + PPL * lane;
+      if constexpr (PPL == 2) {
+        const d2 a = *reinterpret_cast<const d2*>(r + i), b = *reinterpret_cast<const d2*>(r + i - N);
+        const d2 cc = *reinterpret_cast<const d2*>(r + i + N);
+        rr[0] = a.x; rr[1] = a.y; rr[2] = b.x; rr[3] = b.y; rr[4] = cc.x; rr[5] = cc.y;
+      } else {
+        rr[0] = r[i];
+        rr[1] = r[i - N];
+        rr[2] = r[i + N];
+      }
       // lane 0: the west neighbour of the tile's first point, lane 63: the east one of its last (0 at the domain edge)
-      const int64_t iy0 = (t % tpr) * TW_P;
-      redge = lane == 0 ? (iy0 > 0 ? r[i - 1] : 0.0) : (lane == 63 ? (iy0 + TW_P < N ? r[i + 1] : 0.0) : 0.0);
+      const int64_t iy0 = (t % tpr) * TP;
+      rr[3 * PPL] = lane == 0 ? (iy0 > 0 ? r[li0 - 1] : 0.0) : (lane == 63 ? (iy0 + TP < N ? r[li0 + TP] : 0.0) : 0.0);
     }
   };
-  auto stage = [&]() {
+  auto stage = [&](const d2* st) {
 #pragma unroll
     for (int rho = 0; rho < ROUNDS; ++rho) {
-      const int j = 8 * rho + jc0;
-      if (j < kk) *reinterpret_cast<d2*>(Vt + j * TW_LD + q2) = st[rho];
+      const int j = CPR * rho + jc0;
+      if (j < kk) *reinterpret_cast<d2*>(Vt + j * LD + q2) = st[rho];
     }
   };
   double acc = 0.0, ss = 0.0, mx = 0.0;
-  int64_t t = blockIdx.x;
-  if (t < ntiles) {
-    load(t);
-    stage();
-  }
-  __syncthreads();
-  for (; t < ntiles; t += gridDim.x) {
-    const int64_t lr = t / tpr, li0 = lr * N + (t % tpr) * TW_P;
+  // tile t from LDS (its r in rr); ends with every wave past its LDS reads
+  auto tile = [&](int64_t t, const double* rr) {
+    const int64_t lr = t / tpr, li0 = lr * N + (t % tpr) * TP;
     const bool owned = lr >= G && lr < G + geo.nrows;          // block-uniform
-    const double rct = rc, rnt = rn, rst = rs, ret = redge;    // this tile's r (the next load overwrites)
-    const int64_t tn = t + gridDim.x;
-    if (tn < ntiles) load(tn);                                 // in flight during A..C
-    // A: lane = point, wave w sums columns [w Q, (w + 1) Q) of the settled ones in column order
+    const int p0 = PPL * lane;                                 // this lane's first point in the tile
+    // A: wave w sums columns [w Q, (w + 1) Q) of the settled ones in column order, per point
     {
       const int Q = (ks + 3) / 4;
       const int j0 = wave * Q, j1 = min(ks, j0 + Q);
-      double s = 0.0, xs = 0.0;
+      double s[PPL] = {}, xs[PPL] = {};
       for (int j = j0; j < j1; ++j) {
-        const double v = Vt[j * TW_LD + lane];
-        if (PEND) s = s + v * hl[j];
-        xs = xs + v * cl[j];
+        double v[PPL];
+        if constexpr (PPL == 2) {
+          const d2 vv = *reinterpret_cast<const d2*>(Vt + j * LD + p0);
+          v[0] = vv.x;
+          v[1] = vv.y;
+        } else {
+          v[0] = Vt[j * LD + p0];
+        }
+#pragma unroll
+        for (int q = 0; q < PPL; ++q) {
+          if (PEND) s[q] = s[q] + v[q] * hl[j];
+          xs[q] = xs[q] + v[q] * cl[j];
+        }
       }
-      sp[wave * TW_P + lane] = s;
-      sp[(4 + wave) * TW_P + lane] = xs;
+#pragma unroll
+      for (int q = 0; q < PPL; ++q) {
+        sp[wave * TP + p0 + q] = s[q];
+        sp[(4 + wave) * TP + p0 + q] = xs[q];
+      }
     }
     __syncthreads();
     // B: wave 0 combines, materialises w, stores x, forms g on owned rows
     if (wave == 0) {
-      double xs = ((sp[4 * TW_P + lane] + sp[5 * TW_P + lane]) + sp[6 * TW_P + lane]) + sp[7 * TW_P + lane];
-      if (PEND) {
-        const double sw = ((sp[lane] + sp[TW_P + lane]) + sp[2 * TW_P + lane]) + sp[3 * TW_P + lane];
-        const double wv = Vt[k * TW_LD + lane] - sw;
-        Vt[k * TW_LD + lane] = wv;
-        st_nt(wcol + li0 + lane, wv);
-        xs = xs + wv * cl[k];
-        if (owned) {
-          ss += wv * wv;
-          mx = nan_max(mx, fabs(wv));
+      double xv[PPL];
+#pragma unroll
+      for (int q = 0; q < PPL; ++q) {
+        const int p = p0 + q;
+        double xs = ((sp[4 * TP + p] + sp[5 * TP + p]) + sp[6 * TP + p]) + sp[7 * TP + p];
+        if (PEND) {
+          const double sw = ((sp[p] + sp[TP + p]) + sp[2 * TP + p]) + sp[3 * TP + p];
+          const double wv = Vt[k * LD + p] - sw;
+          Vt[k * LD + p] = wv;
+          st_nt(wcol + li0 + p, wv);
+          xs = xs + wv * cl[k];
+          if (owned) {
+            ss += wv * wv;
+            mx = nan_max(mx, fabs(wv));
+          }
         }
+        xv[q] = xs;
       }
-      st_nt(x + li0 + lane, xs);
+      if constexpr (PPL == 2) st_nt(x + li0 + p0, d2{xv[0], xv[1]});
+      else st_nt(x + li0 + p0, xv[0]);
       if (owned) {
-        const int64_t iy = (t % tpr) * TW_P + lane;
-        const bool hw = iy > 0, he = iy + 1 < N;
-        double rw = __shfl_up(rct, 1), re = __shfl_down(rct, 1);
-        if (lane == 0) rw = ret;
-        if (lane == 63) re = ret;
-        const double gv = -vjp_pt(c, jdiag(c, xs), rnt, rw, hw, rct, re, he, rst);
-        st_nt(g + li0 + lane, gv);
-        gl[lane] = gv;
+        const int64_t iy = (t % tpr) * TP + p0;
+        const double re_ = rr[3 * PPL];
+        double gv[PPL];
+        if constexpr (PPL == 2) {
+          // points 2l, 2l + 1: rc = (rr[0], rr[1]), north (rr[2], rr[3]), south (rr[4], rr[5])
+          double rw = lane_prev(rr[1]), re = lane_next(rr[0]);
+          if (lane == 0) rw = re_;
+          if (lane == 63) re = re_;
+          gv[0] = -vjp_pt(c, jdiag(c, xv[0]), rr[2], rw, iy > 0, rr[0], rr[1], true, rr[4]);
+          gv[1] = -vjp_pt(c, jdiag(c, xv[1]), rr[3], rr[0], true, rr[1], re, iy + 2 < N, rr[5]);
+          st_nt(g + li0 + p0, d2{gv[0], gv[1]});
+        } else {
+          double rw = lane_prev(rr[0]), re = lane_next(rr[0]);
+          if (lane == 0) rw = re_;
+          if (lane == 63) re = re_;
+          gv[0] = -vjp_pt(c, jdiag(c, xv[0]), rr[1], rw, iy > 0, rr[0], re, iy + 1 < N, rr[2]);
+          st_nt(g + li0 + p0, gv[0]);
+        }
+#pragma unroll
+        for (int q = 0; q < PPL; ++q) gl[p0 + q] = gv[q];
       }
     }
     __syncthreads();
     // C: thread j accumulates V'_j . g over the tile's points: four chains (points p = 4i + m, i ascending),
     // ((a_0 + a_1) + a_2) + a_3 added to the running sum -- short dependency chains, a fixed order
     if (owned && tid < kk) {
-      const double* col = Vt + tid * TW_LD;
+      const double* col = Vt + tid * LD;
       double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
-#pragma unroll 4
-      for (int p = 0; p < TW_P; p += 4) {
+#pragma unroll 2
+      for (int p = 0; p < TP; p += 4) {
         a0 = a0 + col[p] * gl[p];
         a1 = a1 + col[p + 1] * gl[p + 1];
         a2 = a2 + col[p + 2] * gl[p + 2];
@@ -970,8 +1008,39 @@ __global__ __launch_bounds__(BLOCK) void k_trial_w(const double* __restrict__ V,
       acc = acc + (((a0 + a1) + a2) + a3);
     }
     __syncthreads();
-    if (tn < ntiles) stage();
-    __syncthreads();
+  };
+  int64_t t = blockIdx.x;
+  if (t < ntiles) {
+    load(t, st0, r0);
+    stage(st0);
+  }
+  if (DEPTH == 2 && t + GS < ntiles) load(t + GS, st1, r1);
+  __syncthreads();
+  while (t < ntiles) {
+    // tile t in LDS, its r in r0; st0 free (staged); DEPTH 2: st1 holds tile t + GS
+    {
+      double cur[3 * PPL + 1];
+#pragma unroll
+      for (int q = 0; q < 3 * PPL + 1; ++q) cur[q] = r0[q];
+      const int64_t tl = t + DEPTH * GS;                       // the next free buffer's tile
+      if (tl < ntiles) load(tl, st0, r0);
+      tile(t, cur);
+      if (t + GS < ntiles) stage(DEPTH == 2 ? st1 : st0);
+      __syncthreads();
+      t += GS;
+    }
+    if (DEPTH == 1 || t >= ntiles) continue;
+    // tile t in LDS, its r in r1; st1 free; st0 holds tile t + GS
+    {
+      double cur[3 * PPL + 1];
+#pragma unroll
+      for (int q = 0; q < 3 * PPL + 1; ++q) cur[q] = r1[q];
+      if (t + 2 * GS < ntiles) load(t + 2 * GS, st1, r1);
+      tile(t, cur);
+      if (t + GS < ntiles) stage(st0);
+      __syncthreads();
+      t += GS;
+    }
   }
   if (tid < kk) partial[size_t(blockIdx.x) * kk + tid] = acc;
   if (PEND) block_sum_max_store(wave == 0 ? ss : 0.0, wave == 0 ? mx : 0.0, spart);
@@ -4509,36 +4578,53 @@ const void* vjpg_pick(int kct) { return vjpg_table<V_, P_>(kct, std::make_intege
 }  // namespace
 extern "C" {
 
-// The wide fused first trial (k_trial_w, 25..208 columns): a fixed grid of TW_PER_CU workgroups per CU (two fit
-// LDS and VGPRs up to 104 columns, one above) -- the decomposition of its h partials -- capped by the tiles.
-constexpr int TW_PER_CU = 2;
+// The wide fused first trial (k_trial_w, 25..208 columns) per width class (64-point tiles; ROUNDS 4 / 7 / 13 / 26:
+// up to 32 / 56 / 104 / 208 columns): tiles in flight per workgroup (DEPTH), a fixed grid of TW_PER_CU workgroups
+// per CU -- the decomposition of its h partials -- capped by the tiles, and the register budget that lets that
+// many be resident (amdgpu_waves_per_eu: one wave per SIMD per workgroup).  8192^2, ms per launch
+// (profiles/round6/trial_w_ab.jsonl): 25..32 columns depth 2 x 3 per CU 3.87-4.37 vs depth 1 x 4 4.45-5.15;
+// 40..56 depth 1 x 3 5.08-6.27 vs depth 2 x 3 7.7-9.3; 64..100 depth 2 x 2 7.9-11.5 vs 2 x 3 10.2-13.2.
+constexpr int TW_DEPTH[4] = {2, 1, 2, 1};
+constexpr int TW_PER_CU[4] = {3, 3, 2, 1};
 
 static int trial_w_launch(gnk_ctx* ctx, const char* what, const double* V, int64_t ldv, int k, const double* c,
                           const double* hh, const double* r, double* x, double* g, double* h_out, double* stats_out) {
   const bool pend = hh != nullptr;
   const int kk = k + (pend ? 1 : 0);
-  if (kk > TW_KMAX || seg_on(ctx) || ctx->geo.N % TW_P != 0 || ldv % 2 != 0)
-    return fail(ctx, std::string(what) + ": more than 24 columns need N % 64 == 0, even ldv, no segments, <= 208");
+  if (kk > TW_KMAX || seg_on(ctx) || ctx->geo.N % 128 != 0 || ldv % 2 != 0)
+    return fail(ctx, std::string(what) + ": more than 24 columns need N % 128 == 0, even ldv, no segments, <= 208");
   double* wcol = pend ? const_cast<double*>(V) + int64_t(k) * ldv : nullptr;
   if (pend && (g == wcol || x == wcol)) return fail(ctx, std::string(what) + ": g / x alias the pending column");
-  const int need = (kk + 7) / 8;
-  const int R = need <= 4 ? 4 : need <= 7 ? 7 : need <= 13 ? 13 : 26;
-  const int64_t ntiles = (ctx->geo.nrows + 2 * G) * (ctx->geo.N / TW_P);
-  const int nblk = int(std::max<int64_t>(1, std::min<int64_t>(ntiles, int64_t(R <= 13 ? TW_PER_CU : 1) * DECOMP_CUS)));
+  const int cls = kk <= 32 ? 0 : kk <= 56 ? 1 : kk <= 104 ? 2 : 3;
+  constexpr int TP = 64;
+  // GNK_TUNE_TRIALW (tooling A/B): 16 * depth + workgroups per CU
+  const int tt = tuning(ctx, GNK_TUNE_TRIALW);
+  const int depth = (tt >> 4) == 1 ? 1 : (tt >> 4) == 2 ? 2 : TW_DEPTH[cls];
+  const int per_cu = (tt & 15) ? (tt & 15) : TW_PER_CU[cls];
+  if (cls == 3 && depth == 2) return fail(ctx, std::string(what) + ": depth 2 not built for > 104 columns");
+  const int64_t ntiles = (ctx->geo.nrows + 2 * G) * (ctx->geo.N / TP);
+  const int nblk = int(std::max<int64_t>(1, std::min<int64_t>(ntiles, int64_t(per_cu) * DECOMP_CUS)));
   const size_t soff = (size_t(nblk) * kk + 1) & ~size_t(1);
   if (soff + 2 * size_t(nblk) > SCRATCH_DOUBLES / 2) return fail(ctx, std::string(what) + ": scratch too small");
   double* spart = ctx->scratch + soff;
-  const size_t lds = (size_t(kk) * TW_LD + 9 * TW_P + 2 * size_t(kk)) * sizeof(double) + decomp_lds(ctx);
+  const size_t lds = (size_t(kk) * (TP + 2) + 9 * size_t(TP) + 2 * size_t(kk)) * sizeof(double) + decomp_lds(ctx);
   if (lds > 160 * 1024) return fail(ctx, std::string(what) + ": LDS tile too large");
   TimedLaunch tl(ctx, GNK_TIMER_TRIAL, 8.0 * double(ctx->geo.nrows) * double(ctx->geo.N) * double(k + 3 + (pend ? 2 : 0)));
-#define TRIALW(RV, PV)                                                                                          \
-  hipLaunchKernelGGL((k_trial_w<RV, PV>), dim3(unsigned(nblk)), dim3(BLOCK), lds, ctx->stream, V, ldv, k, c, hh, wcol, \
-                     r, x, g, ctx->geo, ctx->coef, ntiles, ctx->scratch, spart)
+#define TRIALW(TV, RV, DV, PV, WV)                                                                                  \
+  hipLaunchKernelGGL((k_trial_w<TV, RV, DV, PV, WV>), dim3(unsigned(nblk)), dim3(BLOCK), lds, ctx->stream, V, ldv, k, c, \
+                     hh, wcol, r, x, g, ctx->geo, ctx->coef, ntiles, ctx->scratch, spart)
+#define TRIALWD(TV, RV, PV, WV, WV2) do { if (depth == 2) TRIALW(TV, RV, 2, PV, WV2); else TRIALW(TV, RV, 1, PV, WV); } \
+  while (0)
+  // register budget (amdgpu_waves_per_eu) of each class: its workgroups per CU, one wave per SIMD each (depth 2:
+  // one fewer for the two tiles' VGPRs; 2 = the default for 57..104 columns, A/B in profiles/round6/trial_w_ab.jsonl)
   if (pend) {
-    if (R == 4) TRIALW(4, true); else if (R == 7) TRIALW(7, true); else if (R == 13) TRIALW(13, true); else TRIALW(26, true);
+    if (cls == 0) TRIALWD(64, 4, true, 4, 3); else if (cls == 1) TRIALWD(64, 7, true, 3, 2);
+    else if (cls == 2) TRIALWD(64, 13, true, 2, 2); else TRIALW(64, 26, 1, true, 1);
   } else {
-    if (R == 4) TRIALW(4, false); else if (R == 7) TRIALW(7, false); else if (R == 13) TRIALW(13, false); else TRIALW(26, false);
+    if (cls == 0) TRIALWD(64, 4, false, 4, 3); else if (cls == 1) TRIALWD(64, 7, false, 3, 2);
+    else if (cls == 2) TRIALWD(64, 13, false, 2, 2); else TRIALW(64, 26, 1, false, 1);
   }
+#undef TRIALWD
 #undef TRIALW
   tl.done();
   int rc = check_launch(ctx, what);

@@ -57,7 +57,7 @@ def is_breakdown(sumsq: float, maxabs: float) -> bool:
 
 
 FUSE_KMAX_NARROW = 24               # k_gemv_vjpg: a point's basis row in VGPRs
-FUSE_KMAX_WIDE = 208                # k_trial_w: 64-point tiles of the basis through LDS (N % 64 == 0, no segments)
+FUSE_KMAX_WIDE = 208                # k_trial_w: tiles of the basis through LDS (N % 128 == 0, no segments)
 
 
 class DeviceKrylovBasis:
@@ -69,7 +69,7 @@ class DeviceKrylovBasis:
         self.kmax = int(kmax)
         # columns the first-trial kernel with the update products covers (gnk_basis_gemv_vjp_gemv_t*): the
         # narrow register kernel up to 24, the wide LDS kernel beyond when the grid allows it
-        wide = dev.slab.N % 64 == 0 and not getattr(dev, "seg_rows", 0)
+        wide = dev.slab.N % 128 == 0 and not getattr(dev, "seg_rows", 0)
         self.FUSE_KMAX = FUSE_KMAX_WIDE if wide else FUSE_KMAX_NARROW
         self.V = self.be.zeros(self.kmax, dev.slab.length)
         self.k = 0                       # settled columns

@@ -88,7 +88,9 @@ int64_t gnk_segment_fallbacks(const gnk_ctx* ctx);
  *                        that wide bases with segments need; the same bits)
  *   GNK_TUNE_DECOMP_LDS  > 0: bytes of extra dynamic LDS per workgroup of the persistent kernels (first trial,
  *                        pending column, marching Gram, CG normal matvec): fewer resident workgroups, the same
- *                        grid -- tests that no result depends on occupancy (the same bits) */
+ *                        grid -- tests that no result depends on occupancy (the same bits)
+ *   GNK_TUNE_TRIALW      16 * depth + workgroups per CU of the wide fused first trial (tooling A/B; the grid is
+ *                        its reduction decomposition, so a different per-CU count changes h's last bits) */
 #define GNK_TUNE_GRAM_PATH 0
 #define GNK_TUNE_GRAM_RING 1
 #define GNK_TUNE_GRAM_V1MIN 2
@@ -99,7 +101,8 @@ int64_t gnk_segment_fallbacks(const gnk_ctx* ctx);
 #define GNK_TUNE_LLS 7
 #define GNK_TUNE_VJPG_ZMAX 8
 #define GNK_TUNE_DECOMP_LDS 9
-#define GNK_TUNE_COUNT 10
+#define GNK_TUNE_TRIALW 10
+#define GNK_TUNE_COUNT 11
 int gnk_set_tuning(gnk_ctx* ctx, int key, int value);
 /* doubles in the context's scratch arena (bounds the wide generic Gram: kp * m <= this) */
 int64_t gnk_scratch_doubles(void);
@@ -144,9 +147,9 @@ int gnk_vjp_gemv_t(gnk_ctx* ctx, const double* u, const double* r,
 /* Fused first Armijo trial + basis-update products (version "res_old"): x = V[:, :k] @ c on
  * the whole slab (rounding of gnk_basis_gemv), then on owned rows g = -(J(x)^T r) and
  * h = V[:, :k]^T g -- gnk_basis_gemv followed by gnk_vjp_gemv_t(u = x) from one read of V.
- * 1 <= k <= 24 (a point's basis row in VGPRs); 25 <= k <= 208 when N % 64 == 0, ldv is even and
- * segments are off (64-point tiles of V through LDS; x and w then sum the columns in four blocked
- * quarters, not in one sequence).   ref:krylow.py:42, :62, :64 + gauss_newton_krylow.py:91,115 */
+ * 1 <= k <= 24 (a point's basis row in VGPRs); 25 <= k <= 208 when N % 128 == 0, ldv is even and
+ * segments are off (tiles of V through LDS; x and w then sum the columns in four blocked quarters,
+ * not in one sequence).   ref:krylow.py:42, :62, :64 + gauss_newton_krylow.py:91,115 */
 int gnk_basis_gemv_vjp_gemv_t(gnk_ctx* ctx, const double* V, int64_t ldv, int k, const double* c, const double* r,
                               double* x, double* g, double* h_out);
 
