@@ -667,14 +667,17 @@ def main():
                        "trial": {**twindow, "launch_bytes": t_by}}, f)
     gram_share = sum(g_ms) * 1e-3 / elapsed_all if g_ms else float("nan")
     # per basis size: columns = bytes / (8 n_rank) - 2 (V, u, r); kernel as gnk_gram dispatches a pass
-    # with P^-1 and r: VALU k <= 9 (one point per lane from 8), staged k <= 20 (N % 128 == 0), chunked
+    # with P^-1 and r: VALU k <= 7, staged on 4x4x4 blocks k = 8..20 (N % 128 == 0; else VALU one point per lane
+    # at 8, 9), chunked
     # k_gram_w up to 31 columns (+ r), the marching k_gram_x for 3..7 column blocks (N % 32 == 0; else the
     # chunked k_gram_w at 3 blocks and the prefetching k_gram_wp at 4), the pair-split k_gram beyond
     def gram_kernel(kk):
-        if kk <= 9:
-            return "k_gram_v" if kk <= 7 else "k_gram_v1"
+        if kk <= 7:
+            return "k_gram_v"
         if kk <= 20 and N % 128 == 0:
-            return "k_gram_s"
+            return "k_gram_q"                  # the 4x4x4-block staged pass (k_gram_s with GNK_TUNE_GRAM_Q 1)
+        if kk <= 9:
+            return "k_gram_v1"
         if kk + 1 <= 32:
             return "k_gram_w"
         if (kk + 16) // 16 <= 7 and N % 32 == 0:
@@ -745,8 +748,8 @@ def main():
                    # reductions of the timed steps that ran unsegmented while segments were on (wide Gram
                    # passes): 0 = the timed steps' bits do not depend on the rank count
                    "segment_fallbacks": int(fallbacks)},
-        "roofline": {"kernel": "Gram pass of the CholeskyQR solve, J V T on the fly (k_gram_v: VALU, k <= 9; "
-                               "k_gram_s: staged fp64 MFMA, k > 9)", "bound": "hbm",
+        "roofline": {"kernel": "Gram pass of the CholeskyQR solve, J V T on the fly (k_gram_v: VALU, k <= 7; "
+                               "k_gram_q: staged, 4x4x4 fp64 MFMA blocks, k >= 8)", "bound": "hbm",
                      "achieved": g_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": g_gbs / HBM_PEAK_GBS,
                      "traffic": traffic, "traffic_source": traffic_src,
                      "traffic_over_algorithmic": (traffic / g_avg_bytes) if traffic else None, "window": window,

@@ -22,7 +22,7 @@ TIMER_GRAM, TIMER_JVP, TIMER_CG_MATVEC, TIMER_TRIAL, TIMER_PROBE, TIMER_CG_XR, T
 ABI_VERSION = 6  # GNK_ABI_VERSION
 # GNK_TUNE_* keys of gnk_set_tuning (tests / A/B tooling only; the solver never sets them)
 TUNE = {"gram_path": 0, "gram_ring": 1, "gram_v1min": 2, "cg_matvec": 3, "vjpg_blocks": 4, "gram_wide": 5, "gram_rpr": 6, "lls": 7, "vjpg_zmax": 8,
-        "decomp_lds": 9, "trialw": 10}
+        "decomp_lds": 9, "trialw": 10, "gram_tm": 11, "gram_q": 12}
 
 _c_int, _c_i64, _c_dbl, _c_vp = ctypes.c_int, ctypes.c_int64, ctypes.c_double, ctypes.c_void_p
 

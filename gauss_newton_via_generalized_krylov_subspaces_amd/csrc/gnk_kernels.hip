@@ -2779,6 +2779,8 @@ __global__ __launch_bounds__(BLOCK) void k_gram_m(const double* __restrict__ u, 
 // and blocks in a fixed order, like the MFMA tile.
 constexpr int GS_SW = 128;
 constexpr int GS_NW = 8;
+constexpr int GS_TM_MIN = 3;    // first tail (k - 16) whose lead-column sums run on 4x4x4 MFMA (k_gram_s TM)
+constexpr int GQ_KMIN = 8;      // first k of the 4x4x4-block staged Gram (k_gram_q)
 constexpr int GS_KMAX = 20;     // V columns the staged kernel covers (k 21..24 would fit the LDS
                                 // ring but the two-block instance then spills past 256 VGPRs)
 
@@ -2819,15 +2821,21 @@ constexpr int gs_ss(int R) { return R == 4 ? 132 : 144; }
 // 0 .. TAIL-1 (Y there needs only the first 4-column k-step of the triangular transform: 1 MFMA),
 // block 1 = the 16 main columns TAIL .. TAIL+15 (every k-step: 5 MFMAs) -- 6 transform MFMAs per
 // row step instead of 9 with the 16 columns first (whose 4-column remainder needs all 5 k-steps too).
-// The MFMA Gram tile is the main block; the lead columns' sums run on VALU (row_newbcast).
-template <int NB, int L, int KSL, int TAIL, int R, int WPE>
+// The MFMA Gram tile is the main block; the lead columns' sums run on VALU (row_newbcast), or with TM on
+// 4x4x4 f64 MFMA blocks (v_mfma_f64_4x4x4_4b: the 16x16 C/D layout of Y -- lane 16p + c: point p, column c --
+// is that instruction's B layout with block c >> 2, and its A layout once the lead block's RinvAug fragment
+// repeats the lead columns in every 4-lane group; tools/probes/mfma44.hip): lead x main in 4 MFMAs per step,
+// lead x lead in one (the four point groups as the four blocks, summed in the scatter).
+template <int NB, int L, int KSL, int TAIL, int R, int WPE, bool TM = false>
 __global__ __launch_bounds__(64 * GS_NW) __attribute__((amdgpu_waves_per_eu(WPE))) void k_gram_s(const double* __restrict__ u, const double* __restrict__ V,
                                                        int64_t ldv, int k, const double* __restrict__ rinv,
                                                        int ldr, const double* __restrict__ r, Geo geo, Coef cf,
                                                        int64_t rpr, double* __restrict__ partial, int plog) {
-  constexpr int NACC = gs_nacc(NB, KSL);
-  constexpr int TMAX = NB == 2 ? 4 * KSL : 0;             // tail accumulator slots of this instance
+  constexpr bool TMF = NB == 2 && TM;                     // lead columns' sums on 4x4x4 MFMA
+  constexpr int NACC = TMF ? NB + 3 : gs_nacc(NB, KSL);
+  constexpr int TMAX = NB == 2 && !TMF ? 4 * KSL : 0;     // VALU tail accumulator slots of this instance
   constexpr int ER = NB * TMAX, RR = ER + NB;             // accumulator slots of r . Y and r . r
+  constexpr int QLM = RR + 1, QLL = RR + 2;               // TMF: lead x main / lead x lead (4x4x4 D layouts)
   constexpr int SS = gs_ss(R);                            // slot stride (doubles)
   extern __shared__ __attribute__((aligned(16))) double lds[];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -2859,8 +2867,11 @@ __global__ __launch_bounds__(64 * GS_NW) __attribute__((amdgpu_waves_per_eu(WPE)
 #pragma unroll
       for (int ks = 0; ks < nkt(cb, ab); ++ks) {
         const int row = ab * 16 + ks * 4 + (lane >> 4);
-        if (NB == 2)   // lead block: columns 0 .. TAIL-1 (the rest of its tile 0); main: TAIL + cl
-          rB[cb][ab][ks] = cb == 0 ? (cl < TAIL ? rinv[row * ldr + cl] : 0.0) : rinv[row * ldr + TAIL + cl];
+        // lead block: columns 0 .. TAIL-1 (the rest of its tile 0; TMF: repeated in every 4-lane group);
+        // main: TAIL + cl
+        const int lc = TMF ? (cl & 3) : cl;
+        if (NB == 2)
+          rB[cb][ab][ks] = cb == 0 ? (lc < TAIL ? rinv[row * ldr + lc] : 0.0) : rinv[row * ldr + TAIL + cl];
         else
           rB[cb][ab][ks] = rinv[row * ldr + cl];
         // opaque use: the load retires here, before the first DMA (a VGPR load still counted
@@ -2982,10 +2993,18 @@ __global__ __launch_bounds__(64 * GS_NW) __attribute__((amdgpu_waves_per_eu(WPE)
   // H[cb][i] = Y[16w + (l>>4) + 4i][col(cb) + (l&15)] (col: 0 for NB = 1; 0 / TAIL for the lead / main
   // block of NB = 2): the MFMA operand of rows 4i..4i+3, and for the VALU part this lane's column at
   // point p = 16w + (l>>4) + 4i
+  const int zb = (lane >> 2) & 3;                   // TMF: this lane's 4x4x4 block
   auto gram = [&](const d4 (&Y)[NB], const double* Lr) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) acc = mfma64(Y[NB - 1][i], Y[NB - 1][i], acc);
-    if (NB == 2) {
+    if constexpr (TMF) {
+      // lead x main: block b = main columns 4b..4b+3, A = the lead columns (repeated), k = the 4 points of group i
+#pragma unroll
+      for (int i = 0; i < 4; ++i) ev[QLM] = __builtin_amdgcn_mfma_f64_4x4x4f64(Y[0][i], Y[NB - 1][i], ev[QLM], 0, 0, 0);
+      // lead x lead: block b takes point group b (lane 16p + 4b + c holds Y[p + 4b][c])
+      const double z = zb == 0 ? Y[0][0] : zb == 1 ? Y[0][1] : zb == 2 ? Y[0][2] : Y[0][3];
+      ev[QLL] = __builtin_amdgcn_mfma_f64_4x4x4f64(z, z, ev[QLL], 0, 0, 0);
+    } else if (NB == 2) {
 #pragma unroll
       for (int t = 0; t < TAIL; ++t) {
 #pragma unroll
@@ -3121,8 +3140,265 @@ __global__ __launch_bounds__(64 * GS_NW) __attribute__((amdgpu_waves_per_eu(WPE)
     } else {
       const int ln = (t - 256) / NACC, q = (t - 256) % NACC, col = ln & 15;
       const double* e = red + 256 + q;
-      out[t] = (ln >> 4) ? 0.0 : ((e[col * NACC] + e[(16 + col) * NACC]) + e[(32 + col) * NACC]) + e[(48 + col) * NACC];
+      if (TMF && q == QLM) {       // lead x main (4x4x4 D layout): every lane its own entry
+        out[t] = red[t];
+      } else if (TMF && q == QLL) {  // lead x lead: the four point-group blocks summed here, into block 0
+        const int bl = (ln >> 2) & 3, l0 = ln - 4 * bl;
+        out[t] = bl ? 0.0 : ((e[l0 * NACC] + e[(l0 + 4) * NACC]) + e[(l0 + 8) * NACC]) + e[(l0 + 12) * NACC];
+      } else
+        out[t] = (ln >> 4) ? 0.0 : ((e[col * NACC] + e[(16 + col) * NACC]) + e[(32 + col) * NACC]) + e[(48 + col) * NACC];
     }
+  }
+}
+
+// ---------------------------------------------------------------- staged Gram pass on 4x4x4 f64 MFMA blocks
+// k_gram_s's ring, LDS-DMA pipeline and A fragments, with the transform and the Gram at 4-column granularity on
+// v_mfma_f64_4x4x4_4b (512 flops in ~19 cycles: the 16x16x4 form's rate; tools/probes/mfma44.hip maps its
+// layouts -- A / B lane 16 k + 4 b + i, D lane 16 i + 4 b + j, b the block).  A stencil fragment of column group
+// a (lane 16 q + p: point p = 4 b + i, column 4 a + q) is that instruction's A operand with the four point groups
+// as the four blocks, so
+//   transform: Y_c = sum_{a <= c} W_a R_ac   -- one 4x4x4 MFMA per (a <= c): the triangle at 4-column granularity,
+//              D lane 16 i + 4 b + j = Y[point 4 b + i][column 4 c + j];
+//   Gram:      G_cd += Y_c^T Y_d (c <= d)    -- Y_c's D layout read as A is Y_c^T and as B is Y_d, blocks = point
+//              groups: one MFMA per group pair, each block a 4-point partial (summed per workgroup below).
+// For NG groups that is NG (NG + 1) MFMAs of 19 cycles per 16-point row step, against (transform k-steps + 4)
+// 16x16x4 MFMAs of 64 cycles in k_gram_s, with no padding beyond the last 4-column group and no lead/tail split.
+// r stays on VALU (r . Y per lane column, r . r).  Per workgroup the lane partials are summed over the point
+// groups (and over the points, for r) in a fixed order before any reduction over workgroups, segments or ranks;
+// partial[tile][16 NP + 4 NG + 1] holds the group-pair 4x4 blocks, r . Y and r . r (k_gram_scatter_q).
+constexpr int gq_np(int ng) { return ng * (ng + 1) / 2; }
+constexpr int gq_pl(int ng) { return 16 * gq_np(ng) + 4 * ng + 1; }
+__host__ __device__ constexpr int gq_pair(int a, int c) { return c * (c + 1) / 2 + a; }   // a <= c
+
+template <int NG, int L, int R, int WPE>
+__global__ __launch_bounds__(64 * GS_NW) __attribute__((amdgpu_waves_per_eu(WPE))) void k_gram_q(
+    const double* __restrict__ u, const double* __restrict__ V, int64_t ldv, int k, const double* __restrict__ rinv,
+    int ldr, const double* __restrict__ r, Geo geo, Coef cf, int64_t rpr, double* __restrict__ partial, int plog) {
+  constexpr int NP = gq_np(NG);
+  constexpr int NACC = NP + NG + 1;                 // lane slots: group pairs, r . Y_c, r . r
+  constexpr int SS = gs_ss(R);
+  constexpr bool EB = R == 4;
+  extern __shared__ __attribute__((aligned(16))) double lds[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int64_t N = geo.N;
+  const int nrow = k + 1 + (r ? 1 : 0);             // ring rows: V_0..V_{k-1}, u, (r)
+  const int QS = R * SS;
+  const int ninst = nrow + 1;
+
+  const int nstrips = int(N / GS_SW);
+  const int nwg = gridDim.x, b = blockIdx.x;
+  const int idx = (nwg % 8 == 0) ? (b % 8) * (nwg / 8) + b / 8 : b;
+  const int64_t x0 = int64_t(idx / nstrips) * rpr;
+  const int64_t x1 = min(geo.nrows, x0 + rpr);
+  const int64_t col0 = int64_t(idx % nstrips) * GS_SW;
+
+  // RinvAug B fragments R_ac (a <= c): lane 16 q + 4 b + j -> RinvAug[4 a + q][4 c + j], every block the same
+  double rq[NP];
+#pragma unroll
+  for (int c = 0; c < NG; ++c)
+#pragma unroll
+    for (int a = 0; a <= c; ++a) {
+      rq[gq_pair(a, c)] = rinv[(4 * a + (lane >> 4)) * ldr + 4 * c + (lane & 3)];
+      asm volatile("" : "+v"(rq[gq_pair(a, c)]));   // retired before the first DMA (see k_gram_s)
+    }
+  double acc[NP], er[NG], err = 0.0;
+#pragma unroll
+  for (int p = 0; p < NP; ++p) acc[p] = 0.0;
+#pragma unroll
+  for (int c = 0; c < NG; ++c) er[c] = 0.0;
+
+  const double* dsrc[L];
+  int ddst[L];
+  bool isu[L];
+#pragma unroll
+  for (int m = 0; m < L; ++m) {
+    int q = wave + GS_NW * m;
+    if (q >= ninst) q = k;
+    isu[m] = q == k;
+    if (q < nrow) {
+      const double* rowp = q < k ? V + int64_t(q) * ldv : (q == k ? u : r);
+      dsrc[m] = rowp + col0 + 2 * lane;
+    } else {
+      const int cc = min(lane >> 1, k - 1);
+      const int64_t off = (lane & 1) ? (col0 + GS_SW < N ? col0 + GS_SW : col0 + GS_SW - 2) : (col0 > 0 ? col0 - 2 : 0);
+      dsrc[m] = V + int64_t(cc) * ldv + off;
+    }
+    ddst[m] = q * QS;
+  }
+  const int64_t rmax = geo.nrows + G - 1;
+  auto issue_row = [&](int64_t xr, int slot) {
+    const int64_t roff = (G + min(xr, rmax)) * N;
+    const int64_t roffu = (G + min(xr + (EB ? 3 : 0), rmax)) * N;
+    double* sbase = lds + slot * SS;
+#pragma unroll
+    for (int m = 0; m < L; ++m)
+      __builtin_amdgcn_global_load_lds((glb_cvp)(dsrc[m] + (isu[m] ? roffu : roff)), (lds_vp)(sbase + ddst[m]), 16,
+                                       0, 0);
+  };
+
+  // stencil offsets of column group g (column 4 g + l>>4, point e), slot 0
+  const int e = wave * 16 + (lane & 15);
+  const int cq = lane >> 4;
+  const double cwm = (col0 + e > 0) ? cf.hm2 : 0.0;
+  const double cem = (col0 + e + 1 < N) ? cf.hm2 : 0.0;
+  const double up = -cf.j_lin_up;
+  const int hq = nrow * QS;
+  int fo[NG], fw[NG], fe[NG];
+  const bool lastv = 4 * (NG - 1) + cq < k;         // the last group's column is a V column (else padding)
+#pragma unroll
+  for (int g = 0; g < NG; ++g) {
+    const int j = 4 * g + cq;
+    const int jr = j < k ? j : 0;
+    fo[g] = jr * QS + e;
+    fw[g] = e > 0 ? jr * QS + e - 1 : hq + 4 * jr + 1;
+    fe[g] = e < GS_SW - 1 ? jr * QS + e + 1 : hq + 4 * jr + 2;
+  }
+  const int ou = k * QS + e;
+  // r at this lane's point in the D layout (lane 16 i + 4 b + j: point 4 b + i)
+  const int orq = (k + 1) * QS + wave * 16 + 4 * ((lane >> 2) & 3) + (lane >> 4);
+
+  auto stencil = [&](const double* Ln, const double* Lc, const double* Ls, double dn, double (&a)[NG]) {
+#pragma unroll
+    for (int g = 0; g < NG; ++g) {
+      const int o = fo[g];
+      const double vn = Ln[o], vw = Lc[fw[g]], vc = Lc[o], ve = Lc[fe[g]], vs = Ls[o];
+      double sv;
+      if (g == NG - 1) {           // only the last group can hold padding columns (coefficients 0)
+        const double cn = lastv ? cf.hm2 : 0.0, cw = lastv ? cwm : 0.0, cc = lastv ? dn : 0.0;
+        const double ce = lastv ? cem : 0.0, cs = lastv ? up : 0.0;
+        sv = cn * vn;
+        sv = fma(cw, vw, sv);
+        sv = fma(cc, vc, sv);
+        sv = fma(ce, ve, sv);
+        sv = fma(cs, vs, sv);
+      } else {
+        sv = cf.hm2 * vn;
+        sv = fma(cwm, vw, sv);
+        sv = fma(dn, vc, sv);
+        sv = fma(cem, ve, sv);
+        sv = fma(up, vs, sv);
+      }
+      a[g] = sv;
+    }
+  };
+  auto transform = [&](const double (&a)[NG], double (&Y)[NG]) {
+#pragma unroll
+    for (int c = 0; c < NG; ++c) {
+      double h = 0.0;
+#pragma unroll
+      for (int aa = 0; aa <= c; ++aa) h = __builtin_amdgcn_mfma_f64_4x4x4f64(a[aa], rq[gq_pair(aa, c)], h, 0, 0, 0);
+      Y[c] = h;
+    }
+  };
+  auto gram = [&](const double (&Y)[NG], const double* Lr) {
+#pragma unroll
+    for (int d = 0; d < NG; ++d)
+#pragma unroll
+      for (int c = 0; c <= d; ++c)
+        acc[gq_pair(c, d)] = __builtin_amdgcn_mfma_f64_4x4x4f64(Y[c], Y[d], acc[gq_pair(c, d)], 0, 0, 0);
+    if (r) {
+      const double rv = Lr[orq];
+#pragma unroll
+      for (int c = 0; c < NG; ++c) er[c] = fma(rv, Y[c], er[c]);
+      err = fma(rv, rv, err);
+    }
+  };
+
+  constexpr int INF = R - 4;
+  if (x0 < x1) {
+    double dn0 = 0.0, dnb = 0.0;
+    if (EB) {
+      const int64_t i0 = (G + x0) * N + col0 + e;
+      double ua = u[i0], ub = u[i0 + N];
+      asm volatile("" : "+v"(ua), "+v"(ub));
+      dn0 = -jdiag(cf, ua);
+      dnb = -jdiag(cf, ub);
+    }
+#pragma unroll
+    for (int s = 0; s < R; ++s) issue_row(x0 - 1 + s, s);
+    __builtin_amdgcn_s_waitcnt(waitcnt_vm_lgkm0(L * (INF + 1)));
+    __builtin_amdgcn_s_barrier();
+    double Y[NG];
+    {
+      double a[NG];
+      stencil(lds, lds + SS, lds + 2 * SS, EB ? dn0 : -jdiag(cf, lds[SS + ou]), a);
+      transform(a, Y);
+    }
+    double dn = EB ? 0.0 : -jdiag(cf, lds[2 * SS + ou]);
+    __builtin_amdgcn_s_waitcnt(waitcnt_vm_lgkm0(L * INF));
+    __builtin_amdgcn_s_barrier();
+    for (int64_t xb = x0; xb < x1; xb += R) {
+#pragma unroll
+      for (int st = 0; st < R; ++st) {
+        const int64_t x = xb + st;
+        if (x >= x1) break;
+        if (EB) {
+          if (st == 0) {
+            dn = __shfl(dnb, 48 + (lane & 15));
+            const int sg = (st + cq) % R;
+            double ug = lds[sg * SS + ou];
+            asm volatile("" : "+v"(ug));
+            __builtin_amdgcn_s_barrier();
+            dnb = -jdiag(cf, ug);
+          } else {
+            dn = __shfl(dnb, (st - 1) * 16 + (lane & 15));
+          }
+        }
+        issue_row(x + R - 1, st);
+        const double* Lx = lds + ((st + 1) % R) * SS;
+        const double* Lx1 = lds + ((st + 2) % R) * SS;
+        const double* Lx2 = lds + ((st + 3) % R) * SS;
+        gram(Y, Lx);
+        if (x + 1 < x1) {
+          double a[NG];
+          stencil(Lx, Lx1, Lx2, dn, a);
+          transform(a, Y);
+          if (!EB) dn = -jdiag(cf, Lx2[ou]);
+        }
+        __builtin_amdgcn_s_waitcnt(waitcnt_vm_lgkm0(L * INF));
+        __builtin_amdgcn_s_barrier();
+      }
+    }
+  }
+  __builtin_amdgcn_s_waitcnt(waitcnt_vm_lgkm0(0));
+  __builtin_amdgcn_s_barrier();
+
+  // waves summed in order through LDS ([lane * NACC + slot]), then per workgroup: each group pair's 4x4 block
+  // over the four point groups ((b0 + b1) + b2) + b3, r . Y_c's column j and r . r over the 16 points (i, b)
+  double* red = lds;
+  for (int w = 0; w < GS_NW; ++w) {
+    if (wave == w) {
+#pragma unroll
+      for (int q = 0; q < NP; ++q) {
+        double* dst = red + lane * NACC + q;
+        *dst = (w == 0) ? acc[q] : *dst + acc[q];
+      }
+#pragma unroll
+      for (int c = 0; c < NG; ++c) {
+        double* dst = red + lane * NACC + NP + c;
+        *dst = (w == 0) ? er[c] : *dst + er[c];
+      }
+      double* dst = red + lane * NACC + NP + NG;
+      *dst = (w == 0) ? err : *dst + err;
+    }
+    __syncthreads();
+  }
+  constexpr int PL = gq_pl(NG);
+  double* out = partial + size_t(plog ? idx : b) * PL;
+  for (int t = tid; t < PL; t += blockDim.x) {
+    double v = 0.0;
+    if (t < 16 * NP) {
+      const int p = t >> 4, i = (t >> 2) & 3, j = t & 3;
+      const double* e0 = red + (16 * i + j) * NACC + p;
+      v = ((e0[0] + e0[4 * NACC]) + e0[8 * NACC]) + e0[12 * NACC];
+    } else {
+      const int c = (t - 16 * NP) >> 2, j = (t - 16 * NP) & 3;   // c == NG: r . r (lanes j = 0)
+      const int q = c < NG ? NP + c : NP + NG;
+      for (int i = 0; i < 4; ++i)
+        for (int bb = 0; bb < 4; ++bb) v += red[(16 * i + 4 * bb + (c < NG ? j : 0)) * NACC + q];
+    }
+    out[t] = v;
   }
 }
 
@@ -3339,10 +3615,10 @@ __global__ __launch_bounds__(64) void k_gram_scatter_v(const double* __restrict_
 // first, k_gram_s): the VALU sums hold the tail = k - 16 lead columns, the MFMA tile columns
 // tail..tail+15; then G[k][c], G[k][k] from the r sums.
 __global__ __launch_bounds__(BLOCK) void k_gram_scatter_s(const double* __restrict__ red, int nb, int nacc, int k,
-                                                          int has_r, int KP, double* __restrict__ Gout) {
+                                                          int has_r, int KP, int tm, double* __restrict__ Gout) {
   const int tail = nb == 2 ? k - 16 : 0;
   const int c0 = tail;                               // first column of the MFMA tile
-  const int er = nb == 1 ? 0 : nacc - 3, rr = er + nb;
+  const int er = nb == 1 || tm ? 0 : nacc - 3, rr = er + nb;
   const double* ev = red + 256;
   auto lsum = [&](int col_in_block, int q) {
     double s = 0.0;
@@ -3371,7 +3647,13 @@ __global__ __launch_bounds__(BLOCK) void k_gram_scatter_s(const double* __restri
       // lead = 0: columns c <= 16 + t of row 16 + t;  lead = 1: columns c <= t and the 16 main ones
       const bool want = c0 ? (c <= t || (c >= c0 && c < c0 + 16)) : (c <= 16 + t);
       if (t < tail && want && c < k) {
-        const double v = lsum(cin(c), t * nb + blk(c));
+        // tm: lead x main at lane 16t + (c - c0) of slot rr + 1; lead x lead at lanes 16t + 4b + c of slot
+        // rr + 2, the four point-group blocks b summed in order
+        const double* e = red + 256;
+        const double v = !tm ? lsum(cin(c), t * nb + blk(c))
+                         : c >= c0 ? e[(16 * t + c - c0) * nacc + rr + 1]
+                                   : ((e[(16 * t + c) * nacc + rr + 2] + e[(16 * t + 4 + c) * nacc + rr + 2]) +
+                                      e[(16 * t + 8 + c) * nacc + rr + 2]) + e[(16 * t + 12 + c) * nacc + rr + 2];
         Gout[trow * KP + c] = v;
         Gout[c * KP + trow] = v;
       }
@@ -3385,6 +3667,28 @@ __global__ __launch_bounds__(BLOCK) void k_gram_scatter_s(const double* __restri
         Gout[k * KP + k] = lsum(0, rr);
       }
     }
+  }
+}
+
+// G from k_gram_q's reduced partial (gq_pl layout): V-column entries from the group-pair blocks, then r . Y, r . r;
+// zero outside [0, k + has_r)^2
+__global__ __launch_bounds__(BLOCK) void k_gram_scatter_q(const double* __restrict__ red, int ng, int k, int has_r,
+                                                          int KP, double* __restrict__ Gout) {
+  const int np = ng * (ng + 1) / 2;
+  const int K1 = k + has_r;
+  for (int idx = blockIdx.x * BLOCK + threadIdx.x; idx < KP * KP; idx += gridDim.x * BLOCK) {
+    const int a = idx / KP, c = idx % KP;
+    double v = 0.0;
+    if (a < K1 && c < K1) {
+      const int lo = min(a, c), hi = max(a, c);
+      if (hi < k)            // group pair (lo / 4, hi / 4), entry (lo % 4, hi % 4): one value for both triangles
+        v = red[16 * gq_pair(lo >> 2, hi >> 2) + 4 * (lo & 3) + (hi & 3)];
+      else if (lo < k)       // r . Y_lo
+        v = red[16 * np + lo];
+      else                   // r . r
+        v = red[16 * np + 4 * ng];
+    }
+    Gout[idx] = v;
   }
 }
 
@@ -4788,7 +5092,11 @@ int gnk_gram(gnk_ctx* ctx, const double* u, const double* V, int64_t ldv, int k,
   // 3 disables it, 1 (tests) forces the staged kernel instead
   const int path = tuning(ctx, GNK_TUNE_GRAM_PATH);
   const int v1t = tuning(ctx, GNK_TUNE_GRAM_V1MIN);          // tooling A/B: first k of the one-point form
-  const int gv_kmax = v1t < 0 ? GV1_KMIN - 1 : GV_KMAX;
+  int gv_kmax = v1t < 0 ? GV1_KMIN - 1 : GV_KMAX;
+  // preconditioned passes: from GQ_KMIN the 4x4x4-block staged pass (k_gram_q) beats the one-point VALU kernel
+  // (k = 8 / 9: 1.06 / 1.22-1.25 vs 1.19 / 1.32 ms, profiles/round6/gram_q_small_ab.jsonl)
+  const int q_t = tuning(ctx, GNK_TUNE_GRAM_Q);
+  if (rinv && q_t != 1 && v1t == 0 && path != 2 && ctx->geo.N % GS_SW == 0) gv_kmax = std::min(gv_kmax, GQ_KMIN - 1);
   if (r && k <= gv_kmax && ctx->geo.N % GV_SW == 0 && path != 3 && path != 1) {
     const double* tv = rinv ? rinv : ctx->ident + ident_offset(KP / 16);
     const int v1min = v1t > 0 ? std::max(7, v1t) : GV1_KMIN;
@@ -4880,8 +5188,20 @@ int gnk_gram(gnk_ctx* ctx, const double* u, const double* V, int64_t ldv, int k,
       const double* rv = rinv ? rinv : ctx->ident + ident_offset(KP / 16);
       // 4-column k-steps of the last transform block
       const int ksl = ((k - 16 * (nbs - 1)) + 3) / 4;
-      const int nacc = gs_nacc(nbs, ksl);
-      const int PL = 256 + 64 * nacc;
+      // two blocks, 5-slot ring: the lead columns' sums on 4x4x4 MFMA for tails of >= GS_TM_MIN columns
+      // (GNK_TUNE_GRAM_TM 1: never, 2: every tail)
+      const int tm_t = tuning(ctx, GNK_TUNE_GRAM_TM);
+      const int tm = nbs == 2 && ring == 5 && tm_t != 1 && (tm_t == 2 || k - 16 >= GS_TM_MIN) ? 1 : 0;
+      const int nacc = tm ? nbs + 3 : gs_nacc(nbs, ksl);
+      // the 4x4x4-block form (k_gram_q) for k >= GQ_KMIN: NG = ceil(k / 4) column groups, the ring depth chosen
+      // above (4 slots up to 16 columns, 5 above); GNK_TUNE_GRAM_Q 1: never, 2: from k = 5 (k = 5..7 measured
+      // 1.03-1.08 ms against the VALU kernel's 0.66-0.87)
+      const int ng = (k + 3) / 4;
+      const bool qinst = (ng == 2 && L <= 2) || (ng == 3 && L == 2) || (ng == 4 && (L == 2 || L == 3)) ||
+                         (ng == 5 && L == 3);
+      const bool useq = q_t != 1 && k >= (q_t == 2 ? 5 : GQ_KMIN) && qinst &&
+                        (ng == 5 || ring == 4);
+      const int PL = useq ? gq_pl(ng) : 256 + 64 * nacc;
       const int wgpc = std::max(1, std::min(2, int((160 * 1024) / lds)));
       const int64_t nstrips = ctx->geo.N / GS_SW;
       const int64_t nrows = ctx->geo.nrows;
@@ -4909,10 +5229,13 @@ int gnk_gram(gnk_ctx* ctx, const double* u, const double* V, int64_t ldv, int k,
     else if (two_wg) GRAMS_RW(NBV, LV, KV, 0, 5, 4);                       \
     else GRAMS_RW(NBV, LV, KV, 0, 5, 2);                                   \
   } while (0)
-#define GRAMS_TR(LV, TV)                                                   \
-  do {                                                                     \
-    if (ring == 4) GRAMS_RW(2, LV, 1, TV, 4, 2);                           \
-    else GRAMS_RW(2, LV, 1, TV, 5, 2);                                     \
+#define GRAMS_TR(LV, TV)                                                                                      \
+  do {                                                                                                        \
+    if (ring == 4) GRAMS_RW(2, LV, 1, TV, 4, 2);                                                              \
+    else if (tm)                                                                                              \
+      hipLaunchKernelGGL((k_gram_s<2, LV, 1, TV, 5, 2, true>), dim3(unsigned(nwg)), dim3(64 * GS_NW), lds,      \
+                         ctx->stream, u, V, ldv, k, rv, KP, r, ctx->geo, ctx->coef, rpr, ctx->scratch, plog); \
+    else GRAMS_RW(2, LV, 1, TV, 5, 2);                                                                        \
   } while (0)
 #define GRAMS_T(LV)                                                                              \
   do {                                                                                           \
@@ -4924,11 +5247,22 @@ int gnk_gram(gnk_ctx* ctx, const double* u, const double* V, int64_t ldv, int k,
     if (ksl == 1) GRAMS(NBV, LV, 1); else if (ksl == 2) GRAMS(NBV, LV, 2);  \
     else if (ksl == 3) GRAMS(NBV, LV, 3); else GRAMS(NBV, LV, 4);           \
   } while (0)
-      if (nbs == 1) {
+#define GRAMQ(NGV, LV, RV, WV)                                                                                 \
+  hipLaunchKernelGGL((k_gram_q<NGV, LV, RV, WV>), dim3(unsigned(nwg)), dim3(64 * GS_NW), lds, ctx->stream, u, V, ldv, \
+                     k, rv, KP, r, ctx->geo, ctx->coef, rpr, ctx->scratch, plog)
+      if (useq) {
+        if (ng == 5) { if (ring == 5) GRAMQ(5, 3, 5, 2); else GRAMQ(5, 3, 4, 2); }
+        else if (ng == 2 && L == 1) { if (two_wg) GRAMQ(2, 1, 4, 4); else GRAMQ(2, 1, 4, 2); }
+        else if (ng == 2) { if (two_wg) GRAMQ(2, 2, 4, 4); else GRAMQ(2, 2, 4, 2); }
+        else if (ng == 3) { if (two_wg) GRAMQ(3, 2, 4, 4); else GRAMQ(3, 2, 4, 2); }
+        else if (L == 2) { if (two_wg) GRAMQ(4, 2, 4, 4); else GRAMQ(4, 2, 4, 2); }
+        else { if (two_wg) GRAMQ(4, 3, 4, 4); else GRAMQ(4, 3, 4, 2); }
+      } else if (nbs == 1) {
         if (L == 1) GRAMS_K(1, 1); else if (L == 2) GRAMS_K(1, 2); else if (L == 3) GRAMS_K(1, 3); else GRAMS_K(1, 4);
       } else {
         if (L == 3) GRAMS_T(3); else GRAMS_T(4);      // k = 17..20: one tail k-step, k - 16 tail columns
       }
+#undef GRAMQ
 #undef GRAMS_T
 #undef GRAMS_TR
 #undef GRAMS_K
@@ -4945,8 +5279,12 @@ int gnk_gram(gnk_ctx* ctx, const double* u, const double* V, int64_t ldv, int k,
         rcs = wreduce(ctx, ctx->scratch, int(nwg), PL, int64_t(PL), PL, 0, nullptr, red);
       }
       if (rcs) return rcs;
-      hipLaunchKernelGGL(k_gram_scatter_s, dim3(4), dim3(BLOCK), 0, ctx->stream, red, nbs, nacc, k, r ? 1 : 0, KP,
-                         G_out);
+      if (useq)
+        hipLaunchKernelGGL(k_gram_scatter_q, dim3((KP * KP + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, ctx->stream, red, ng,
+                           k, r ? 1 : 0, KP, G_out);
+      else
+        hipLaunchKernelGGL(k_gram_scatter_s, dim3(4), dim3(BLOCK), 0, ctx->stream, red, nbs, nacc, k, r ? 1 : 0, KP,
+                           tm, G_out);
       return check_launch(ctx, "gram scatter (staged)");
     }
   }

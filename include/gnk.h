@@ -90,7 +90,11 @@ int64_t gnk_segment_fallbacks(const gnk_ctx* ctx);
  *                        pending column, marching Gram, CG normal matvec): fewer resident workgroups, the same
  *                        grid -- tests that no result depends on occupancy (the same bits)
  *   GNK_TUNE_TRIALW      16 * depth + workgroups per CU of the wide fused first trial (tooling A/B; the grid is
- *                        its reduction decomposition, so a different per-CU count changes h's last bits) */
+ *                        its reduction decomposition, so a different per-CU count changes h's last bits)
+ *   GNK_TUNE_GRAM_TM     staged Gram, k = 17..20: 1 = the lead columns' sums on VALU for every tail, 2 = on 4x4x4
+ *                        f64 MFMA blocks for every tail (tooling A/B and tests; a different summation order)
+ *   GNK_TUNE_GRAM_Q      staged Gram: 1 = never the 4x4x4-block form (k_gram_q; k = 8, 9 then on the VALU kernel), 2 = from
+ *                        k = 5 (default: k >= 8) */
 #define GNK_TUNE_GRAM_PATH 0
 #define GNK_TUNE_GRAM_RING 1
 #define GNK_TUNE_GRAM_V1MIN 2
@@ -102,7 +106,9 @@ int64_t gnk_segment_fallbacks(const gnk_ctx* ctx);
 #define GNK_TUNE_VJPG_ZMAX 8
 #define GNK_TUNE_DECOMP_LDS 9
 #define GNK_TUNE_TRIALW 10
-#define GNK_TUNE_COUNT 11
+#define GNK_TUNE_GRAM_TM 11
+#define GNK_TUNE_GRAM_Q 12
+#define GNK_TUNE_COUNT 13
 int gnk_set_tuning(gnk_ctx* ctx, int key, int value);
 /* doubles in the context's scratch arena (bounds the wide generic Gram: kp * m <= this) */
 int64_t gnk_scratch_doubles(void);

@@ -275,23 +275,56 @@ GRAM_CASES = [(24, 1, False, False), (24, 5, True, True), (100, 20, False, False
                                                   (128, 70, True, False), (96, 90, False, False),
                                                   # pair-split k_gram, k >= 112 (C5's range on 8 GPUs)
                                                   (64, 112, True, True), (96, 150, True, False), (64, 200, True, True),
-                                                  (32, 130, False, False)]
-# "forced" / "ring5" only where the staged kernel applies (N % 128 == 0, k <= 20)
-GRAM_PARAMS = [(N, k, r, ri, st) for (N, k, r, ri) in GRAM_CASES
-               for st in (("default", "forced", "ring5") if N % 128 == 0 and k <= 20 else ("default",))]
+                                                  (32, 130, False, False),
+                                                  # two-block Gram at N % 128 != 0 (not the staged kernel), one
+                                                  # 128-point strip, without r
+                                                  (64, 17, True, True), (192, 20, True, True), (320, 18, False, False),
+                                                  (128, 19, False, True), (1024, 18, True, True)]
+
+
+def _staged_modes(N, k):
+    # "forced" / "ring5" only where the staged kernel applies (N % 128 == 0, k <= 20).  The 4x4x4-block form
+    # (k_gram_q) is the default from k = 8: "noq" runs k_gram_s there instead, "v1" the one-point VALU kernel at
+    # k = 8, 9, "valu" / "tm" k_gram_s's two lead-column forms at k = 17..20; "q" forces k_gram_q at k = 5..7
+    if N % 128 != 0 or k > 20:
+        return ("default",)
+    modes = ("default", "forced", "ring5")
+    if k >= 8:
+        modes += ("noq",)
+    if k in (8, 9):
+        modes += ("v1",)
+    if k >= 17:
+        modes += ("valu", "tm")
+    if 5 <= k <= 7:
+        modes += ("q",)
+    return modes
+
+
+GRAM_PARAMS = [(N, k, r, ri, st) for (N, k, r, ri) in GRAM_CASES for st in _staged_modes(N, k)]
 
 
 @pytest.mark.parametrize("N,k,with_r,with_rinv,staged", GRAM_PARAMS)
 def test_gram_mfma(N, k, with_r, with_rinv, staged):
     """W = [J V | r] @ RinvAug on fp64 MFMA vs an fp64 NumPy Gram (host BLAS).  "forced" runs
     the staged LDS-DMA kernel for every pass it supports (N % 128 == 0, k <= 20) with its default
-    4-slot ring (jdiag batched over 4 rows); "ring5" forces the 5-slot ring (one jdiag per row step)."""
+    4-slot ring (jdiag batched over 4 rows); "ring5" forces the 5-slot ring (one jdiag per row step); "noq" runs
+    k_gram_s instead of the 4x4x4-block k_gram_q (default from k = 8), "v1" the one-point VALU kernel at k = 8, 9,
+    "valu" / "tm" k_gram_s's lead columns' sums at k = 17..20 on VALU / on 4x4x4 blocks, "q" forces k_gram_q at
+    k = 5..7."""
     prob, dev, ref = make(N)
     be = dev.backend
-    if staged != "default":
+    if staged == "v1":
+        be.set_tuning("gram_q", 1)
+    elif staged != "default":
         be.set_tuning("gram_path", 1)
         if staged == "ring5":
             be.set_tuning("gram_ring", 5)
+        if staged in ("valu", "tm", "noq"):
+            be.set_tuning("gram_q", 1)
+        if staged in ("valu", "tm"):
+            be.set_tuning("gram_tm", 1 if staged == "valu" else 2)
+        if staged == "q":
+            be.set_tuning("gram_q", 2)
     rng = np.random.default_rng(N + k)
     n = N * N
     Vh = np.linalg.qr(rng.standard_normal((n, k)))[0].T.copy()

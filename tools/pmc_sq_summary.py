@@ -20,7 +20,7 @@ import re
 import sys
 from collections import defaultdict
 
-GRAM = re.compile(r"k_gram_(?:[smw]p?|v1?)<")
+GRAM = re.compile(r"k_gram_(?:[smwqx]p?|v1?)<")
 MIN_NS = 100e3                       # bench-grid Gram launches take >= 0.28 ms; the 256^2 pre-warm's a few us
 CTRS = ("SQ_INSTS_VALU", "SQ_INSTS_MFMA", "SQ_VALU_MFMA_BUSY_CYCLES", "SQ_BUSY_CYCLES", "SQ_WAIT_INST_ANY",
         "SQ_WAVE_CYCLES", "SQ_INSTS_LDS", "GRBM_GUI_ACTIVE")

@@ -19,7 +19,7 @@ import re
 import sys
 from collections import defaultdict
 
-GRAM = re.compile(r"k_gram_(?:[smw]p?|v1?)<")    # every Gram-pass kernel (staged / marching / chunked / VALU)
+GRAM = re.compile(r"k_gram_(?:[smwqx]p?|v1?)<")    # every Gram-pass kernel (staged / marching / chunked / VALU)
 TRIAL = re.compile(r"k_gemv_vjpg<")                # the first Armijo trial + update products
 BENCH_GRID_MIN = 50e6                              # bytes: launches on the bench grid (not the 256^2 pre-warm)
 

@@ -14,7 +14,7 @@ import re
 import sys
 from collections import defaultdict
 
-GRAM = re.compile(r"k_gram_(?:[smw]p?|v1?)<")
+GRAM = re.compile(r"k_gram_(?:[smwqx]p?|v1?)<")
 
 
 def short(name):

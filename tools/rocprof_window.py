@@ -11,7 +11,7 @@ import json
 import re
 import sys
 
-GRAM = re.compile(r"k_gram_(?:[smw]p?|v1?)<")
+GRAM = re.compile(r"k_gram_(?:[smwqx]p?|v1?)<")
 TRIAL = re.compile(r"k_gemv_vjpg<")
 
 
