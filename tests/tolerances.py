@@ -89,8 +89,9 @@ ARMIJO_TIE_ULPS = 4.0
 # new count against the counts the reference's reordering family produces (last_nfev_values).  86 from round 4 (the
 # round-6 fixed decompositions kept every reduction's bits: tests/test_gpu_decomp.py) until round 6 moved the k = 19,
 # 20 Gram passes' lead-column sums onto 4x4x4 MFMA blocks (82, the family's most frequent count: 30 of its 70
-# reorderings), then the Gram passes from k = 8 onto the 4x4x4-block kernel k_gram_q: 83 since, the reference's own.
-DEVICE_LAST_NFEV = {"c2_res_old": 83}
+# reorderings; with k_gram_q from k = 10: 83, the reference's own), then every preconditioned Gram pass from k = 8
+# onto the 4x4x4-block kernel k_gram_q: 92 since (2 of the 70 reorderings).
+DEVICE_LAST_NFEV = {"c2_res_old": 92}
 
 
 def last_nfev_values(case):
