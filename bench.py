@@ -667,15 +667,15 @@ def main():
                        "trial": {**twindow, "launch_bytes": t_by}}, f)
     gram_share = sum(g_ms) * 1e-3 / elapsed_all if g_ms else float("nan")
     # per basis size: columns = bytes / (8 n_rank) - 2 (V, u, r); kernel as gnk_gram dispatches a pass
-    # with P^-1 and r: VALU k <= 7, staged on 4x4x4 blocks k = 8..20 (N % 128 == 0; else VALU one point per lane
+    # with P^-1 and r: VALU k <= 7, staged on 4x4x4 blocks k = 8..31 (N % 128 == 0; else VALU one point per lane
     # at 8, 9), chunked
     # k_gram_w up to 31 columns (+ r), the marching k_gram_x for 3..7 column blocks (N % 32 == 0; else the
     # chunked k_gram_w at 3 blocks and the prefetching k_gram_wp at 4), the pair-split k_gram beyond
     def gram_kernel(kk):
         if kk <= 7:
             return "k_gram_v"
-        if kk <= 20 and N % 128 == 0:
-            return "k_gram_q"                  # the 4x4x4-block staged pass (k_gram_s with GNK_TUNE_GRAM_Q 1)
+        if kk <= 31 and N % 128 == 0:
+            return "k_gram_q"                  # the 4x4x4-block staged pass (k_gram_s / k_gram_w with GNK_TUNE_GRAM_Q 1)
         if kk <= 9:
             return "k_gram_v1"
         if kk + 1 <= 32:

@@ -2781,6 +2781,7 @@ constexpr int GS_SW = 128;
 constexpr int GS_NW = 8;
 constexpr int GS_TM_MIN = 3;    // first tail (k - 16) whose lead-column sums run on 4x4x4 MFMA (k_gram_s TM)
 constexpr int GQ_KMIN = 8;      // first k of the 4x4x4-block staged Gram (k_gram_q)
+constexpr int GQ_KMAX = 31;     // last k of k_gram_q (8 column groups; above, the marching / chunked wide passes)
 constexpr int GS_KMAX = 20;     // V columns the staged kernel covers (k 21..24 would fit the LDS
                                 // ring but the two-block instance then spills past 256 VGPRs)
 
@@ -5163,7 +5164,16 @@ int gnk_gram(gnk_ctx* ctx, const double* u, const double* V, int64_t ldv, int k,
   // staged kernel (measured faster than the chunked / marching kernels for the preconditioned
   // pass from k = 4 up; the marching kernel stays faster for the plain pass);
   // tuning GNK_TUNE_GRAM_PATH 1 forces it for every pass (tests), 2 disables it
-  if (path != 2 && (path == 1 || (rinv && k >= 4)) && k <= GS_KMAX && ctx->geo.N % GS_SW == 0) {
+  // the 4x4x4-block pass (k_gram_q) instances: column groups x DMA instructions per wave and row
+  auto gq_inst = [](int ng, int L) {
+    return (ng == 2 && L <= 2) || (ng == 3 && L == 2) || (ng == 4 && (L == 2 || L == 3)) || (ng == 5 && L == 3) ||
+           (ng == 6 && (L == 3 || L == 4)) || (ng == 7 && L == 4) || (ng == 8 && (L == 4 || L == 5));
+  };
+  // preconditioned passes with k = 21..GQ_KMAX: k_gram_q too (4 ring slots, one workgroup per CU), instead of the
+  // chunked k_gram_w
+  const bool qwide = rinv && q_t != 1 && path != 2 && k > GS_KMAX && k <= GQ_KMAX &&
+                     gq_inst((k + 3) / 4, (k + 1 + (r ? 1 : 0) + 1 + GS_NW - 1) / GS_NW);
+  if (path != 2 && (path == 1 || (rinv && k >= 4)) && (k <= GS_KMAX || qwide) && ctx->geo.N % GS_SW == 0) {
     const int nbs = k <= 16 ? 1 : 2;                        // MFMA transform blocks of the V columns
     const int nrow = k + 1 + (r ? 1 : 0);
     const int L = (nrow + 1 + GS_NW - 1) / GS_NW;
@@ -5181,10 +5191,11 @@ int gnk_gram(gnk_ctx* ctx, const double* u, const double* V, int64_t ldv, int k,
     // 5 slots -- a row in flight across each barrier -- measured faster: profiles/round3/gram_eb.jsonl)
     int ring = nbs == 1 ? 4 : 5;
     if (ring_env == 4 || ring_env == 5) ring = ring_env;
+    if (k > GS_KMAX) ring = 4;
     if (ring_bytes(ring) > 160 * 1024) ring = 4;
     const size_t lds = ring_bytes(ring);
     const bool two_wg = lds <= half_lds;                      // 4 waves per SIMD: VGPRs capped at 128
-    if (L <= 4 && lds <= 160 * 1024) {
+    if ((L <= 4 || k > GS_KMAX) && lds <= 160 * 1024) {
       const double* rv = rinv ? rinv : ctx->ident + ident_offset(KP / 16);
       // 4-column k-steps of the last transform block
       const int ksl = ((k - 16 * (nbs - 1)) + 3) / 4;
@@ -5197,8 +5208,7 @@ int gnk_gram(gnk_ctx* ctx, const double* u, const double* V, int64_t ldv, int k,
       // above (4 slots up to 16 columns, 5 above); GNK_TUNE_GRAM_Q 1: never, 2: from k = 5 (k = 5..7 measured
       // 1.03-1.08 ms against the VALU kernel's 0.66-0.87)
       const int ng = (k + 3) / 4;
-      const bool qinst = (ng == 2 && L <= 2) || (ng == 3 && L == 2) || (ng == 4 && (L == 2 || L == 3)) ||
-                         (ng == 5 && L == 3);
+      const bool qinst = gq_inst(ng, L);
       const bool useq = q_t != 1 && k >= (q_t == 2 ? 5 : GQ_KMIN) && qinst &&
                         (ng == 5 || ring == 4);
       const int PL = useq ? gq_pl(ng) : 256 + 64 * nacc;
@@ -5252,6 +5262,9 @@ int gnk_gram(gnk_ctx* ctx, const double* u, const double* V, int64_t ldv, int k,
                      k, rv, KP, r, ctx->geo, ctx->coef, rpr, ctx->scratch, plog)
       if (useq) {
         if (ng == 5) { if (ring == 5) GRAMQ(5, 3, 5, 2); else GRAMQ(5, 3, 4, 2); }
+        else if (ng == 6) { if (L == 3) GRAMQ(6, 3, 4, 2); else GRAMQ(6, 4, 4, 2); }
+        else if (ng == 7) GRAMQ(7, 4, 4, 2);
+        else if (ng == 8) { if (L == 4) GRAMQ(8, 4, 4, 2); else GRAMQ(8, 5, 4, 2); }
         else if (ng == 2 && L == 1) { if (two_wg) GRAMQ(2, 1, 4, 4); else GRAMQ(2, 1, 4, 2); }
         else if (ng == 2) { if (two_wg) GRAMQ(2, 2, 4, 4); else GRAMQ(2, 2, 4, 2); }
         else if (ng == 3) { if (two_wg) GRAMQ(3, 2, 4, 4); else GRAMQ(3, 2, 4, 2); }

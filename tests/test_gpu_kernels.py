@@ -279,13 +279,18 @@ GRAM_CASES = [(24, 1, False, False), (24, 5, True, True), (100, 20, False, False
                                                   # two-block Gram at N % 128 != 0 (not the staged kernel), one
                                                   # 128-point strip, without r
                                                   (64, 17, True, True), (192, 20, True, True), (320, 18, False, False),
-                                                  (128, 19, False, True), (1024, 18, True, True)]
+                                                  (128, 19, False, True), (1024, 18, True, True),
+                                                  # k_gram_q's wide instances (k = 21..31, N % 128 == 0, with P^-1)
+                                                  (256, 21, True, True), (128, 24, True, True), (256, 27, True, True),
+                                                  (128, 29, True, True), (256, 31, True, True), (384, 26, False, True)]
 
 
 def _staged_modes(N, k):
     # "forced" / "ring5" only where the staged kernel applies (N % 128 == 0, k <= 20).  The 4x4x4-block form
     # (k_gram_q) is the default from k = 8: "noq" runs k_gram_s there instead, "v1" the one-point VALU kernel at
     # k = 8, 9, "valu" / "tm" k_gram_s's two lead-column forms at k = 17..20; "q" forces k_gram_q at k = 5..7
+    if N % 128 == 0 and 21 <= k <= 31:
+        return ("default", "noq")              # k_gram_q / the chunked k_gram_w
     if N % 128 != 0 or k > 20:
         return ("default",)
     modes = ("default", "forced", "ring5")
