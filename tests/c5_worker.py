@@ -5,7 +5,7 @@ C5 itself is Bratu 16384^2 with no restart (ref:gauss_newton_krylow.py:81-82: kr
 ref:krylow.py:72-73 appends a column per iteration) to k = 200: its basis is 201 x 2.15 GB = 429 GB, which
 needs the 8 GPUs' HBM.  Eight ranks sharing cuda:0 hold the same total, so the rehearsal runs the same
 algorithm at 8192^2 (V = 201 x 537 MB = 108 GB): every Gram kernel of the wide path in turn -- staged MFMA
-(k <= 20), chunked / prefetching (21..63), the marching wide pass (64..111) and the pair-split k_gram
+(k <= 31, the 4x4x4-block k_gram_q from k = 8), the marching wide pass (32..111) and the pair-split k_gram
 (112..200) -- with the (k+1)^2 Grams all-gathered and rank-summed, the host least-squares solve past the
 device solve's 32 columns, and the unfused trial / update kernels past the fused trial's 24 columns.
 Collectives go through slab.Comm's RCCL branches on the host-staged transport (tests/transport_shim.py);
@@ -14,8 +14,8 @@ grid.  Reported (rank 0 writes --out):
   * identical decisions and per-iteration scalars on every rank;
   * 8 ranks vs 1 rank, both with reduction segments (gnk_set_segments): nit / nrev / njev, per-iteration
     nfev and basis size, stdout; per-iteration ||x_k|| and ||r_k|| relative differences -- bit for bit while
-    the basis is on the segmented kernels (k <= 20), then differing by rounding: the wide Gram kernels
-    (k > 20) reduce over their own slab decomposition (the numbers are recorded, not asserted);
+    the basis is on the segmented kernels (k <= 31), then differing by rounding: the wide Gram kernels
+    (k > 31) reduce over their own slab decomposition (the numbers are recorded, not asserted);
   * the one-rank run's reference basis (sc_j V_j) orthonormal: max |V^T V - I| (gnk_flat_gemv_t);
   * seconds per run and the Gram pass per k (the one-rank run's HIP-event timer).
 

@@ -12,8 +12,8 @@
   ||r_k|| bit for bit (compensated CG scalars merged across ranks before rounding; the rest segmented).
 * C5 (configs[4]): Bratu 16384^2 with the basis growing without restart (krylow_restart 100,
   ref:gauss_newton_krylow.py:81-82, ref:krylow.py:72-73) to k = 99 -- through every Gram kernel of
-  the wide path: the staged MFMA pass (k <= 20), the chunked pass (k_gram_w, 21..47), the prefetching
-  pass (k_gram_wp, 48..63) and the marching wide pass (k_gram_x, 64..99; V = 101 x 2.15 GB = 217 GB).
+  the wide path: the staged MFMA pass (k <= 31; k_gram_q on 4x4x4 blocks from k = 8) and the marching wide
+  pass (k_gram_x, 32..99; V = 101 x 2.15 GB = 217 GB).
   k >= 112 (the pair-split k_gram, C5's range on 8 GPUs) is covered against the NumPy Gram at small N
   (tests/test_gpu_kernels.py::test_gram_mfma).  k = 200 does not fit one GPU
   (the basis alone is 429 GB); the full-size run is checked by properties:
@@ -75,8 +75,9 @@ def test_c5_k200_eight_ranks_on_one_gpu(tmp_path):
     (host-staged transport), then one rank over the whole grid.  Asserted: identical decisions on every rank
     and vs one rank (ref:krylow.py:72-73 grows the basis every iteration, ref:gauss_newton_krylow.py:81-82
     never restarts), per-iteration ||x_k|| / ||r_k|| bit for bit while the basis is on the segmented kernels
-    (iterations 1..20: iteration i solves on the k = i column basis, and from k = 21 the Gram pass is a wide kernel
-    that counts a segment fallback) and within 1e-12 after (the wide kernels reduce over their own slab
+    (iterations 1..31: iteration i solves on the k = i column basis, up to k = 31 with the segmented staged Gram
+    pass; from k = 32 the Gram pass is a wide kernel that counts a segment fallback) and within 1e-12 after (the
+    wide kernels reduce over their own slab
     decomposition), the one-rank reference basis orthonormal (max |V^T V - I| <= ORTH_TOL) and every accepted
     least-squares factor well conditioned (cond(R_Y) <= COND_ACCEPT, the threshold of a second CholeskyQR pass)."""
     out = tmp_path / "c5.json"
@@ -88,7 +89,7 @@ def test_c5_k200_eight_ranks_on_one_gpu(tmp_path):
     assert rep["ranks_identical"] and rep["bookkeeping_equal"]
     ex, er = np.array(rep["rel_xnorm_diff"]), np.array(rep["rel_rnorm_diff"])
     assert ex.size == er.size == 200
-    assert np.all(ex[:20] == 0.0) and np.all(er[:20] == 0.0), (ex[:20], er[:20])
+    assert np.all(ex[:31] == 0.0) and np.all(er[:31] == 0.0), (ex[:31], er[:31])
     assert ex.max() <= 1e-12 and er.max() <= 1e-12, (ex.max(), er.max())
     assert rep["single_max_abs_VtV_minus_I"] <= ORTH_TOL
     assert rep["max_cond_multi"] <= COND_ACCEPT and rep["max_cond_single"] <= COND_ACCEPT
