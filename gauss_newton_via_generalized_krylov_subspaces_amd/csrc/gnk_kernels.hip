@@ -3167,6 +3167,8 @@ __global__ __launch_bounds__(64 * GS_NW) __attribute__((amdgpu_waves_per_eu(WPE)
 // r stays on VALU (r . Y per lane column, r . r).  Per workgroup the lane partials are summed over the point
 // groups (and over the points, for r) in a fixed order before any reduction over workgroups, segments or ranks;
 // partial[tile][16 NP + 4 NG + 1] holds the group-pair 4x4 blocks, r . Y and r . r (k_gram_scatter_q).
+// Instances: 2..4 groups (k = 5..16) on the 4-slot ring, two workgroups per CU; 5 groups (k = 17..20) on 5 slots,
+// one per CU; 6..8 groups (k = 21..31, replacing the chunked k_gram_w there) on 4 slots, one per CU, 200-256 VGPRs.
 constexpr int gq_np(int ng) { return ng * (ng + 1) / 2; }
 constexpr int gq_pl(int ng) { return 16 * gq_np(ng) + 4 * ng + 1; }
 __host__ __device__ constexpr int gq_pair(int a, int c) { return c * (c + 1) / 2 + a; }   // a <= c
