@@ -2,6 +2,7 @@
     python tools/trial_dump.py TAG kk1,kk2,... [--grid N] [--reps R] [--tune key=value,...]
 prints one JSON line per width (median ms, GB/s of the k + 5 vectors it moves)."""
 import argparse
+import hashlib
 import json
 import os
 import sys
@@ -55,7 +56,9 @@ def main():
             ms.append(s.elapsed_time(e))
         med = float(np.median(ms))
         print(json.dumps({"tag": a.tag, "kk": kk, "grid": N, "ms": med, "GBs": 8.0 * n * (k + 5) / (med * 1e-3) / 1e9,
-                          "h0": float(h[0].item())}), flush=True)
+                          "h0": float(h[0].item()),
+                          "bits": hashlib.sha1(b"".join(t.cpu().numpy().tobytes() for t in (h[:kk], x[sl.own], gg[sl.own], st[:2])))
+                          .hexdigest()[:16]}), flush=True)
 
 
 if __name__ == "__main__":
